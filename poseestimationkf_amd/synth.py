@@ -1,0 +1,252 @@
+"""Synthetic IMU streams: host (NumPy) mirror of the device generator ``pekf_synth_dev``.
+
+The reference's input trace (``Sensor_CSV/KalmanFilter.txt``, read at
+Python Kalman Filter/ReadFile.py:24) was never committed, so every workload here
+is synthetic (SURVEY.md §8d "Synthetic inputs").  Each filter ``b`` owns a
+Philox4x32-10 stream keyed by ``(seed, b)`` with counter ``(step, slot, 0, 0)``,
+and every floating-point operation below is a single IEEE-754 correctly rounded
+op (+ - * / sqrt, no fused multiply-add), so this host mirror and the HIP kernel
+in ``csrc/pekf_synth.hip`` produce bit-identical streams.  Any shard can
+therefore regenerate any subset of filters on the host to check the GPU result.
+
+Per filter:
+  * reference vectors acc0 = normalise([0,0,1] + n), mag0 = normalise([cos60°,0,-sin60°] + n)
+    (the phone's initial calibration means, KFS/Parser.cpp:48-49), rounded to f32;
+  * true body rate w is AR(1): w <- 0.98 w + N(0, 0.3²) rad/s; the true attitude q is
+    advanced with the closed form of the RK4 step (body-frame rate, same convention as
+    ExtendedKalmanFilter.py:27-30);
+  * gyro = w + N(0, 0.02²); acc = normalise(R(q)^T acc0 + N(0,0.02²)); mag likewise;
+  * dt_ns ~ U{4e6 .. 2e7} (variable in every config); optional Bernoulli(0.3)
+    "magnetometer missing" flag (config 5) in bit 31 of the dt word.
+Noise is the sum of 4 uniforms (Irwin-Hall), rescaled to the stated sigma.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+DEFAULT_SEED = 20261015
+
+_MASK = np.uint64(0xFFFFFFFF)
+_PM0 = np.uint64(0xD2511F53)
+_PM1 = np.uint64(0xCD9E8D57)
+_PW0 = np.uint64(0x9E3779B9)
+_PW1 = np.uint64(0xBB67AE85)
+
+INIT_STEP = 0xFFFFFFFF        # counter word used for the per-filter reference vectors
+DT_MIN_NS = 4_000_000
+DT_SPAN_NS = 16_000_001       # dt_ns = DT_MIN_NS + x % DT_SPAN_NS  -> [4e6, 2e7]
+MISS_THRESH = 5_033_165       # (x >> 8) < 0.3 * 2^24
+MISSING_BIT = 0x80000000
+DT_MASK = 0x7FFFFFFF
+
+SQRT3 = 1.7320508075688772    # correctly rounded sqrt(3)
+SIN60 = 0.8660254037844386    # correctly rounded sqrt(3)/2
+
+
+@dataclass(frozen=True)
+class SynthParams:
+    """Noise levels and dynamics; the scales are passed verbatim to the device kernel."""
+    sigma_ref: float = 0.05
+    sigma_w: float = 0.3
+    sigma_gyro: float = 0.02
+    sigma_acc: float = 0.02
+    sigma_mag: float = 0.02
+    ar_w: float = 0.98
+
+    def scales(self):
+        """Irwin-Hall(4) has variance 1/3: scale = sqrt(3) * sigma (one rounding each)."""
+        return (SQRT3 * self.sigma_ref, SQRT3 * self.sigma_w, SQRT3 * self.sigma_gyro,
+                SQRT3 * self.sigma_acc, SQRT3 * self.sigma_mag)
+
+
+def philox4x32(c0, c1, c2, c3, k0, k1):
+    """Philox4x32-10 (Salmon et al., SC'11), vectorised; all inputs uint32-valued arrays."""
+    c0, c1, c2, c3, k0, k1 = (np.asarray(v, dtype=np.uint64) & _MASK for v in (c0, c1, c2, c3, k0, k1))
+    for rnd in range(10):
+        if rnd:
+            k0 = (k0 + _PW0) & _MASK
+            k1 = (k1 + _PW1) & _MASK
+        p0 = _PM0 * c0
+        p1 = _PM1 * c2
+        c0, c1, c2, c3 = ((p1 >> np.uint64(32)) ^ c1 ^ k0, p1 & _MASK,
+                          (p0 >> np.uint64(32)) ^ c3 ^ k1, p0 & _MASK)
+    return c0, c1, c2, c3
+
+
+def _noise(words, scale):
+    u = [(w >> np.uint64(8)).astype(np.float64) * (2.0 ** -24) for w in words]
+    return ((((u[0] + u[1]) + u[2]) + u[3]) - 2.0) * scale
+
+
+def _normalise3(x, y, z):
+    n = np.sqrt((x * x + y * y) + z * z)
+    return x / n, y / n, z / n
+
+
+def reference_vectors(ids, seed=DEFAULT_SEED, params=SynthParams()):
+    """Per-filter (acc0, mag0) as float64 arrays of shape (K,3) holding f32-representable values."""
+    ids = np.asarray(ids, dtype=np.uint64)
+    s_ref = params.scales()[0]
+    n = [_noise(philox4x32(INIT_STEP, s, 0, 0, seed, ids), s_ref) for s in range(6)]
+    a = _normalise3(0.0 + n[0], 0.0 + n[1], 1.0 + n[2])
+    m = _normalise3(0.5 + n[3], 0.0 + n[4], -SIN60 + n[5])
+    acc0 = np.stack([v.astype(np.float32) for v in a], axis=1).astype(np.float64)
+    mag0 = np.stack([v.astype(np.float32) for v in m], axis=1).astype(np.float64)
+    return acc0, mag0
+
+
+def _body(q, v):
+    """R(q)^T v for unit q = [w,x,y,z] mapping body -> world; columns of R dotted with v."""
+    w, x, y, z = q
+    r00 = 1.0 - 2.0 * (y * y + z * z)
+    r01 = 2.0 * (x * y - w * z)
+    r02 = 2.0 * (x * z + w * y)
+    r10 = 2.0 * (x * y + w * z)
+    r11 = 1.0 - 2.0 * (x * x + z * z)
+    r12 = 2.0 * (y * z - w * x)
+    r20 = 2.0 * (x * z - w * y)
+    r21 = 2.0 * (y * z + w * x)
+    r22 = 1.0 - 2.0 * (x * x + y * y)
+    return ((r00 * v[0] + r10 * v[1]) + r20 * v[2],
+            (r01 * v[0] + r11 * v[1]) + r21 * v[2],
+            (r02 * v[0] + r12 * v[1]) + r22 * v[2])
+
+
+def _measure(q, ref, words3, scale):
+    b = _body(q, ref)
+    a = [b[i] + _noise(words3[i], scale) for i in range(3)]
+    a = _normalise3(*a)
+    f = [v.astype(np.float32) for v in a]
+    # keep |z| < 1 and z != 0 in f32 so the Wahba weights |z|, 1-|z| never vanish
+    # (a vanishing weight makes B rank-1 and the reference's SVD rotation ill-defined)
+    big = np.abs(f[2]) >= np.float32(1.0)
+    f[2] = np.where(big, np.copysign(np.float32(0.99999994), f[2]), f[2])
+    f[2] = np.where(f[2] == np.float32(0.0), np.float32(1e-30), f[2]).astype(np.float32)
+    return f
+
+
+@dataclass
+class Records:
+    """Per-filter record view of a window: arrays indexed [step, filter, ...]."""
+    gyro: np.ndarray   # (W,K,3) float32
+    acc: np.ndarray    # (W,K,3) float32
+    mag: np.ndarray    # (W,K,3) float32
+    dtw: np.ndarray    # (W,K)   uint32: dt_ns | MISSING_BIT
+    acc0: np.ndarray   # (K,3)   float64
+    mag0: np.ndarray   # (K,3)   float64
+
+    @property
+    def dt_ns(self):
+        return (self.dtw & DT_MASK).astype(np.float64)
+
+    @property
+    def missing(self):
+        return (self.dtw & MISSING_BIT) != 0
+
+    def filter(self, k):
+        """(gyro, dt_ns, acc, mag) float64 arrays of filter column k, for the oracle."""
+        return (self.gyro[:, k].astype(np.float64), self.dt_ns[:, k],
+                self.acc[:, k].astype(np.float64), self.mag[:, k].astype(np.float64))
+
+
+def generate(ids, window, seed=DEFAULT_SEED, missing=False, params=SynthParams()):
+    """Generate `window` steps for the filters `ids` (host mirror of pekf_synth_dev)."""
+    ids = np.asarray(ids, dtype=np.uint64)
+    K = ids.shape[0]
+    acc0, mag0 = reference_vectors(ids, seed, params)
+    _, s_w, s_g, s_a, s_m = params.scales()
+    w = [np.zeros(K) for _ in range(3)]
+    q = [np.ones(K), np.zeros(K), np.zeros(K), np.zeros(K)]
+    gyro = np.empty((window, K, 3), np.float32)
+    acc = np.empty((window, K, 3), np.float32)
+    mag = np.empty((window, K, 3), np.float32)
+    dtw = np.empty((window, K), np.uint32)
+    a_ref = [acc0[:, i] for i in range(3)]
+    m_ref = [mag0[:, i] for i in range(3)]
+    for t in range(window):
+        ph = lambda slot: philox4x32(t, slot, 0, 0, seed, ids)  # noqa: E731
+        s0 = ph(0)
+        dt = np.uint64(DT_MIN_NS) + s0[0] % np.uint64(DT_SPAN_NS)
+        word = dt.astype(np.uint32)
+        if missing:
+            flag = (s0[1] >> np.uint64(8)) < np.uint64(MISS_THRESH)
+            word = np.where(flag, word | np.uint32(MISSING_BIT), word).astype(np.uint32)
+        dtw[t] = word
+        for i in range(3):
+            w[i] = params.ar_w * w[i] + _noise(ph(1 + i), s_w)
+        h = dt.astype(np.float64) * 1e-9
+        th2 = 0.25 * ((w[0] * w[0] + w[1] * w[1]) + w[2] * w[2])
+        x = (h * h) * th2
+        ca = (1.0 - x * 0.5) + (x * x) / 24.0
+        cb = h * (1.0 - x / 6.0)
+        r0 = 0.5 * ((-(w[0] * q[1]) - w[1] * q[2]) - w[2] * q[3])
+        r1 = 0.5 * ((w[0] * q[0] + w[2] * q[2]) - w[1] * q[3])
+        r2 = 0.5 * ((w[1] * q[0] - w[2] * q[1]) + w[0] * q[3])
+        r3 = 0.5 * ((w[2] * q[0] + w[1] * q[1]) - w[0] * q[2])
+        q = [ca * q[0] + cb * r0, ca * q[1] + cb * r1, ca * q[2] + cb * r2, ca * q[3] + cb * r3]
+        n = np.sqrt(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3])
+        q = [c / n for c in q]
+        for i in range(3):
+            gyro[t, :, i] = (w[i] + _noise(ph(4 + i), s_g)).astype(np.float32)
+        a = _measure(q, a_ref, [ph(7), ph(8), ph(9)], s_a)
+        m = _measure(q, m_ref, [ph(10), ph(11), ph(12)], s_m)
+        for i in range(3):
+            acc[t, :, i] = a[i]
+            mag[t, :, i] = m[i]
+    return Records(gyro, acc, mag, dtw, acc0, mag0)
+
+
+# ---------------------------------------------------------------------------------------------
+# HBM stream layout (see DESIGN.md "Data layout"): three planes per step, filter-minor.
+#   plane GD : float4 {gx, gy, gz, bits(dt word)}   [window][batch]
+#   plane AM : float4 {ax, ay, az, mx}              [window][batch]
+#   plane MY : float2 {my, mz}                      [window][batch]
+# 40 B per filter-step; a wavefront reads 1 KiB + 1 KiB + 512 B per step, fully coalesced.
+# ---------------------------------------------------------------------------------------------
+
+def pack_planes(rec: Records):
+    """Records -> (gd (W,K,4) f32, am (W,K,4) f32, my (W,K,2) f32) contiguous planes."""
+    W, K = rec.dtw.shape
+    gd = np.empty((W, K, 4), np.float32)
+    gd[..., :3] = rec.gyro
+    gd[..., 3] = rec.dtw.view(np.float32)
+    am = np.empty((W, K, 4), np.float32)
+    am[..., :3] = rec.acc
+    am[..., 3] = rec.mag[..., 0]
+    my = np.ascontiguousarray(rec.mag[..., 1:3])
+    return gd, am, my
+
+
+def unpack_planes(gd, am, my, acc0, mag0):
+    """Inverse of pack_planes (used to pull sampled filters back off the device)."""
+    gyro = np.ascontiguousarray(gd[..., :3])
+    dtw = np.ascontiguousarray(gd[..., 3]).view(np.uint32)
+    acc = np.ascontiguousarray(am[..., :3])
+    mag = np.concatenate([am[..., 3:4], my], axis=-1)
+    return Records(gyro, acc, mag, dtw, np.asarray(acc0, np.float64), np.asarray(mag0, np.float64))
+
+
+def refs_array(acc0, mag0):
+    """Per-filter constants block for the fused kernel: (K,6) float64 [acc0 xyz, mag0 xyz]."""
+    return np.ascontiguousarray(np.concatenate([acc0, mag0], axis=1), dtype=np.float64)
+
+
+def window_bytes(batch, window):
+    return int(batch) * int(window) * 40
+
+
+def c1_timestamps(dt_ns, t0_ns=1_234_567_890_123):
+    """Absolute ns timestamps for the single-filter log (config 1): T0 then cumulative sums."""
+    t = [float(t0_ns)]
+    acc = t0_ns
+    for d in np.asarray(dt_ns, dtype=np.int64):
+        acc += int(d)
+        t.append(float(acc))
+    return t
+
+
+__all__ = ["DEFAULT_SEED", "SynthParams", "Records", "philox4x32", "reference_vectors", "generate",
+           "pack_planes", "unpack_planes", "refs_array", "window_bytes", "c1_timestamps",
+           "MISSING_BIT", "DT_MASK"]
