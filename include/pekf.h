@@ -1,0 +1,149 @@
+/*
+ * pekf.h -- C ABI of libpekf.so, the MI355X (gfx950) batched quaternion-EKF engine.
+ *
+ * The reference exposes this path as a pure-Python module API with no FFI
+ * (SURVEY.md §8b).  Each entry point below replaces one reference interface; the
+ * Python drop-in modules (poseestimationkf_amd/dropin/) bind them with ctypes, exactly
+ * as a maintainer would bind them from the reference side.
+ * Paths are relative to "/root/reference/Python Kalman Filter/".
+ *
+ * Conventions
+ *   - Plain C types only: int64_t counts, double/float/uint32_t arrays, void* streams.
+ *   - Quaternions are [w, x, y, z]; 4x4 / 3x3 / 4x3 matrices are row-major.
+ *   - "_dev" entry points take DEVICE pointers and a hipStream_t (as void*, NULL =
+ *     the null stream) and only enqueue work.  The other batched entry points take
+ *     HOST pointers, stage through a pinned buffer, and return when results are on
+ *     the host.  All pointers are caller-owned and contiguous.
+ *   - Every entry returns a status (PEKF_OK = 0).  pekf_last_error() gives the
+ *     calling thread's message for the last failure.  No exceptions cross the ABI.
+ *   - There is no CPU fallback: without a usable gfx950 device every compute entry
+ *     returns PEKF_ERR_NODEVICE.
+ */
+#ifndef PEKF_H
+#define PEKF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PEKF_ABI_VERSION 1
+
+#define PEKF_OK 0
+#define PEKF_ERR_INVALID 1  /* bad argument (null pointer, negative size, ...)          */
+#define PEKF_ERR_HIP 2      /* HIP runtime error (message has hipGetErrorString)        */
+#define PEKF_ERR_SINGULAR 3 /* S = P + R singular in predict: np.linalg.LinAlgError      */
+#define PEKF_ERR_NODEVICE 4 /* no HIP device visible                                     */
+
+/* Bit 31 of a stream record's dt word: magnetometer sample missing ("Wahba-skip"). */
+#define PEKF_MISSING_MAG_BIT 0x80000000u
+
+int pekf_abi_version(void);
+const char *pekf_last_error(void);
+
+/* ---------------- device, memory, streams, events (host plumbing, no PyTorch) ---------------- */
+int pekf_device_count(int *count);
+int pekf_set_device(int device);
+int pekf_get_device(int *device);
+int pekf_device_name(int device, char *buf, int buflen); /* gcnArchName, e.g. "gfx950:sramecc+:xnack-" */
+int pekf_malloc(void **dptr, size_t bytes);
+int pekf_free(void *dptr);
+int pekf_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream);
+int pekf_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream);
+int pekf_memcpy_d2d(void *dst, const void *src, size_t bytes, void *stream);
+int pekf_memset(void *dst, int value, size_t bytes, void *stream);
+int pekf_stream_create(void **stream);
+int pekf_stream_destroy(void *stream);
+int pekf_stream_sync(void *stream);
+int pekf_device_sync(void);
+int pekf_event_create(void **event);
+int pekf_event_destroy(void *event);
+int pekf_event_record(void *event, void *stream);
+int pekf_event_sync(void *event);
+int pekf_event_elapsed_ms(float *ms, void *start, void *stop);
+
+/* ---------------- per-call operators (batched over n independent items) ----------------
+ * One GPU thread per item.  These are the drop-in replacements for the reference's
+ * per-timestep methods; at n = 1 they serve main_file.py through the Python shims. */
+
+/* KalmanFilter.RungeKutta4(q_0, T, w), ExtendedKalmanFilter.py:25-41.
+ * q0[n*4], dt_ns[n] (nanoseconds; dt = dt_ns * 1e-9 as at :32), w[n*3] -> q_out[n*4]. */
+int pekf_rk4(int64_t n, const double *q0, const double *dt_ns, const double *w, double *q_out);
+int pekf_rk4_dev(int64_t n, const double *q0, const double *dt_ns, const double *w, double *q_out,
+                 void *stream);
+
+/* UtilityFunctions.norm(a), UtilityFunctions.py:16-21: sqrt of the sequential sum of squares
+ * of each of n vectors of length len: a[n*len] -> out[n]. */
+int pekf_norm(int64_t n, int64_t len, const double *a, double *out);
+
+/* KalmanFilter.GetJacobian_A(w) -> 0.5*Omega(w) [n*16], ExtendedKalmanFilter.py:43-48 */
+int pekf_jacobian_a(int64_t n, const double *w, double *A);
+/* KalmanFilter.GetJacobian_B(q) -> 0.5*Xi(q) [n*12], ExtendedKalmanFilter.py:51-56 */
+int pekf_jacobian_b(int64_t n, const double *q, double *Jb);
+/* KalmanFilter.Comparator(q1, q2) -> conj(q1) (x) q2 [n*4], ExtendedKalmanFilter.py:16-23 */
+int pekf_comparator(int64_t n, const double *q1, const double *q2, double *out);
+
+/* KalmanFilter.Prediction(Gyro, T, X_k, P_k), ExtendedKalmanFilter.py:58-68, minus the
+ * previousT bookkeeping (:62,:67), which stays with the caller: dt_ns = T - previousT.
+ * gyro[n*3], dt_ns[n], X[n*4], P[n*16], Q[n*9], R[n*16] -> z[n*4], Pm[n*16], K[n*16].
+ * Returns PEKF_ERR_SINGULAR if any S = Pm + R is singular (the reference raises
+ * np.linalg.LinAlgError from np.linalg.inv, :65). */
+int pekf_predict(int64_t n, const double *gyro, const double *dt_ns, const double *X,
+                 const double *P, const double *Q, const double *R, double *z, double *Pm,
+                 double *K);
+int pekf_predict_dev(int64_t n, const double *gyro, const double *dt_ns, const double *X,
+                     const double *P, const double *Q, const double *R, double *z, double *Pm,
+                     double *K, int *dev_singular /* device int, may be NULL */, void *stream);
+
+/* KalmanFilter.Correction(Mag, Acc, z_k, P_k, K_k), ExtendedKalmanFilter.py:70-80, with the
+ * filter's Wahba reference vectors acc0/mag0 (Wahba.__init__, Wahba.py:4-6).
+ * mag[n*3], acc[n*3], z[n*4], P[n*16], K[n*16], acc0[n*3], mag0[n*3] -> X[n*4], P_out[n*16]. */
+int pekf_correct(int64_t n, const double *mag, const double *acc, const double *z,
+                 const double *P, const double *K, const double *acc0, const double *mag0,
+                 double *X, double *P_out);
+int pekf_correct_dev(int64_t n, const double *mag, const double *acc, const double *z,
+                     const double *P, const double *K, const double *acc0, const double *mag0,
+                     double *X, double *P_out, void *stream);
+
+/* Wahba.getRotation(acc, mag, k_acc, k_mag), Wahba.py:8-17 -> R[n*9] (closed form) */
+int pekf_wahba_rotation(int64_t n, const double *acc0, const double *mag0, const double *acc,
+                        const double *mag, const double *k_acc, const double *k_mag, double *R);
+/* Wahba.getQuarternion(acc, mag, k_acc, k_mag), Wahba.py:49-50 -> q[n*4] */
+int pekf_wahba_quaternion(int64_t n, const double *acc0, const double *mag0, const double *acc,
+                          const double *mag, const double *k_acc, const double *k_mag, double *q);
+/* Wahba.RotationMatrix2Quart(M), Wahba.py:19-47 -> q[n*4] (3-branch, strict '>', no trace branch) */
+int pekf_rotmat_to_quat(int64_t n, const double *M, double *q);
+
+/* ---------------- fused hot path: the whole main_file.py:38-47 loop on the device ----------------
+ * One lane per filter; each lane runs n_steps of Prediction + Correction with X and P in
+ * registers.  Step t of the launch reads stream row (step0 + t) % window:
+ *   plane_gd : float4 [window][batch] {gyro x, y, z, bits(dt word)}   dt word = dt_ns | flags
+ *   plane_am : float4 [window][batch] {acc x, y, z, mag x}
+ *   plane_my : float2 [window][batch] {mag y, z}
+ * refs[batch*6] = {acc0 xyz, mag0 xyz} (float64; KalmanFilter(T0, mag_0, acc_0), :6-11).
+ * X[batch*4], P[batch*16] (row-major, symmetric; the kernel reads the upper triangle) are
+ * read at launch start and written at the end.  q, r: setQ/setR scales (:12-15).
+ * A record whose dt word has PEKF_MISSING_MAG_BIT set runs Prediction only (X = z, P = P-).
+ * traj (optional, NULL to skip): X after every step, [n_steps][batch][4]. */
+int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
+                 const void *plane_gd, const void *plane_am, const void *plane_my,
+                 const double *refs, double *X, double *P, double q, double r, double *traj,
+                 void *stream);
+
+/* X = [1,0,0,0], P = I for every filter (main_file.py:23,26). */
+int pekf_reset_state_dev(int64_t batch, double *X, double *P, void *stream);
+
+/* ---------------- synthetic IMU streams (device mirror of poseestimationkf_amd/synth.py) --------
+ * Filters first_filter .. first_filter+batch-1, window steps, bit-identical to the host
+ * generator.  scales[5] = sqrt(3)*sigma for {ref, w, gyro, acc, mag}; ar_w = AR(1) factor.
+ * Writes the three planes ([window][batch]) and refs[batch*6]. */
+int pekf_synth_dev(int64_t batch, int64_t window, int64_t first_filter, uint32_t seed,
+                   int missing_mag, const double *scales, double ar_w, void *plane_gd,
+                   void *plane_am, void *plane_my, double *refs, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PEKF_H */

@@ -1,0 +1,68 @@
+// pekf_internal.hpp -- shared host-side plumbing of libpekf.so (error state, HIP checks,
+// the pinned/device staging workspace used by the host-pointer entry points).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <initializer_list>
+
+#include "../../include/pekf.h"
+
+namespace pekf {
+
+int set_error(int code, const char *fmt, ...);
+int hip_fail(hipError_t e, const char *what);
+int require_device();
+
+#define PEKF_HIP(call)                                                   \
+    do {                                                                 \
+        hipError_t e_ = (call);                                          \
+        if (e_ != hipSuccess) return ::pekf::hip_fail(e_, #call);        \
+    } while (0)
+
+#define PEKF_CHECK_ARG(cond, msg)                                        \
+    do {                                                                 \
+        if (!(cond)) return ::pekf::set_error(PEKF_ERR_INVALID, "%s", msg); \
+    } while (0)
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
+
+// One host<->device transfer in each direction for a host-pointer call: inputs are
+// packed into a pinned buffer, copied once, outputs copied back once.
+struct HostArg {
+    const void *ptr;
+    size_t bytes;
+};
+struct HostOut {
+    void *ptr;
+    size_t bytes;
+};
+
+class Staging {
+  public:
+    // Packs `ins` into device memory; returns device addresses for ins and outs.
+    // The caller enqueues its kernel on stream() between stage_in() and stage_out().
+    int stage_in(std::initializer_list<HostArg> ins, std::initializer_list<size_t> out_bytes,
+                 void **dev_in, void **dev_out);
+    int stage_out(std::initializer_list<HostOut> outs, void *const *dev_out);
+    hipStream_t stream() const { return stream_; }
+    int *dev_flag() const { return flag_; }
+    ~Staging();
+
+    static Staging &get();  // per calling thread, per current device
+  private:
+    int reserve(size_t bytes);
+    hipStream_t stream_ = nullptr;
+    char *dev_ = nullptr;
+    char *host_ = nullptr;
+    int *flag_ = nullptr;
+    size_t cap_ = 0;
+    size_t in_bytes_ = 0;
+    int device_ = -1;
+};
+
+}  // namespace pekf

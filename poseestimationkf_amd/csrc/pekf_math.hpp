@@ -1,0 +1,315 @@
+// pekf_math.hpp -- FP64 device math of the quaternion EKF (gfx950, one lane per filter).
+//
+// Two families:
+//  * literal building blocks that keep the reference's dense formulation, used by the
+//    per-call kernels behind the drop-in API (results agree with NumPy to ~1e-15);
+//  * the lane-resident forms used by the fused kernel, which exploit the algebra of the
+//    reference model to cut the FP64 work per step (DESIGN.md "Fused step algebra"):
+//      - 0.5*Omega(w) squares to -(|w|^2/4) I, so classical RK4 (ExtendedKalmanFilter.py:25-41)
+//        is exactly  q1 = (1 - x/2 + x^2/24) q + h (1 - x/6) 0.5*Omega(w) q,  x = h^2 |w|^2 / 4;
+//      - Xi(q) Xi(q)^T = |q|^2 I - q q^T, so Jb Q Jb^T = (q_scale/4)(|X|^2 I - X X^T) (:51-56,61);
+//      - S = P- + rI is SPD, K = P- S^-1 = I - r S^-1 and P- - K P- = r K (:63-66,78);
+//      - B (Wahba.py:11-13) has rank 2: its SVD rotation is R = Fw diag(P2, c) Fv^T with Fw, Fv
+//        the Gram-Schmidt frames of (acc0, mag0) and (acc, mag), P2 the orthogonal polar factor
+//        of the 2x2 core C = Fw^T B Fv and c = sign(det C) = sign(k_acc k_mag) (Wahba.py:14-16).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#define PEKF_DEV __device__ __forceinline__
+
+namespace pekf {
+
+constexpr double kNsToS = 1e-09;  // ExtendedKalmanFilter.py:32 (10**-9)
+
+// ------------------------------- literal (per-call) forms -------------------------------------
+
+// 0.5*Omega(w), ExtendedKalmanFilter.py:27-30 and :44-47
+PEKF_DEV void omega_half(const double *w, double *A) {
+    A[0] = 0.0;          A[1] = -0.5 * w[0];  A[2] = -0.5 * w[1];  A[3] = -0.5 * w[2];
+    A[4] = 0.5 * w[0];   A[5] = 0.0;          A[6] = 0.5 * w[2];   A[7] = -0.5 * w[1];
+    A[8] = 0.5 * w[1];   A[9] = -0.5 * w[2];  A[10] = 0.0;         A[11] = 0.5 * w[0];
+    A[12] = 0.5 * w[2];  A[13] = 0.5 * w[1];  A[14] = -0.5 * w[0]; A[15] = 0.0;
+}
+
+// 0.5*Xi(q), ExtendedKalmanFilter.py:52-55
+PEKF_DEV void xi_half(const double *q, double *J) {
+    J[0] = -0.5 * q[1];  J[1] = -0.5 * q[2];  J[2] = -0.5 * q[3];
+    J[3] = 0.5 * q[0];   J[4] = 0.5 * q[3];   J[5] = -0.5 * q[2];
+    J[6] = -0.5 * q[3];  J[7] = 0.5 * q[0];   J[8] = 0.5 * q[1];
+    J[9] = 0.5 * q[2];   J[10] = -0.5 * q[1]; J[11] = 0.5 * q[0];
+}
+
+template <int N, int K, int M>
+PEKF_DEV void matmul(const double *a, const double *b, double *c) {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            double s = 0.0;
+#pragma unroll
+            for (int t = 0; t < K; ++t) s += a[i * K + t] * b[t * M + j];
+            c[i * M + j] = s;
+        }
+}
+
+template <int N, int M>
+PEKF_DEV void transpose(const double *a, double *at) {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int j = 0; j < M; ++j) at[j * N + i] = a[i * M + j];
+}
+
+// UtilityFunctions.norm (UtilityFunctions.py:16-21): sequential sum of squares
+PEKF_DEV double loop_norm4(const double *a) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s += a[i] * a[i];
+    return sqrt(s);
+}
+
+// Classical 4-stage RK4 (ExtendedKalmanFilter.py:25-41)
+PEKF_DEV void rk4_literal(const double *q0, double dt_ns, const double *w, double *out) {
+    double W[16], k1[4], k2[4], k3[4], k4[4], t[4];
+    omega_half(w, W);
+    const double h = dt_ns * kNsToS;
+    matmul<4, 4, 1>(W, q0, k1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t[i] = q0[i] + h / 2 * k1[i];
+    matmul<4, 4, 1>(W, t, k2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t[i] = q0[i] + h / 2 * k2[i];
+    matmul<4, 4, 1>(W, t, k3);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t[i] = q0[i] + h * k3[i];
+    matmul<4, 4, 1>(W, t, k4);
+    const double c = 1.0 / 6.0 * h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = q0[i] + c * (k1[i] + 2 * k2[i] + 2 * k3[i] + k4[i]);
+    const double n = loop_norm4(out);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = out[i] / n;
+}
+
+// General 4x4 inverse by 2x2 cofactors (np.linalg.inv at ExtendedKalmanFilter.py:65).
+// Returns false iff the determinant is exactly zero (LinAlgError "Singular matrix").
+PEKF_DEV bool inverse4(const double *m, double *inv) {
+    const double s0 = m[0] * m[5] - m[4] * m[1];
+    const double s1 = m[0] * m[6] - m[4] * m[2];
+    const double s2 = m[0] * m[7] - m[4] * m[3];
+    const double s3 = m[1] * m[6] - m[5] * m[2];
+    const double s4 = m[1] * m[7] - m[5] * m[3];
+    const double s5 = m[2] * m[7] - m[6] * m[3];
+    const double c5 = m[10] * m[15] - m[14] * m[11];
+    const double c4 = m[9] * m[15] - m[13] * m[11];
+    const double c3 = m[9] * m[14] - m[13] * m[10];
+    const double c2 = m[8] * m[15] - m[12] * m[11];
+    const double c1 = m[8] * m[14] - m[12] * m[10];
+    const double c0 = m[8] * m[13] - m[12] * m[9];
+    const double det = s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0;
+    if (det == 0.0 || !isfinite(det)) return false;
+    const double id = 1.0 / det;
+    inv[0] = (m[5] * c5 - m[6] * c4 + m[7] * c3) * id;
+    inv[1] = (-m[1] * c5 + m[2] * c4 - m[3] * c3) * id;
+    inv[2] = (m[13] * s5 - m[14] * s4 + m[15] * s3) * id;
+    inv[3] = (-m[9] * s5 + m[10] * s4 - m[11] * s3) * id;
+    inv[4] = (-m[4] * c5 + m[6] * c2 - m[7] * c1) * id;
+    inv[5] = (m[0] * c5 - m[2] * c2 + m[3] * c1) * id;
+    inv[6] = (-m[12] * s5 + m[14] * s2 - m[15] * s1) * id;
+    inv[7] = (m[8] * s5 - m[10] * s2 + m[11] * s1) * id;
+    inv[8] = (m[4] * c4 - m[5] * c2 + m[7] * c0) * id;
+    inv[9] = (-m[0] * c4 + m[1] * c2 - m[3] * c0) * id;
+    inv[10] = (m[12] * s4 - m[13] * s2 + m[15] * s0) * id;
+    inv[11] = (-m[8] * s4 + m[9] * s2 - m[11] * s0) * id;
+    inv[12] = (-m[4] * c3 + m[5] * c1 - m[6] * c0) * id;
+    inv[13] = (m[0] * c3 - m[1] * c1 + m[2] * c0) * id;
+    inv[14] = (-m[12] * s3 + m[13] * s1 - m[14] * s0) * id;
+    inv[15] = (m[8] * s3 - m[9] * s1 + m[10] * s0) * id;
+    return true;
+}
+
+// Wahba.RotationMatrix2Quart (Wahba.py:19-47): 3 branches, strict '>' ties, no trace branch.
+// Evaluated without contraction and with true division: bit-identical to the reference
+// for the same M (tests/test_gpu_parity.py::test_r2q_bit_exact).
+PEKF_DEV void rotm_to_quat(const double *M, double *q) {
+#pragma clang fp contract(off)
+    const double t1 = ((1.0 + M[0]) - M[4]) - M[8];
+    const double t2 = ((1.0 - M[0]) + M[4]) - M[8];
+    const double t3 = ((1.0 - M[0]) - M[4]) + M[8];
+    if (t1 > t2 && t1 > t3) {
+        const double S = sqrt(t1) * 2.0;
+        q[0] = (M[7] - M[5]) / S; q[1] = 0.25 * S; q[2] = (M[1] + M[3]) / S; q[3] = (M[2] + M[6]) / S;
+    } else if (t2 > t1 && t2 > t3) {
+        const double S = sqrt(t2) * 2.0;
+        q[0] = (M[2] - M[6]) / S; q[1] = (M[1] + M[3]) / S; q[2] = 0.25 * S; q[3] = (M[5] + M[7]) / S;
+    } else {
+        const double S = sqrt(t3) * 2.0;
+        q[0] = (M[3] - M[1]) / S; q[1] = (M[2] + M[6]) / S; q[2] = (M[5] + M[7]) / S; q[3] = 0.25 * S;
+    }
+}
+
+// ------------------------------- Wahba closed form -------------------------------------------
+
+// Orthonormal frame of a vector pair (a, m): e1 = a/|a|, e2 = GramSchmidt(m), u3 = e1 x e2,
+// with the coordinates of a and m in it: a = alpha e1, m = beta1 e1 + beta2 e2.
+struct Frame {
+    double e1[3], e2[3], u3[3];
+    double alpha, beta1, beta2;
+};
+
+PEKF_DEV void make_frame(const double *a, const double *m, Frame &F) {
+    const double na = sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+    const double ia = 1.0 / na;
+    F.e1[0] = a[0] * ia; F.e1[1] = a[1] * ia; F.e1[2] = a[2] * ia;
+    const double b1 = F.e1[0] * m[0] + F.e1[1] * m[1] + F.e1[2] * m[2];
+    const double t0 = m[0] - b1 * F.e1[0], t1 = m[1] - b1 * F.e1[1], t2 = m[2] - b1 * F.e1[2];
+    const double nb = sqrt(t0 * t0 + t1 * t1 + t2 * t2);
+    const double ib = 1.0 / nb;
+    F.e2[0] = t0 * ib; F.e2[1] = t1 * ib; F.e2[2] = t2 * ib;
+    F.u3[0] = F.e1[1] * F.e2[2] - F.e1[2] * F.e2[1];
+    F.u3[1] = F.e1[2] * F.e2[0] - F.e1[0] * F.e2[2];
+    F.u3[2] = F.e1[0] * F.e2[1] - F.e1[1] * F.e2[0];
+    F.alpha = na;
+    F.beta1 = b1;
+    F.beta2 = nb;
+}
+
+// R = argmax_{R in SO(3)} tr(R^T B), B = ka acc0 acc^T + km mag0 mag^T (Wahba.py:8-17):
+// W = frame of the reference pair (acc0, mag0), V = frame of the current pair (acc, mag).
+PEKF_DEV void wahba_rotation(const Frame &W, const Frame &V, double ka, double km, double *R) {
+    const double c00 = ka * W.alpha * V.alpha + km * W.beta1 * V.beta1;
+    const double c01 = km * W.beta1 * V.beta2;
+    const double c10 = km * W.beta2 * V.beta1;
+    const double c11 = km * W.beta2 * V.beta2;
+    // det C = ka km alpha_W alpha_V beta2_W beta2_V exactly; alpha, beta2 >= 0
+    const bool proper = ka * km >= 0.0;
+    double p, s;
+    if (proper) { p = c00 + c11; s = c10 - c01; }
+    else        { p = c00 - c11; s = c01 + c10; }
+    const double ih = 1.0 / sqrt(p * p + s * s);
+    p *= ih;
+    s *= ih;
+    // P2 = [[p, -s], [s, p]] (rotation) or [[p, s], [s, -p]] (reflection); c = +1 / -1
+    const double p00 = p, p01 = proper ? -s : s, p10 = s, p11 = proper ? p : -p;
+    const double c = proper ? 1.0 : -1.0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double g0 = W.e1[i] * p00 + W.e2[i] * p10;
+        const double g1 = W.e1[i] * p01 + W.e2[i] * p11;
+        const double g2 = c * W.u3[i];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) R[i * 3 + j] = g0 * V.e1[j] + g1 * V.e2[j] + g2 * V.u3[j];
+    }
+}
+
+PEKF_DEV void wahba_rotation_vectors(const double *acc0, const double *mag0, const double *acc,
+                                     const double *mag, double ka, double km, double *R) {
+    Frame W, V;
+    make_frame(acc0, mag0, W);
+    make_frame(acc, mag, V);
+    wahba_rotation(W, V, ka, km, R);
+}
+
+// ------------------------------- fused-step forms --------------------------------------------
+
+// Symmetric 4x4 stored as its upper triangle: 00 01 02 03 11 12 13 22 23 33
+struct Sym4 {
+    double a00, a01, a02, a03, a11, a12, a13, a22, a23, a33;
+};
+
+// P- = 0.25 * Omega(w) P Omega(w)^T + (qs/4) (|x|^2 I - x x^T)   (ExtendedKalmanFilter.py:61)
+PEKF_DEV Sym4 propagate_cov(const Sym4 &P, const double *w, const double *x, double qs) {
+    const double w0 = w[0], w1 = w[1], w2 = w[2];
+    // T = Omega P (full 4x4), rows of Omega: [0,-w0,-w1,-w2] [w0,0,w2,-w1] [w1,-w2,0,w0] [w2,w1,-w0,0]
+    const double p[4][4] = {{P.a00, P.a01, P.a02, P.a03},
+                            {P.a01, P.a11, P.a12, P.a13},
+                            {P.a02, P.a12, P.a22, P.a23},
+                            {P.a03, P.a13, P.a23, P.a33}};
+    double T[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        T[0][j] = -w0 * p[1][j] - w1 * p[2][j] - w2 * p[3][j];
+        T[1][j] = w0 * p[0][j] + w2 * p[2][j] - w1 * p[3][j];
+        T[2][j] = w1 * p[0][j] - w2 * p[1][j] + w0 * p[3][j];
+        T[3][j] = w2 * p[0][j] + w1 * p[1][j] - w0 * p[2][j];
+    }
+    // M = T Omega^T: M_ij = T_i . Omega_j
+    auto m = [&](int i, int j) -> double {
+        switch (j) {
+            case 0: return -w0 * T[i][1] - w1 * T[i][2] - w2 * T[i][3];
+            case 1: return w0 * T[i][0] + w2 * T[i][2] - w1 * T[i][3];
+            case 2: return w1 * T[i][0] - w2 * T[i][1] + w0 * T[i][3];
+            default: return w2 * T[i][0] + w1 * T[i][1] - w0 * T[i][2];
+        }
+    };
+    const double n2 = x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
+    const double g = 0.25 * qs;
+    Sym4 o;
+    o.a00 = 0.25 * m(0, 0) + g * (n2 - x[0] * x[0]);
+    o.a01 = 0.25 * m(0, 1) - g * (x[0] * x[1]);
+    o.a02 = 0.25 * m(0, 2) - g * (x[0] * x[2]);
+    o.a03 = 0.25 * m(0, 3) - g * (x[0] * x[3]);
+    o.a11 = 0.25 * m(1, 1) + g * (n2 - x[1] * x[1]);
+    o.a12 = 0.25 * m(1, 2) - g * (x[1] * x[2]);
+    o.a13 = 0.25 * m(1, 3) - g * (x[1] * x[3]);
+    o.a22 = 0.25 * m(2, 2) + g * (n2 - x[2] * x[2]);
+    o.a23 = 0.25 * m(2, 3) - g * (x[2] * x[3]);
+    o.a33 = 0.25 * m(3, 3) + g * (n2 - x[3] * x[3]);
+    return o;
+}
+
+// Inverse of an SPD 4x4 by LDL^T (no pivoting needed: S = P- + rI, r > 0).
+PEKF_DEV Sym4 spd_inverse(const Sym4 &S) {
+    const double d0 = S.a00, i0 = 1.0 / d0;
+    const double l10 = S.a01 * i0, l20 = S.a02 * i0, l30 = S.a03 * i0;
+    const double d1 = S.a11 - l10 * S.a01, i1 = 1.0 / d1;
+    const double a21 = S.a12 - l20 * S.a01, a31 = S.a13 - l30 * S.a01;
+    const double l21 = a21 * i1, l31 = a31 * i1;
+    const double d2 = S.a22 - l20 * S.a02 - l21 * a21, i2 = 1.0 / d2;
+    const double a32 = S.a23 - l30 * S.a02 - l31 * a21;
+    const double l32 = a32 * i2;
+    const double d3 = S.a33 - l30 * S.a03 - l31 * a31 - l32 * a32, i3 = 1.0 / d3;
+    // N = L^-1 (unit lower)
+    const double n10 = -l10;
+    const double n21 = -l21, n20 = -(l20 + l21 * n10);
+    const double n32 = -l32, n31 = -(l31 + l32 * n21), n30 = -(l30 + l31 * n10 + l32 * n20);
+    // S^-1 = N^T D^-1 N
+    Sym4 o;
+    o.a33 = i3;
+    o.a23 = n32 * i3;
+    o.a22 = i2 + n32 * n32 * i3;
+    o.a13 = n31 * i3;
+    o.a12 = n21 * i2 + n31 * n32 * i3;
+    o.a11 = i1 + n21 * n21 * i2 + n31 * n31 * i3;
+    o.a03 = n30 * i3;
+    o.a02 = n20 * i2 + n30 * n32 * i3;
+    o.a01 = n10 * i1 + n20 * n21 * i2 + n30 * n31 * i3;
+    o.a00 = i0 + n10 * n10 * i1 + n20 * n20 * i2 + n30 * n30 * i3;
+    return o;
+}
+
+// Closed form of the classical RK4 step + normalisation (ExtendedKalmanFilter.py:25-41).
+PEKF_DEV void rk4_closed(const double *x, double dt_ns, const double *w, double *z) {
+    const double h = dt_ns * kNsToS;
+    const double th2 = 0.25 * (w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    const double xx = (h * h) * th2;
+    const double ca = 1.0 - 0.5 * xx + xx * xx * (1.0 / 24.0);
+    const double cb = 0.5 * h * (1.0 - xx * (1.0 / 6.0));
+    // Omega(w) x
+    const double o0 = -w[0] * x[1] - w[1] * x[2] - w[2] * x[3];
+    const double o1 = w[0] * x[0] + w[2] * x[2] - w[1] * x[3];
+    const double o2 = w[1] * x[0] - w[2] * x[1] + w[0] * x[3];
+    const double o3 = w[2] * x[0] + w[1] * x[1] - w[0] * x[2];
+    z[0] = ca * x[0] + cb * o0;
+    z[1] = ca * x[1] + cb * o1;
+    z[2] = ca * x[2] + cb * o2;
+    z[3] = ca * x[3] + cb * o3;
+    const double in = 1.0 / sqrt(z[0] * z[0] + z[1] * z[1] + z[2] * z[2] + z[3] * z[3]);
+    z[0] *= in; z[1] *= in; z[2] *= in; z[3] *= in;
+}
+
+}  // namespace pekf

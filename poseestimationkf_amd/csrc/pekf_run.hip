@@ -1,0 +1,178 @@
+// pekf_run.hip -- the fused hot path: main_file.py:38-47 (Prediction + Correction per record)
+// for a whole batch of independent filters, n_steps records per launch.
+//
+// Mapping (DESIGN.md "Kernel"): one LANE owns one filter, so a wavefront advances 64
+// filters in lock-step and every per-step input field is a coalesced 1 KiB (float4) or
+// 512 B (float2) wave load from the filter-minor planes.  X (4 f64), the symmetric P
+// (10 f64) and the filter's Wahba reference frame live in VGPRs for the whole launch;
+// HBM traffic is the 40 B/filter-step input record plus, once per launch, the state
+// and reference vectors.  The next step's record is loaded before the current step's
+// arithmetic so its latency hides under ~600 FP64 instructions of work.
+// No MFMA: every contraction is 4x4 / 3x3 per lane.
+#include "pekf_internal.hpp"
+#include "pekf_math.hpp"
+
+namespace pekf {
+
+constexpr int kRunBlock = 256;
+
+struct Rec {
+    float4 gd;  // gx, gy, gz, bits(dt word)
+    float4 am;  // ax, ay, az, mx
+    float2 my;  // my, mz
+};
+
+__device__ __forceinline__ Rec load_rec(const float4 *__restrict__ gd, const float4 *__restrict__ am,
+                                        const float2 *__restrict__ my, int64_t idx) {
+    Rec r;
+    r.gd = gd[idx];
+    r.am = am[idx];
+    r.my = my[idx];
+    return r;
+}
+
+template <bool TRAJ>
+__global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_steps, int64_t window,
+                                                   int64_t step0, const float4 *__restrict__ gd,
+                                                   const float4 *__restrict__ am,
+                                                   const float2 *__restrict__ my,
+                                                   const double *__restrict__ refs,
+                                                   double *__restrict__ Xio, double *__restrict__ Pio,
+                                                   double qs, double rs, double *__restrict__ traj) {
+    const int64_t b = (int64_t)blockIdx.x * kRunBlock + threadIdx.x;
+    if (b >= batch) return;
+
+    // per-filter constants: the Wahba reference frame of (acc0, mag0) (Wahba.py:4-6)
+    Frame Wf;
+    {
+        const double a0[3] = {refs[6 * b + 0], refs[6 * b + 1], refs[6 * b + 2]};
+        const double m0[3] = {refs[6 * b + 3], refs[6 * b + 4], refs[6 * b + 5]};
+        make_frame(a0, m0, Wf);
+    }
+    double x[4] = {Xio[4 * b + 0], Xio[4 * b + 1], Xio[4 * b + 2], Xio[4 * b + 3]};
+    const double *pp = Pio + 16 * b;
+    Sym4 P = {pp[0], pp[1], pp[2], pp[3], pp[5], pp[6], pp[7], pp[10], pp[11], pp[15]};
+
+    int64_t row = step0 % window;
+    Rec cur = load_rec(gd, am, my, row * batch + b);
+    for (int64_t t = 0; t < n_steps; ++t) {
+        // prefetch the next record (wraps around the resident window)
+        int64_t nrow = row + 1 == window ? 0 : row + 1;
+        Rec nxt;
+        if (t + 1 < n_steps) nxt = load_rec(gd, am, my, nrow * batch + b);
+
+        const double w[3] = {cur.gd.x, cur.gd.y, cur.gd.z};
+        const uint32_t word = __float_as_uint(cur.gd.w);
+        const double dt_ns = (double)(word & 0x7FFFFFFFu);
+
+        // ---- Prediction (ExtendedKalmanFilter.py:58-68) ----
+        const Sym4 Pm = propagate_cov(P, w, x, qs);  // Jb from the prior X (:60)
+        double z[4];
+        rk4_closed(x, dt_ns, w, z);                  // (:62)
+
+        if (word & PEKF_MISSING_MAG_BIT) {
+            // Wahba-skip: no Correction for this record (X = z, P = P-)
+            x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
+            P = Pm;
+        } else {
+            const Sym4 S = {Pm.a00 + rs, Pm.a01, Pm.a02, Pm.a03, Pm.a11 + rs,
+                            Pm.a12, Pm.a13, Pm.a22 + rs, Pm.a23, Pm.a33 + rs};
+            const Sym4 Si = spd_inverse(S);
+            // K = P- S^-1 = I - r S^-1 (symmetric)      (:63-66)
+            const Sym4 K = {1.0 - rs * Si.a00, -rs * Si.a01, -rs * Si.a02, -rs * Si.a03,
+                            1.0 - rs * Si.a11, -rs * Si.a12, -rs * Si.a13,
+                            1.0 - rs * Si.a22, -rs * Si.a23, 1.0 - rs * Si.a33};
+
+            // ---- Correction (ExtendedKalmanFilter.py:70-80) ----
+            const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
+            const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
+            const double ka = fabs(acc[2]);            // (:71)
+            Frame Vf;
+            make_frame(acc, mag, Vf);
+            double R[9], y[4];
+            wahba_rotation(Wf, Vf, ka, 1.0 - ka, R);   // Wahba.py:8-17
+            rotm_to_quat(R, y);                         // Wahba.py:19-47
+            const double cmp = y[0] * z[0] + y[1] * z[1] + y[2] * z[2] + y[3] * z[3];
+            const double sg = cmp < 0.0 ? -1.0 : 1.0;   // (:73-75)
+            const double e0 = sg * y[0] - z[0], e1 = sg * y[1] - z[1];
+            const double e2 = sg * y[2] - z[2], e3 = sg * y[3] - z[3];
+            // X = z + K e (:77), normalised (:79)
+            const double x0 = z[0] + K.a00 * e0 + K.a01 * e1 + K.a02 * e2 + K.a03 * e3;
+            const double x1 = z[1] + K.a01 * e0 + K.a11 * e1 + K.a12 * e2 + K.a13 * e3;
+            const double x2 = z[2] + K.a02 * e0 + K.a12 * e1 + K.a22 * e2 + K.a23 * e3;
+            const double x3 = z[3] + K.a03 * e0 + K.a13 * e1 + K.a23 * e2 + K.a33 * e3;
+            const double in = 1.0 / sqrt(x0 * x0 + x1 * x1 + x2 * x2 + x3 * x3);
+            x[0] = x0 * in; x[1] = x1 * in; x[2] = x2 * in; x[3] = x3 * in;
+            // P = P- - K P- = r K (:78)
+            P = {rs * K.a00, rs * K.a01, rs * K.a02, rs * K.a03, rs * K.a11,
+                 rs * K.a12, rs * K.a13, rs * K.a22, rs * K.a23, rs * K.a33};
+        }
+        if (TRAJ) {
+            double2 *o = reinterpret_cast<double2 *>(traj + (t * batch + b) * 4);
+            o[0] = make_double2(x[0], x[1]);
+            o[1] = make_double2(x[2], x[3]);
+        }
+        cur = nxt;
+        row = nrow;
+    }
+    Xio[4 * b + 0] = x[0]; Xio[4 * b + 1] = x[1]; Xio[4 * b + 2] = x[2]; Xio[4 * b + 3] = x[3];
+    double *po = Pio + 16 * b;
+    po[0] = P.a00; po[1] = P.a01; po[2] = P.a02; po[3] = P.a03;
+    po[4] = P.a01; po[5] = P.a11; po[6] = P.a12; po[7] = P.a13;
+    po[8] = P.a02; po[9] = P.a12; po[10] = P.a22; po[11] = P.a23;
+    po[12] = P.a03; po[13] = P.a13; po[14] = P.a23; po[15] = P.a33;
+}
+
+__global__ __launch_bounds__(kRunBlock) void k_reset(int64_t batch, double *X, double *P) {
+    const int64_t b = (int64_t)blockIdx.x * kRunBlock + threadIdx.x;
+    if (b >= batch) return;
+    X[4 * b] = 1.0; X[4 * b + 1] = 0.0; X[4 * b + 2] = 0.0; X[4 * b + 3] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) P[16 * b + k] = (k % 5 == 0) ? 1.0 : 0.0;
+}
+
+}  // namespace pekf
+
+using namespace pekf;
+
+extern "C" {
+
+int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
+                 const void *plane_gd, const void *plane_am, const void *plane_my,
+                 const double *refs, double *X, double *P, double q, double r, double *traj,
+                 void *stream) {
+    PEKF_CHECK_ARG(batch >= 0 && n_steps >= 0, "negative size");
+    if (batch == 0 || n_steps == 0) return PEKF_OK;
+    PEKF_CHECK_ARG(window > 0 && step0 >= 0, "window must be > 0 and step0 >= 0");
+    PEKF_CHECK_ARG(plane_gd && plane_am && plane_my && refs && X && P, "null pointer");
+    PEKF_CHECK_ARG(((uintptr_t)plane_gd % 16 == 0) && ((uintptr_t)plane_am % 16 == 0) &&
+                       ((uintptr_t)plane_my % 8 == 0) && ((uintptr_t)traj % 16 == 0),
+                   "misaligned plane / traj pointer");
+    PEKF_CHECK_ARG(r > 0.0, "r must be > 0 (S = P- + rI must be SPD)");
+    const dim3 grid(grid_for(batch, kRunBlock)), block(kRunBlock);
+    const auto *gd = static_cast<const float4 *>(plane_gd);
+    const auto *am = static_cast<const float4 *>(plane_am);
+    const auto *my = static_cast<const float2 *>(plane_my);
+    if (traj)
+        hipLaunchKernelGGL(k_run<true>, grid, block, 0, as_stream(stream), batch, n_steps, window,
+                           step0, gd, am, my, refs, X, P, q, r, traj);
+    else
+        hipLaunchKernelGGL(k_run<false>, grid, block, 0, as_stream(stream), batch, n_steps, window,
+                           step0, gd, am, my, refs, X, P, q, r, nullptr);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "k_run");
+    return PEKF_OK;
+}
+
+int pekf_reset_state_dev(int64_t batch, double *X, double *P, void *stream) {
+    PEKF_CHECK_ARG(batch >= 0, "negative size");
+    if (batch == 0) return PEKF_OK;
+    PEKF_CHECK_ARG(X && P, "null pointer");
+    hipLaunchKernelGGL(k_reset, dim3(grid_for(batch, kRunBlock)), dim3(kRunBlock), 0,
+                       as_stream(stream), batch, X, P);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "k_reset");
+    return PEKF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,50 @@
+"""Drop-in for the reference module ``ExtendedKalmanFilter`` (Python Kalman Filter/ExtendedKalmanFilter.py).
+
+``KalmanFilter`` keeps the reference's constructor, attributes (previousT, wahba, Q, R,
+eps), methods and return tuples, so ``main_file.py`` runs unchanged against it.  X, P, z
+and K are caller-owned values: every call returns fresh arrays and never mutates its
+inputs (main_file.py:39-44 keeps the returned X in a list).  The arithmetic runs in the
+per-call gfx950 kernels of libpekf.so (k_predict, k_correct, k_rk4, ...).  For many
+filters at once use ``poseestimationkf_amd.engine.BatchedEKF`` (the fused kernel).
+"""
+import numpy as np
+from _bootstrap import engine as _eng
+from Wahba import Wahba
+
+
+class KalmanFilter:
+    def __init__(self, T0, mag_0, acc_0, eps):          # ExtendedKalmanFilter.py:6-11
+        self.previousT = T0
+        self.wahba = Wahba(acc_0, mag_0)
+        self.Q = np.identity(3)
+        self.R = np.identity(4)
+        self.eps = eps
+
+    def setQ(self, q):                                   # :12-13
+        self.Q *= q
+
+    def setR(self, r):                                   # :14-15
+        self.R *= r
+
+    def Comparator(self, q1, q2):                        # :16-23
+        return _eng.comparator(q1, q2)[0]
+
+    @staticmethod
+    def RungeKutta4(q_0, T, w):                          # :25-41 (T in ns)
+        return _eng.rk4(q_0, T, w)[0]
+
+    def GetJacobian_A(self, w):                          # :43-48
+        return _eng.jacobian_a(w)[0]
+
+    def GetJacobian_B(self, q):                          # :51-56
+        return _eng.jacobian_b(q)[0]
+
+    def Prediction(self, Gyro, T, X_k, P_k):             # :58-68
+        dt = T - self.previousT                          # same float64 op as :62
+        z, P, K = _eng.predict(Gyro, dt, X_k, P_k, self.Q, self.R)   # LinAlgError if S singular
+        self.previousT = T                               # :67, only after a successful step
+        return z[0], P[0], K[0]
+
+    def Correction(self, Mag, Acc, z_k, P_k, K_k):       # :70-80
+        X, P = _eng.correct(Mag, Acc, z_k, P_k, K_k, self.wahba.w_initial_acc, self.wahba.w_initial_mag)
+        return X[0], P[0]

@@ -1,0 +1,302 @@
+"""Host side of the batched engine: device buffers, resident IMU windows, fused runs.
+
+Everything here is plumbing around the C ABI (include/pekf.h); all arithmetic of the
+filter runs in the HIP kernels of libpekf.so.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import synth
+from ._lib import check, dptr, f64, lib
+
+
+# ------------------------------------------------------------------ device plumbing
+
+class DeviceBuffer:
+    """A raw hipMalloc allocation owned by Python."""
+
+    def __init__(self, nbytes):
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        check(lib.pekf_malloc(ctypes.byref(p), max(1, self.nbytes)))
+        self.ptr = p.value
+
+    def upload(self, arr, stream=None):
+        a = np.ascontiguousarray(arr)
+        assert a.nbytes <= self.nbytes, (a.nbytes, self.nbytes)
+        check(lib.pekf_memcpy_h2d(self.ptr, a.ctypes.data, a.nbytes, stream))
+        return self
+
+    def download(self, shape, dtype, stream=None, offset=0):
+        out = np.empty(shape, dtype)
+        assert offset + out.nbytes <= self.nbytes
+        check(lib.pekf_memcpy_d2h(out.ctypes.data, self.ptr + offset, out.nbytes, stream))
+        return out
+
+    def free(self):
+        if getattr(self, "ptr", None):
+            lib.pekf_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Stream:
+    def __init__(self):
+        s = ctypes.c_void_p()
+        check(lib.pekf_stream_create(ctypes.byref(s)))
+        self.handle = s.value
+
+    def sync(self):
+        check(lib.pekf_stream_sync(self.handle))
+
+    def __del__(self):
+        try:
+            if self.handle:
+                lib.pekf_stream_destroy(self.handle)
+        except Exception:
+            pass
+
+
+class Event:
+    def __init__(self):
+        e = ctypes.c_void_p()
+        check(lib.pekf_event_create(ctypes.byref(e)))
+        self.handle = e.value
+
+    def record(self, stream=None):
+        check(lib.pekf_event_record(self.handle, stream))
+
+    def sync(self):
+        check(lib.pekf_event_sync(self.handle))
+
+    def elapsed_ms(self, end):
+        ms = ctypes.c_float()
+        check(lib.pekf_event_elapsed_ms(ctypes.byref(ms), self.handle, end.handle))
+        return ms.value
+
+    def __del__(self):
+        try:
+            if self.handle:
+                lib.pekf_event_destroy(self.handle)
+        except Exception:
+            pass
+
+
+def set_device(dev):
+    check(lib.pekf_set_device(int(dev)))
+
+
+def device_name(dev=0):
+    buf = ctypes.create_string_buffer(128)
+    check(lib.pekf_device_name(int(dev), buf, 128))
+    return buf.value.decode()
+
+
+# ------------------------------------------------------------------ resident IMU window
+
+class IMUWindow:
+    """`window` steps x `batch` filters of the 40 B/step input record, resident in HBM.
+
+    Planes (filter-minor, see synth.pack_planes): gd float4, am float4, my float2, plus the
+    per-filter reference block refs (batch, 6) float64.  Either uploaded from host records or
+    generated on the device with the bit-identical Philox generator (pekf_synth_dev).
+    """
+
+    def __init__(self, batch, window):
+        self.batch, self.window = int(batch), int(window)
+        n = self.batch * self.window
+        self.gd = DeviceBuffer(16 * n)
+        self.am = DeviceBuffer(16 * n)
+        self.my = DeviceBuffer(8 * n)
+        self.refs = DeviceBuffer(48 * self.batch)
+
+    @property
+    def nbytes(self):
+        return self.gd.nbytes + self.am.nbytes + self.my.nbytes
+
+    @classmethod
+    def from_records(cls, rec: synth.Records):
+        W, K = rec.dtw.shape
+        win = cls(K, W)
+        gd, am, my = synth.pack_planes(rec)
+        win.gd.upload(gd)
+        win.am.upload(am)
+        win.my.upload(my)
+        win.refs.upload(synth.refs_array(rec.acc0, rec.mag0))
+        return win
+
+    @classmethod
+    def from_planes(cls, gd, am, my, acc0, mag0):
+        W, K = gd.shape[:2]
+        win = cls(K, W)
+        win.gd.upload(np.ascontiguousarray(gd, np.float32))
+        win.am.upload(np.ascontiguousarray(am, np.float32))
+        win.my.upload(np.ascontiguousarray(my, np.float32))
+        win.refs.upload(synth.refs_array(acc0, mag0))
+        return win
+
+    def synthesize(self, seed=synth.DEFAULT_SEED, first_filter=0, missing=False,
+                   params=synth.SynthParams(), stream=None):
+        sc = np.array(params.scales(), dtype=np.float64)
+        check(lib.pekf_synth_dev(self.batch, self.window, int(first_filter), int(seed) & 0xFFFFFFFF,
+                                 1 if missing else 0, dptr(sc), float(params.ar_w), self.gd.ptr,
+                                 self.am.ptr, self.my.ptr, self.refs.ptr, stream))
+        if stream is None:
+            check(lib.pekf_device_sync())
+        return self
+
+    def download_filters(self, cols):
+        """Pull the records of filter columns `cols` back to the host as synth.Records."""
+        cols = np.asarray(cols)
+        gd = self.gd.download((self.window, self.batch, 4), np.float32)[:, cols]
+        am = self.am.download((self.window, self.batch, 4), np.float32)[:, cols]
+        my = self.my.download((self.window, self.batch, 2), np.float32)[:, cols]
+        refs = self.refs.download((self.batch, 6), np.float64)[cols]
+        return synth.unpack_planes(gd, am, my, refs[:, :3], refs[:, 3:])
+
+
+# ------------------------------------------------------------------ the batched filter
+
+class BatchedEKF:
+    """B independent filters of the reference model, state resident on the device.
+
+    Equivalent, filter by filter, to the reference's main_file.py:19-47 driver:
+    KalmanFilter(T0, mag_0, acc_0) with setQ(q), setR(r), P = I, X = [1,0,0,0], then
+    Prediction + Correction for every record.  `run` advances all filters n_steps records.
+    """
+
+    def __init__(self, batch, q=1.0, r=0.1):
+        self.batch = int(batch)
+        self.q, self.r = float(q), float(r)
+        self.X = DeviceBuffer(32 * self.batch)
+        self.P = DeviceBuffer(128 * self.batch)
+        self.reset()
+
+    def reset(self, stream=None):
+        check(lib.pekf_reset_state_dev(self.batch, self.X.ptr, self.P.ptr, stream))
+        check(lib.pekf_device_sync() if stream is None else lib.pekf_stream_sync(stream))
+
+    def set_state(self, X, P):
+        self.X.upload(f64(X, (self.batch, 4)))
+        self.P.upload(f64(P, (self.batch, 4, 4)))
+
+    def get_state(self):
+        return (self.X.download((self.batch, 4), np.float64),
+                self.P.download((self.batch, 4, 4), np.float64))
+
+    def run_async(self, win: IMUWindow, n_steps, step0=0, stream=None, traj=None):
+        """Enqueue one fused launch; traj: optional DeviceBuffer of n_steps*batch*32 bytes."""
+        assert win.batch == self.batch
+        check(lib.pekf_run_dev(self.batch, int(n_steps), win.window, int(step0), win.gd.ptr,
+                               win.am.ptr, win.my.ptr, win.refs.ptr, self.X.ptr, self.P.ptr,
+                               self.q, self.r, traj.ptr if traj is not None else None, stream))
+
+    def run(self, win: IMUWindow, n_steps=None, step0=0, want_traj=False):
+        n_steps = win.window if n_steps is None else int(n_steps)
+        tb = DeviceBuffer(32 * n_steps * self.batch) if want_traj else None
+        self.run_async(win, n_steps, step0, None, tb)
+        check(lib.pekf_device_sync())
+        if want_traj:
+            return tb.download((n_steps, self.batch, 4), np.float64)
+        return None
+
+
+# ------------------------------------------------------------------ batched per-call operators
+# NumPy-level wrappers over the host-pointer entry points (one GPU thread per item).
+
+def _n(a, k):
+    a = np.asarray(a, dtype=np.float64)
+    return a.size // k
+
+
+def rk4(q0, dt_ns, w):
+    n = _n(q0, 4)
+    q0, dt, w = f64(q0, (n, 4)), f64(dt_ns, (n,)), f64(w, (n, 3))
+    out = np.empty((n, 4))
+    check(lib.pekf_rk4(n, dptr(q0), dptr(dt), dptr(w), dptr(out)))
+    return out
+
+
+def norm(a):
+    """Row norms of a (n, len) array, sequential sum of squares (UtilityFunctions.py:16-21)."""
+    a = np.atleast_2d(np.asarray(a, dtype=np.float64))
+    n, k = a.shape
+    a = f64(a, (n, k))
+    out = np.empty(n)
+    check(lib.pekf_norm(n, k, dptr(a), dptr(out)))
+    return out
+
+
+def jacobian_a(w):
+    n = _n(w, 3)
+    w = f64(w, (n, 3))
+    out = np.empty((n, 4, 4))
+    check(lib.pekf_jacobian_a(n, dptr(w), dptr(out)))
+    return out
+
+
+def jacobian_b(q):
+    n = _n(q, 4)
+    q = f64(q, (n, 4))
+    out = np.empty((n, 4, 3))
+    check(lib.pekf_jacobian_b(n, dptr(q), dptr(out)))
+    return out
+
+
+def comparator(q1, q2):
+    n = _n(q1, 4)
+    a, b = f64(q1, (n, 4)), f64(q2, (n, 4))
+    out = np.empty((n, 4))
+    check(lib.pekf_comparator(n, dptr(a), dptr(b), dptr(out)))
+    return out
+
+
+def predict(gyro, dt_ns, X, P, Q, R):
+    n = _n(X, 4)
+    args = [f64(gyro, (n, 3)), f64(dt_ns, (n,)), f64(X, (n, 4)), f64(P, (n, 4, 4)),
+            f64(Q, (n, 3, 3)), f64(R, (n, 4, 4))]
+    z, Pm, K = np.empty((n, 4)), np.empty((n, 4, 4)), np.empty((n, 4, 4))
+    check(lib.pekf_predict(n, *[dptr(a) for a in args], dptr(z), dptr(Pm), dptr(K)))
+    return z, Pm, K
+
+
+def correct(mag, acc, z, P, K, acc0, mag0):
+    n = _n(z, 4)
+    args = [f64(mag, (n, 3)), f64(acc, (n, 3)), f64(z, (n, 4)), f64(P, (n, 4, 4)), f64(K, (n, 4, 4)),
+            f64(acc0, (n, 3)), f64(mag0, (n, 3))]
+    X, Po = np.empty((n, 4)), np.empty((n, 4, 4))
+    check(lib.pekf_correct(n, *[dptr(a) for a in args], dptr(X), dptr(Po)))
+    return X, Po
+
+
+def _wahba(fn, k, acc0, mag0, acc, mag, k_acc, k_mag):
+    n = _n(acc, 3)
+    args = [f64(acc0, (n, 3)), f64(mag0, (n, 3)), f64(acc, (n, 3)), f64(mag, (n, 3)),
+            f64(k_acc, (n,)), f64(k_mag, (n,))]
+    out = np.empty((n,) + k)
+    check(fn(n, *[dptr(a) for a in args], dptr(out)))
+    return out
+
+
+def wahba_rotation(acc0, mag0, acc, mag, k_acc, k_mag):
+    return _wahba(lib.pekf_wahba_rotation, (3, 3), acc0, mag0, acc, mag, k_acc, k_mag)
+
+
+def wahba_quaternion(acc0, mag0, acc, mag, k_acc, k_mag):
+    return _wahba(lib.pekf_wahba_quaternion, (4,), acc0, mag0, acc, mag, k_acc, k_mag)
+
+
+def rotmat_to_quat(M):
+    n = _n(M, 9)
+    M = f64(M, (n, 3, 3))
+    out = np.empty((n, 4))
+    check(lib.pekf_rotmat_to_quat(n, dptr(M), dptr(out)))
+    return out

@@ -1,0 +1,230 @@
+"""HIP path (libpekf.so on an MI355X, through the C ABI) vs the oracle and the reference's golden vectors.
+
+Tolerance: the north_star asks for quaternions within 1e-5 absolute of the NumPy reference
+(ATOL_Q).  The kernels compute in FP64, so observed errors are ~1e-13; PREC_GUARD catches
+a precision regression long before the 1e-5 contract would.
+"""
+import gzip
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import ekf_numpy as npo
+from poseestimationkf_amd import synth
+
+from .conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+
+ATOL_Q = 1e-5       # north_star: quaternion trajectories within 1e-5 absolute of NumPy
+PREC_GUARD = 1e-9   # FP64 kernel vs FP64 oracle: regression guard, far inside ATOL_Q
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from poseestimationkf_amd import engine
+    from poseestimationkf_amd._lib import device_count
+    assert device_count() > 0, "GPU tests need a HIP device"
+    return engine
+
+
+def _maxerr(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    assert np.array_equal(np.isnan(a), np.isnan(b))
+    return float(np.nanmax(np.abs(a - b), initial=0.0))
+
+
+def test_device_is_gfx950(eng):
+    assert eng.device_name(0).startswith("gfx950")
+
+
+# ------------------------------------------------------------ per-call operators vs golden KATs
+
+def test_rk4(eng, kat):
+    got = eng.rk4(kat["rk4_q0"], kat["rk4_dt"], kat["rk4_w"])
+    assert _maxerr(got, kat["rk4_out"]) < 1e-14
+
+
+def test_jacobians_norm_comparator(eng, kat):
+    assert np.array_equal(eng.jacobian_a(kat["jac_w"]), kat["jac_a"])
+    assert np.array_equal(eng.jacobian_b(kat["jac_q"]), kat["jac_b"])
+    assert _maxerr(eng.norm(kat["norm_in"]), kat["norm_out"]) < 1e-14
+    assert _maxerr(eng.comparator(kat["cmp_q1"], kat["cmp_q2"]), kat["cmp_out"]) < 1e-15
+
+
+def test_r2q_bit_exact(eng, kat):
+    got = eng.rotmat_to_quat(kat["r2q_M"])
+    assert np.array_equal(got, kat["r2q_out"], equal_nan=True)
+
+
+def test_wahba(eng, kat):
+    args = [kat[k] for k in ("wahba_acc0", "wahba_mag0", "wahba_acc", "wahba_mag", "wahba_ka", "wahba_km")]
+    R = eng.wahba_rotation(*args)
+    q = eng.wahba_quaternion(*args)
+    km = kat["wahba_km"]
+    tol = np.maximum(1e-12, 1e-15 / np.abs(km))  # LAPACK's own error grows like eps/k_mag
+    assert (np.abs(R - kat["wahba_R"]).reshape(len(km), -1).max(axis=1) <= tol).all()
+    assert (np.abs(q - kat["wahba_q"]).max(axis=1) <= tol).all()
+    assert np.allclose(q[-1], [0, 0, 0, 1], atol=1e-15)  # WahbaProblem_singularValue.py:4-24
+
+
+def test_predict_correct(eng, kat):
+    z, Pm, K = eng.predict(kat["pc_gyro"], kat["pc_dt"], kat["pc_X"], kat["pc_P"], kat["pc_Q"], kat["pc_R"])
+    assert _maxerr(z, kat["pc_z"]) < 1e-14
+    assert _maxerr(Pm, kat["pc_Pm"]) < 1e-14
+    assert _maxerr(K, kat["pc_K"]) < 1e-12
+    X, P = eng.correct(kat["pc_mag"], kat["pc_acc"], kat["pc_z"], kat["pc_Pm"], kat["pc_K"],
+                       kat["pc_acc0"], kat["pc_mag0"])
+    assert _maxerr(X, kat["pc_Xout"]) < 1e-11
+    assert _maxerr(P, kat["pc_Pout"]) < 1e-13
+
+
+def test_predict_singular_raises(eng):
+    with pytest.raises(np.linalg.LinAlgError):
+        eng.predict(np.zeros(3), 1e7, [1.0, 0, 0, 0], np.zeros((4, 4)), np.zeros((3, 3)), np.zeros((4, 4)))
+
+
+def test_empty_batch_is_noop(eng):
+    assert eng.rk4(np.zeros((0, 4)), np.zeros(0), np.zeros((0, 3))).shape == (0, 4)
+
+
+# ------------------------------------------------------------ fused kernel vs reference trajectories
+
+@pytest.mark.parametrize("tag", ["", "miss_"])
+def test_fused_run_matches_reference_trajectory(eng, traj, tag):
+    win = eng.IMUWindow.from_planes(traj[tag + "gd"], traj[tag + "am"], traj[tag + "my"],
+                                    traj[tag + "acc0"], traj[tag + "mag0"])
+    f = eng.BatchedEKF(win.batch, q=1.0, r=0.1)
+    tr = f.run(win, want_traj=True)
+    err = _maxerr(tr, traj[tag + "traj"])
+    print("fused vs reference (%s): max |dq| = %.3e" % (tag or "full", err))
+    assert err < ATOL_Q
+    assert err < PREC_GUARD
+
+
+def test_device_generator_bit_identical_to_host(eng):
+    K, W = 1000, 48
+    win = eng.IMUWindow(K, W).synthesize(seed=synth.DEFAULT_SEED, first_filter=123, missing=True)
+    dev = win.download_filters(np.arange(K))
+    host = synth.generate(np.arange(123, 123 + K), W, seed=synth.DEFAULT_SEED, missing=True)
+    for name in ("gyro", "acc", "mag"):
+        assert np.array_equal(getattr(dev, name).view(np.uint32), getattr(host, name).view(np.uint32)), name
+    assert np.array_equal(dev.dtw, host.dtw)
+    assert np.array_equal(dev.acc0, host.acc0) and np.array_equal(dev.mag0, host.mag0)
+
+
+def test_cyclic_window_ragged_batch_and_chunking(eng, oracle_c):
+    K, W = 300, 64  # 300 filters: not a multiple of the 256-lane block
+    rec = synth.generate(np.arange(K), W, seed=99, missing=True)
+    win = eng.IMUWindow.from_records(rec)
+    f = eng.BatchedEKF(K)
+    f.run(win, n_steps=150, step0=5)            # wraps the window twice
+    Xg, Pg = f.get_state()
+    Xo, Po, _ = oracle_c.run(rec, n_steps=150, step0=5)
+    assert _maxerr(Xg, Xo) < PREC_GUARD
+    assert _maxerr(Pg, Po) < PREC_GUARD
+    # chunked launches continue exactly where a single launch would be
+    g = eng.BatchedEKF(K)
+    g.run(win, n_steps=70, step0=5)
+    g.run(win, n_steps=80, step0=75)
+    X2, P2 = g.get_state()
+    assert np.array_equal(X2, Xg) and np.array_equal(P2, Pg)
+
+
+def test_set_state_roundtrip_and_resume(eng, oracle_c):
+    K, W = 64, 40
+    rec = synth.generate(np.arange(K), W, seed=5)
+    win = eng.IMUWindow.from_records(rec)
+    X0, P0, _ = oracle_c.run(rec, n_steps=17)          # start from a mid-run state
+    f = eng.BatchedEKF(K)
+    f.set_state(X0, P0)
+    Xs, Ps = f.get_state()
+    assert np.array_equal(Xs, X0) and np.array_equal(Ps, P0)
+    f.run(win, n_steps=23, step0=17)
+    Xo, _, _ = oracle_c.run(rec, n_steps=40)
+    assert _maxerr(f.get_state()[0], Xo) < PREC_GUARD
+
+
+def test_scale_c2_batch_sampled_against_oracle(eng, oracle_c):
+    """Config-2 batch (65,536 filters) on a device-generated window; 64 sampled filters re-run on the host."""
+    B, W, N = 65536, 128, 384
+    win = eng.IMUWindow(B, W).synthesize(seed=synth.DEFAULT_SEED)
+    f = eng.BatchedEKF(B)
+    f.run(win, n_steps=N)
+    X, P = f.get_state()
+    assert np.isfinite(X).all()
+    assert np.abs(np.linalg.norm(X, axis=1) - 1).max() < 1e-12   # size-independent property
+    assert np.abs(P - P.transpose(0, 2, 1)).max() == 0.0          # stored symmetric
+    cols = np.linspace(0, B - 1, 64).astype(np.int64)
+    rec = synth.generate(cols, W, seed=synth.DEFAULT_SEED)
+    Xo, _, _ = oracle_c.run(rec, n_steps=N)
+    err = _maxerr(X[cols], Xo)
+    print("C2 sampled parity: max |dq| = %.3e" % err)
+    assert err < ATOL_Q and err < PREC_GUARD
+
+
+def test_batch_of_one(eng, traj):
+    sl = slice(0, 1)
+    win = eng.IMUWindow.from_planes(traj["gd"][:, sl], traj["am"][:, sl], traj["my"][:, sl],
+                                    traj["acc0"][sl], traj["mag0"][sl])
+    tr = eng.BatchedEKF(1).run(win, want_traj=True)
+    assert _maxerr(tr, traj["traj"][:, sl]) < PREC_GUARD
+
+
+# ------------------------------------------------------------ config 1: the drop-in modules
+
+def test_dropin_main_file_loop_on_c1_log(eng, tmp_path, monkeypatch):
+    """main_file.py:11-47 on the config-1 log, through the drop-in modules, vs main_file's own X_k."""
+    log = tmp_path / "KalmanFilter.txt"
+    with gzip.open(os.path.join(GOLDEN, "c1_log.txt.gz"), "rt") as fh:
+        log.write_text(fh.read())
+    monkeypatch.setenv("PEKF_LOG_PATH", str(log))
+    monkeypatch.syspath_prepend(os.path.join(ROOT, "poseestimationkf_amd", "dropin"))
+    for m in ("ExtendedKalmanFilter", "Wahba", "UtilityFunctions", "ReadFile", "_bootstrap"):
+        sys.modules.pop(m, None)
+    from ExtendedKalmanFilter import KalmanFilter
+    from ReadFile import getData
+    from UtilityFunctions import DimensionalSplit, norm
+    from Wahba import Wahba
+
+    g = getData()
+    w = Wahba(g.acc_0, g.mag_0)
+    k = KalmanFilter(g.timestamp[0][0], g.mag_0, g.acc_0, 0.5)
+    k.setQ(1)
+    k.setR(0.1)
+    P = np.identity(4)
+    g.timestamp = g.timestamp[1:]
+    X = np.asarray([1., 0., 0., 0.])
+    X_k = [X]
+    for i in range(len(g.acc_1)):
+        z_k, P, K_k = k.Prediction(g.gyro[i], g.timestamp[i][0], X, P)
+        w.getQuarternion(g.acc_1[i], g.mag_1[i], 0.5, 0.5)
+        X, P = k.Correction(g.mag_1[i], g.acc_1[i], z_k, P, K_k)
+        X_k.append(X)
+    want = np.load(os.path.join(GOLDEN, "c1_xk.npy"))
+    err = _maxerr(np.array(X_k), want)
+    print("C1 drop-in vs main_file.py: max |dq| = %.3e over %d steps" % (err, len(X_k) - 1))
+    assert err < ATOL_Q and err < PREC_GUARD
+    assert len(DimensionalSplit(X_k)) == 4
+    assert abs(norm(X_k[-1]) - 1.0) < 1e-14
+
+
+def test_dropin_returns_fresh_arrays_and_keeps_inputs(eng, monkeypatch):
+    monkeypatch.syspath_prepend(os.path.join(ROOT, "poseestimationkf_amd", "dropin"))
+    for m in ("ExtendedKalmanFilter", "Wahba", "UtilityFunctions", "_bootstrap"):
+        sys.modules.pop(m, None)
+    from ExtendedKalmanFilter import KalmanFilter
+    k = KalmanFilter(0.0, [0.5, 0.0, -0.86], [0.0, 0.1, 0.99], 0.5)
+    k.setQ(1)
+    k.setR(0.1)
+    X, P = np.asarray([1., 0., 0., 0.]), np.identity(4)
+    Xc, Pc = X.copy(), P.copy()
+    z, Pm, K = k.Prediction([0.1, -0.2, 0.3], 1e7, X, P)
+    assert np.array_equal(X, Xc) and np.array_equal(P, Pc) and k.previousT == 1e7
+    X1, P1 = k.Correction([0.5, 0.01, -0.86], [0.01, 0.1, 0.99], z, Pm, K)
+    want = npo.correct([0.5, 0.01, -0.86], [0.01, 0.1, 0.99], z, Pm, K, [0.0, 0.1, 0.99], [0.5, 0.0, -0.86])
+    assert _maxerr(X1, want[0]) < 1e-13 and _maxerr(P1, want[1]) < 1e-13
+    assert X1 is not z and P1 is not Pm
