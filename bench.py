@@ -132,7 +132,8 @@ def main():
     first, B = shard.shard_range(args.batch * world, rank, world)
     N, W = args.records, args.window
 
-    stream = torch.cuda.current_stream().cuda_stream if world > 1 else engine.Stream().handle
+    own_stream = None if world > 1 else engine.Stream()  # keep the object alive for the whole run
+    stream = torch.cuda.current_stream().cuda_stream if world > 1 else own_stream.handle
 
     def sync():
         if world > 1:
