@@ -54,7 +54,7 @@ def _cpu_worker(args):
     return len(ids) * n_rec, time.perf_counter() - t0
 
 
-def cpu_baseline(seed, missing, filters_per_core=8, n_rec=1000):
+def cpu_baseline(seed, missing, filters_per_core=16, n_rec=1500):
     import multiprocessing as mp
     cores = len(os.sched_getaffinity(0))
     workers = max(1, min(16, cores))
@@ -206,6 +206,7 @@ def main():
         k_s = float(np.mean(kms)) / 1e3
         achieved = B * N * REC_BYTES / k_s / 1e9
         flop = FLOP_PER_STEP
+        traffic, tsrc = measured_traffic(B, N)
         out = {
             "metric": "EKF steps/sec (predict+Wahba+update) at batch=1M; HBM-roofline %",
             "value": value,
@@ -225,12 +226,17 @@ def main():
                        "filters_per_gpu": B, "global_filters": B * world, "records_per_step": N,
                        "window_records": W, "parallelism": "dp%d (filter-batch shards, 1 RCCL gather)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": (os.path.relpath(tsrc[0], ROOT) + " (2 x FETCH_SIZE, separate "
+                                            "rocprofv3 --pmc pass of this command)") if tsrc else None,
                          "kernel": "k_run<false> (pekf_run_dev)", "kernel_ms": k_s * 1e3,
                          "bytes_per_launch": B * N * REC_BYTES},
-            "fp64_valu": {"flop_per_step": flop, "achieved_tflops": B * N * flop / k_s / 1e12,
-                          "peak_tflops": FP64_PEAK_TFLOPS,
-                          "frac": B * N * flop / k_s / 1e12 / FP64_PEAK_TFLOPS},
+            "fp64_valu": {"flop_per_step": flop, "fp64_instr_per_step": FP64_INSTR_PER_STEP,
+                          "achieved_tflops": B * N * flop / k_s / 1e12, "peak_tflops": FP64_PEAK_TFLOPS,
+                          "frac": B * N * flop / k_s / 1e12 / FP64_PEAK_TFLOPS,
+                          "valu_busy_pmc": tsrc[1].get("valu_busy") if tsrc else None,
+                          "note": "the kernel is FP64-VALU-issue-bound (valu_busy ~0.96); "
+                                  "HBM frac is capped by it"},
             "cpu_baseline": cpu,
             "parity": parity,
         }
@@ -239,9 +245,25 @@ def main():
         dist.destroy_process_group()
 
 
-# Algorithmic FP64 work per filter-step of the fused kernel (DESIGN.md "Roofline"):
-# counted from the kernel's formulation (an FMA counts 2).
-FLOP_PER_STEP = 880
+# FP64 work per filter-step of the fused kernel, counted from its gfx950 ISA hot loop by
+# scripts/isa_count.py (DESIGN.md "FP64 budget"): 415 FP64 VALU instructions, of which the
+# arithmetic ones are 619 FLOP with an FMA counted as 2.
+FLOP_PER_STEP = 619
+FP64_INSTR_PER_STEP = 415
+
+
+def measured_traffic(batch, records):
+    """HBM bytes per launch from the newest committed rocprofv3 PMC summary of the same config."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary_*.json"))):
+        with open(path) as fh:
+            s = json.load(fh)
+        if s.get("config") == {"batch": batch, "records": records}:
+            best = (path, s)
+    if best is None:
+        return None, None
+    return best[1]["hbm_traffic_bytes"], best
 
 if __name__ == "__main__":
     main()

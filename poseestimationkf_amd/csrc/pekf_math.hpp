@@ -152,6 +152,33 @@ PEKF_DEV void rotm_to_quat(const double *M, double *q) {
     }
 }
 
+// ------------------------------- reciprocal / rsqrt ------------------------------------------
+// FAST = false: IEEE division and sqrt (per-call kernels).  FAST = true: the hardware
+// v_rcp_f64 / v_rsq_f64 seeds plus two Newton steps each (4 FMAs / 8 ops), accurate to
+// ~1 ulp for the positive, normal operands of this model, without the scale / fixup
+// sequences of a correctly rounded division (fused kernel; DESIGN.md "FP64 budget").
+template <bool FAST>
+PEKF_DEV double recip(double x) {
+    if (!FAST) return 1.0 / x;
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+
+template <bool FAST>
+PEKF_DEV double rsqrt(double x) {
+    if (!FAST) return 1.0 / sqrt(x);
+    double y = __builtin_amdgcn_rsq(x);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const double e = fma(-x * y, y, 1.0);  // 1 - x y^2
+        y = fma(y, 0.5 * e, y);
+    }
+    return y;
+}
+
 // ------------------------------- Wahba closed form -------------------------------------------
 
 // Orthonormal frame of a vector pair (a, m): e1 = a/|a|, e2 = GramSchmidt(m), u3 = e1 x e2,
@@ -161,25 +188,27 @@ struct Frame {
     double alpha, beta1, beta2;
 };
 
+template <bool FAST = false>
 PEKF_DEV void make_frame(const double *a, const double *m, Frame &F) {
-    const double na = sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
-    const double ia = 1.0 / na;
+    const double sa = a[0] * a[0] + a[1] * a[1] + a[2] * a[2];
+    const double ia = rsqrt<FAST>(sa);
     F.e1[0] = a[0] * ia; F.e1[1] = a[1] * ia; F.e1[2] = a[2] * ia;
     const double b1 = F.e1[0] * m[0] + F.e1[1] * m[1] + F.e1[2] * m[2];
     const double t0 = m[0] - b1 * F.e1[0], t1 = m[1] - b1 * F.e1[1], t2 = m[2] - b1 * F.e1[2];
-    const double nb = sqrt(t0 * t0 + t1 * t1 + t2 * t2);
-    const double ib = 1.0 / nb;
+    const double sb = t0 * t0 + t1 * t1 + t2 * t2;
+    const double ib = rsqrt<FAST>(sb);
     F.e2[0] = t0 * ib; F.e2[1] = t1 * ib; F.e2[2] = t2 * ib;
     F.u3[0] = F.e1[1] * F.e2[2] - F.e1[2] * F.e2[1];
     F.u3[1] = F.e1[2] * F.e2[0] - F.e1[0] * F.e2[2];
     F.u3[2] = F.e1[0] * F.e2[1] - F.e1[1] * F.e2[0];
-    F.alpha = na;
+    F.alpha = FAST ? sa * ia : sqrt(sa);
     F.beta1 = b1;
-    F.beta2 = nb;
+    F.beta2 = FAST ? sb * ib : sqrt(sb);
 }
 
 // R = argmax_{R in SO(3)} tr(R^T B), B = ka acc0 acc^T + km mag0 mag^T (Wahba.py:8-17):
 // W = frame of the reference pair (acc0, mag0), V = frame of the current pair (acc, mag).
+template <bool FAST = false>
 PEKF_DEV void wahba_rotation(const Frame &W, const Frame &V, double ka, double km, double *R) {
     const double c00 = ka * W.alpha * V.alpha + km * W.beta1 * V.beta1;
     const double c01 = km * W.beta1 * V.beta2;
@@ -190,7 +219,7 @@ PEKF_DEV void wahba_rotation(const Frame &W, const Frame &V, double ka, double k
     double p, s;
     if (proper) { p = c00 + c11; s = c10 - c01; }
     else        { p = c00 - c11; s = c01 + c10; }
-    const double ih = 1.0 / sqrt(p * p + s * s);
+    const double ih = rsqrt<FAST>(p * p + s * s);
     p *= ih;
     s *= ih;
     // P2 = [[p, -s], [s, p]] (rotation) or [[p, s], [s, -p]] (reflection); c = +1 / -1
@@ -214,16 +243,43 @@ PEKF_DEV void wahba_rotation_vectors(const double *acc0, const double *mag0, con
     wahba_rotation(W, V, ka, km, R);
 }
 
+// Branch-free RotationMatrix2Quart for the fused kernel: the reference's branch choice
+// (Wahba.py:28,35, strict '>', else branch 3) is made by selects, then ONE rsqrt gives both
+// 1/S = 0.5/sqrt(t) and 0.25*S = 0.5*t/sqrt(t).  Agrees with rotm_to_quat to ~1 ulp; at an
+// exact identity both give NaNs (which the filter update propagates identically).
+PEKF_DEV void rotm_to_quat_fast(const double *M, double *q) {
+    const double t1 = ((1.0 + M[0]) - M[4]) - M[8];
+    const double t2 = ((1.0 - M[0]) + M[4]) - M[8];
+    const double t3 = ((1.0 - M[0]) - M[4]) + M[8];
+    const bool b1 = (t1 > t2) && (t1 > t3);
+    const bool b2 = !b1 && (t2 > t1) && (t2 > t3);
+    const bool b3 = !b1 && !b2;
+    const double t = b1 ? t1 : (b2 ? t2 : t3);
+    const double rs = rsqrt<true>(t);
+    const double inv_s = 0.5 * rs, quarter_s = 0.5 * (t * rs);
+    const double dw1 = M[7] - M[5], dw2 = M[2] - M[6], dw3 = M[3] - M[1];
+    const double sxy = M[1] + M[3], sxz = M[2] + M[6], syz = M[5] + M[7];
+    q[0] = (b1 ? dw1 : (b2 ? dw2 : dw3)) * inv_s;
+    q[1] = b1 ? quarter_s : (b2 ? sxy : sxz) * inv_s;
+    q[2] = b2 ? quarter_s : (b1 ? sxy : syz) * inv_s;
+    q[3] = b3 ? quarter_s : (b1 ? sxz : syz) * inv_s;
+}
+
 // ------------------------------- fused-step forms --------------------------------------------
+// With R = rI the reference recursion (ExtendedKalmanFilter.py:61-66,76-78) is, exactly in
+// real arithmetic,
+//   P-  = A P A^T + (q_scale / 4) (|X|^2 I - X X^T)
+//   S   = P- + rI,   K = I - r S^-1,   P = P- - K P- = r I - r^2 S^-1,   X = z + K e = Y - r S^-1 e
+// so only the symmetric S^-1 is formed (no general 4x4 products with K).
 
 // Symmetric 4x4 stored as its upper triangle: 00 01 02 03 11 12 13 22 23 33
 struct Sym4 {
     double a00, a01, a02, a03, a11, a12, a13, a22, a23, a33;
 };
 
-// P- = 0.25 * Omega(w) P Omega(w)^T + (qs/4) (|x|^2 I - x x^T)   (ExtendedKalmanFilter.py:61)
-PEKF_DEV Sym4 propagate_cov(const Sym4 &P, const double *w, const double *x, double qs) {
-    const double w0 = w[0], w1 = w[1], w2 = w[2];
+// A P A^T + g (|x|^2 I - x x^T), A = Omega(h), h = w/2 (ExtendedKalmanFilter.py:44-47,52-55,61)
+PEKF_DEV Sym4 propagate_cov(const Sym4 &P, const double *h, const double *x, double g) {
+    const double w0 = h[0], w1 = h[1], w2 = h[2];
     // T = Omega P (full 4x4), rows of Omega: [0,-w0,-w1,-w2] [w0,0,w2,-w1] [w1,-w2,0,w0] [w2,w1,-w0,0]
     const double p[4][4] = {{P.a00, P.a01, P.a02, P.a03},
                             {P.a01, P.a11, P.a12, P.a13},
@@ -247,68 +303,74 @@ PEKF_DEV Sym4 propagate_cov(const Sym4 &P, const double *w, const double *x, dou
         }
     };
     const double n2 = x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
-    const double g = 0.25 * qs;
+    const double gx0 = g * x[0], gx1 = g * x[1], gx2 = g * x[2], gx3 = g * x[3];
     Sym4 o;
-    o.a00 = 0.25 * m(0, 0) + g * (n2 - x[0] * x[0]);
-    o.a01 = 0.25 * m(0, 1) - g * (x[0] * x[1]);
-    o.a02 = 0.25 * m(0, 2) - g * (x[0] * x[2]);
-    o.a03 = 0.25 * m(0, 3) - g * (x[0] * x[3]);
-    o.a11 = 0.25 * m(1, 1) + g * (n2 - x[1] * x[1]);
-    o.a12 = 0.25 * m(1, 2) - g * (x[1] * x[2]);
-    o.a13 = 0.25 * m(1, 3) - g * (x[1] * x[3]);
-    o.a22 = 0.25 * m(2, 2) + g * (n2 - x[2] * x[2]);
-    o.a23 = 0.25 * m(2, 3) - g * (x[2] * x[3]);
-    o.a33 = 0.25 * m(3, 3) + g * (n2 - x[3] * x[3]);
+    o.a00 = m(0, 0) + g * (n2 - x[0] * x[0]);
+    o.a01 = m(0, 1) - gx0 * x[1];
+    o.a02 = m(0, 2) - gx0 * x[2];
+    o.a03 = m(0, 3) - gx0 * x[3];
+    o.a11 = m(1, 1) + g * (n2 - x[1] * x[1]);
+    o.a12 = m(1, 2) - gx1 * x[2];
+    o.a13 = m(1, 3) - gx1 * x[3];
+    o.a22 = m(2, 2) + g * (n2 - x[2] * x[2]);
+    o.a23 = m(2, 3) - gx2 * x[3];
+    o.a33 = m(3, 3) + g * (n2 - x[3] * x[3]);
+    (void)gx3;
     return o;
 }
 
 // Inverse of an SPD 4x4 by LDL^T (no pivoting needed: S = P- + rI, r > 0).
+template <bool FAST = true>
 PEKF_DEV Sym4 spd_inverse(const Sym4 &S) {
-    const double d0 = S.a00, i0 = 1.0 / d0;
+    const double i0 = recip<FAST>(S.a00);
     const double l10 = S.a01 * i0, l20 = S.a02 * i0, l30 = S.a03 * i0;
-    const double d1 = S.a11 - l10 * S.a01, i1 = 1.0 / d1;
+    const double d1 = S.a11 - l10 * S.a01, i1 = recip<FAST>(d1);
     const double a21 = S.a12 - l20 * S.a01, a31 = S.a13 - l30 * S.a01;
     const double l21 = a21 * i1, l31 = a31 * i1;
-    const double d2 = S.a22 - l20 * S.a02 - l21 * a21, i2 = 1.0 / d2;
+    const double d2 = S.a22 - l20 * S.a02 - l21 * a21, i2 = recip<FAST>(d2);
     const double a32 = S.a23 - l30 * S.a02 - l31 * a21;
     const double l32 = a32 * i2;
-    const double d3 = S.a33 - l30 * S.a03 - l31 * a31 - l32 * a32, i3 = 1.0 / d3;
+    const double d3 = S.a33 - l30 * S.a03 - l31 * a31 - l32 * a32, i3 = recip<FAST>(d3);
     // N = L^-1 (unit lower)
     const double n10 = -l10;
     const double n21 = -l21, n20 = -(l20 + l21 * n10);
     const double n32 = -l32, n31 = -(l31 + l32 * n21), n30 = -(l30 + l31 * n10 + l32 * n20);
     // S^-1 = N^T D^-1 N
+    const double m30 = n30 * i3, m31 = n31 * i3, m32 = n32 * i3;
+    const double m20 = n20 * i2, m21 = n21 * i2;
+    const double m10 = n10 * i1;
     Sym4 o;
     o.a33 = i3;
-    o.a23 = n32 * i3;
-    o.a22 = i2 + n32 * n32 * i3;
-    o.a13 = n31 * i3;
-    o.a12 = n21 * i2 + n31 * n32 * i3;
-    o.a11 = i1 + n21 * n21 * i2 + n31 * n31 * i3;
-    o.a03 = n30 * i3;
-    o.a02 = n20 * i2 + n30 * n32 * i3;
-    o.a01 = n10 * i1 + n20 * n21 * i2 + n30 * n31 * i3;
-    o.a00 = i0 + n10 * n10 * i1 + n20 * n20 * i2 + n30 * n30 * i3;
+    o.a23 = m32;
+    o.a22 = i2 + n32 * m32;
+    o.a13 = m31;
+    o.a12 = m21 + n31 * m32;
+    o.a11 = i1 + n21 * m21 + n31 * m31;
+    o.a03 = m30;
+    o.a02 = m20 + n30 * m32;
+    o.a01 = m10 + n20 * m21 + n30 * m31;
+    o.a00 = i0 + n10 * m10 + n20 * m20 + n30 * m30;
     return o;
 }
 
-// Closed form of the classical RK4 step + normalisation (ExtendedKalmanFilter.py:25-41).
-PEKF_DEV void rk4_closed(const double *x, double dt_ns, const double *w, double *z) {
+// Closed form of the classical RK4 step + normalisation (ExtendedKalmanFilter.py:25-41),
+// h_w = w/2 (so Omega(h_w) = 0.5*Omega(w), the reference's W).
+PEKF_DEV void rk4_closed(const double *x, double dt_ns, const double *hw, double *z) {
     const double h = dt_ns * kNsToS;
-    const double th2 = 0.25 * (w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    const double th2 = hw[0] * hw[0] + hw[1] * hw[1] + hw[2] * hw[2];
     const double xx = (h * h) * th2;
     const double ca = 1.0 - 0.5 * xx + xx * xx * (1.0 / 24.0);
-    const double cb = 0.5 * h * (1.0 - xx * (1.0 / 6.0));
-    // Omega(w) x
-    const double o0 = -w[0] * x[1] - w[1] * x[2] - w[2] * x[3];
-    const double o1 = w[0] * x[0] + w[2] * x[2] - w[1] * x[3];
-    const double o2 = w[1] * x[0] - w[2] * x[1] + w[0] * x[3];
-    const double o3 = w[2] * x[0] + w[1] * x[1] - w[0] * x[2];
+    const double cb = h * (1.0 - xx * (1.0 / 6.0));
+    // 0.5*Omega(w) x
+    const double o0 = -hw[0] * x[1] - hw[1] * x[2] - hw[2] * x[3];
+    const double o1 = hw[0] * x[0] + hw[2] * x[2] - hw[1] * x[3];
+    const double o2 = hw[1] * x[0] - hw[2] * x[1] + hw[0] * x[3];
+    const double o3 = hw[2] * x[0] + hw[1] * x[1] - hw[0] * x[2];
     z[0] = ca * x[0] + cb * o0;
     z[1] = ca * x[1] + cb * o1;
     z[2] = ca * x[2] + cb * o2;
     z[3] = ca * x[3] + cb * o3;
-    const double in = 1.0 / sqrt(z[0] * z[0] + z[1] * z[1] + z[2] * z[2] + z[3] * z[3]);
+    const double in = rsqrt<true>(z[0] * z[0] + z[1] * z[1] + z[2] * z[2] + z[3] * z[3]);
     z[0] *= in; z[1] *= in; z[2] *= in; z[3] *= in;
 }
 

@@ -47,8 +47,10 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     {
         const double a0[3] = {refs[6 * b + 0], refs[6 * b + 1], refs[6 * b + 2]};
         const double m0[3] = {refs[6 * b + 3], refs[6 * b + 4], refs[6 * b + 5]};
-        make_frame(a0, m0, Wf);
+        make_frame<true>(a0, m0, Wf);
     }
+    const double g = 0.25 * qs;       // Jb Q Jb^T = (q/4)(|X|^2 I - X X^T)
+    const double r2 = rs * rs;
     double x[4] = {Xio[4 * b + 0], Xio[4 * b + 1], Xio[4 * b + 2], Xio[4 * b + 3]};
     const double *pp = Pio + 16 * b;
     Sym4 P = {pp[0], pp[1], pp[2], pp[3], pp[5], pp[6], pp[7], pp[10], pp[11], pp[15]};
@@ -61,51 +63,48 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
         Rec nxt;
         if (t + 1 < n_steps) nxt = load_rec(gd, am, my, nrow * batch + b);
 
-        const double w[3] = {cur.gd.x, cur.gd.y, cur.gd.z};
+        const double hw[3] = {0.5 * (double)cur.gd.x, 0.5 * (double)cur.gd.y, 0.5 * (double)cur.gd.z};
         const uint32_t word = __float_as_uint(cur.gd.w);
         const double dt_ns = (double)(word & 0x7FFFFFFFu);
 
         // ---- Prediction (ExtendedKalmanFilter.py:58-68) ----
-        const Sym4 Pm = propagate_cov(P, w, x, qs);  // Jb from the prior X (:60)
+        const Sym4 Pm = propagate_cov(P, hw, x, g);  // Jb from the prior X (:60)
         double z[4];
-        rk4_closed(x, dt_ns, w, z);                  // (:62)
+        rk4_closed(x, dt_ns, hw, z);                 // (:62)
 
         if (word & PEKF_MISSING_MAG_BIT) {
             // Wahba-skip: no Correction for this record (X = z, P = P-)
             x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
             P = Pm;
         } else {
+            // S = P- + rI; K = P- S^-1 = I - r S^-1  (:63-66)
             const Sym4 S = {Pm.a00 + rs, Pm.a01, Pm.a02, Pm.a03, Pm.a11 + rs,
                             Pm.a12, Pm.a13, Pm.a22 + rs, Pm.a23, Pm.a33 + rs};
-            const Sym4 Si = spd_inverse(S);
-            // K = P- S^-1 = I - r S^-1 (symmetric)      (:63-66)
-            const Sym4 K = {1.0 - rs * Si.a00, -rs * Si.a01, -rs * Si.a02, -rs * Si.a03,
-                            1.0 - rs * Si.a11, -rs * Si.a12, -rs * Si.a13,
-                            1.0 - rs * Si.a22, -rs * Si.a23, 1.0 - rs * Si.a33};
+            const Sym4 Si = spd_inverse<true>(S);
 
             // ---- Correction (ExtendedKalmanFilter.py:70-80) ----
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
-            const double ka = fabs(acc[2]);            // (:71)
+            const double ka = fabs(acc[2]);              // (:71)
             Frame Vf;
-            make_frame(acc, mag, Vf);
+            make_frame<true>(acc, mag, Vf);
             double R[9], y[4];
-            wahba_rotation(Wf, Vf, ka, 1.0 - ka, R);   // Wahba.py:8-17
-            rotm_to_quat(R, y);                         // Wahba.py:19-47
+            wahba_rotation<true>(Wf, Vf, ka, 1.0 - ka, R);  // Wahba.py:8-17
+            rotm_to_quat_fast(R, y);                      // Wahba.py:19-47
             const double cmp = y[0] * z[0] + y[1] * z[1] + y[2] * z[2] + y[3] * z[3];
-            const double sg = cmp < 0.0 ? -1.0 : 1.0;   // (:73-75)
-            const double e0 = sg * y[0] - z[0], e1 = sg * y[1] - z[1];
-            const double e2 = sg * y[2] - z[2], e3 = sg * y[3] - z[3];
-            // X = z + K e (:77), normalised (:79)
-            const double x0 = z[0] + K.a00 * e0 + K.a01 * e1 + K.a02 * e2 + K.a03 * e3;
-            const double x1 = z[1] + K.a01 * e0 + K.a11 * e1 + K.a12 * e2 + K.a13 * e3;
-            const double x2 = z[2] + K.a02 * e0 + K.a12 * e1 + K.a22 * e2 + K.a23 * e3;
-            const double x3 = z[3] + K.a03 * e0 + K.a13 * e1 + K.a23 * e2 + K.a33 * e3;
-            const double in = 1.0 / sqrt(x0 * x0 + x1 * x1 + x2 * x2 + x3 * x3);
+            const double sg = cmp < 0.0 ? -1.0 : 1.0;     // (:73-75)
+            y[0] *= sg; y[1] *= sg; y[2] *= sg; y[3] *= sg;
+            const double e0 = y[0] - z[0], e1 = y[1] - z[1], e2 = y[2] - z[2], e3 = y[3] - z[3];
+            // X = z + K e = Y - r S^-1 e (:77), normalised (:79)
+            const double x0 = y[0] - rs * (Si.a00 * e0 + Si.a01 * e1 + Si.a02 * e2 + Si.a03 * e3);
+            const double x1 = y[1] - rs * (Si.a01 * e0 + Si.a11 * e1 + Si.a12 * e2 + Si.a13 * e3);
+            const double x2 = y[2] - rs * (Si.a02 * e0 + Si.a12 * e1 + Si.a22 * e2 + Si.a23 * e3);
+            const double x3 = y[3] - rs * (Si.a03 * e0 + Si.a13 * e1 + Si.a23 * e2 + Si.a33 * e3);
+            const double in = rsqrt<true>(x0 * x0 + x1 * x1 + x2 * x2 + x3 * x3);
             x[0] = x0 * in; x[1] = x1 * in; x[2] = x2 * in; x[3] = x3 * in;
-            // P = P- - K P- = r K (:78)
-            P = {rs * K.a00, rs * K.a01, rs * K.a02, rs * K.a03, rs * K.a11,
-                 rs * K.a12, rs * K.a13, rs * K.a22, rs * K.a23, rs * K.a33};
+            // P = P- - K P- = r K = r I - r^2 S^-1 (:78)
+            P = {rs - r2 * Si.a00, -r2 * Si.a01, -r2 * Si.a02, -r2 * Si.a03, rs - r2 * Si.a11,
+                 -r2 * Si.a12, -r2 * Si.a13, rs - r2 * Si.a22, -r2 * Si.a23, rs - r2 * Si.a33};
         }
         if (TRAJ) {
             double2 *o = reinterpret_cast<double2 *>(traj + (t * batch + b) * 4);
@@ -117,10 +116,11 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     }
     Xio[4 * b + 0] = x[0]; Xio[4 * b + 1] = x[1]; Xio[4 * b + 2] = x[2]; Xio[4 * b + 3] = x[3];
     double *po = Pio + 16 * b;
-    po[0] = P.a00; po[1] = P.a01; po[2] = P.a02; po[3] = P.a03;
-    po[4] = P.a01; po[5] = P.a11; po[6] = P.a12; po[7] = P.a13;
-    po[8] = P.a02; po[9] = P.a12; po[10] = P.a22; po[11] = P.a23;
-    po[12] = P.a03; po[13] = P.a13; po[14] = P.a23; po[15] = P.a33;
+    const Sym4 &Po = P;
+    po[0] = Po.a00; po[1] = Po.a01; po[2] = Po.a02; po[3] = Po.a03;
+    po[4] = Po.a01; po[5] = Po.a11; po[6] = Po.a12; po[7] = Po.a13;
+    po[8] = Po.a02; po[9] = Po.a12; po[10] = Po.a22; po[11] = Po.a23;
+    po[12] = Po.a03; po[13] = Po.a13; po[14] = Po.a23; po[15] = Po.a33;
 }
 
 __global__ __launch_bounds__(kRunBlock) void k_reset(int64_t batch, double *X, double *P) {
