@@ -100,6 +100,10 @@ def main():
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--cpu-baseline", choices=["port", "none"], default="port")
     ap.add_argument("--parity-samples", type=int, default=16)
+    ap.add_argument("--precision", choices=["f64", "mixed"], default="f64",
+                    help="f64 (default, as the reference) or mixed (covariance recursion in f32)")
+    ap.add_argument("--dist", action="store_true",
+                    help="use torch.distributed/RCCL even at world size 1 (exercises the gather path)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -119,11 +123,15 @@ def main():
         log("cpu baseline: %.0f steps/s on %d cores" % (cpu["value"], cpu["cores"]))
 
     torch = dist = None
-    if world > 1:
-        import torch
+    use_dist = world > 1 or args.dist
+    if use_dist:
+        import torch  # before libpekf: the library then binds torch's HIP runtime
         import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL over xGMI
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))  # RCCL over xGMI
 
     import numpy as np
 
@@ -132,25 +140,25 @@ def main():
     first, B = shard.shard_range(args.batch * world, rank, world)
     N, W = args.records, args.window
 
-    own_stream = None if world > 1 else engine.Stream()  # keep the object alive for the whole run
-    stream = torch.cuda.current_stream().cuda_stream if world > 1 else own_stream.handle
+    own_stream = None if use_dist else engine.Stream()  # keep the object alive for the whole run
+    stream = torch.cuda.current_stream().cuda_stream if use_dist else own_stream.handle
 
     def sync():
-        if world > 1:
+        if use_dist:
             torch.cuda.synchronize()
         else:
             engine.check(engine.lib.pekf_stream_sync(stream))
 
     def barrier():
-        if world > 1:
+        if use_dist:
             dist.barrier()
 
     log("rank %d/%d: synthesizing %d filters x %d records (%.1f GB resident)" %
         (rank, world, B, W, synth.window_bytes(B, W) / 1e9))
     win = engine.IMUWindow(B, W).synthesize(seed=args.seed, first_filter=first, missing=args.missing,
                                             stream=stream)
-    filt = engine.BatchedEKF(B, q=1.0, r=0.1)
-    xt = torch.empty((B, 4), dtype=torch.float64, device="cuda") if world > 1 else None
+    filt = engine.BatchedEKF(B, q=1.0, r=0.1, precision=args.precision)
+    xt = torch.empty((B, 4), dtype=torch.float64, device="cuda") if use_dist else None
     sync()
 
     total = args.warmup + args.steps
@@ -163,9 +171,9 @@ def main():
         e0.record(stream)
         filt.run_async(win, N, (k * N) % W, stream)
         e1.record(stream)
-        if world > 1:
+        if use_dist:
             engine.check(engine.lib.pekf_memcpy_d2d(xt.data_ptr(), filt.X.ptr, 32 * B, stream))
-            gathered = shard.gather_quaternions(xt, rank, world)
+            gathered = shard.gather_quaternions(xt, rank, world, force_collective=True)
 
     for k in range(args.warmup):
         bench_step(k)
@@ -180,7 +188,7 @@ def main():
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -218,7 +226,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f64" if args.precision == "f64" else "f64 quaternion path + f32 covariance (P, S^-1)",
             "data": "synthetic (on-device Philox IMU generator, bit-identical host mirror; 40 B records, "
                     "%d-record resident window replayed cyclically)" % W,
             "config": {"workload": "config 5: batch=1,048,576/GPU, 30% missing-mag" if args.missing else
@@ -241,7 +249,11 @@ def main():
             "parity": parity,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
+        if rank == 0 and gathered is not None:  # the gathered quaternions are the filters' final X
+            Xr, _ = filt.get_state()
+            assert np.array_equal(gathered[:B].cpu().numpy(), Xr), "gather mismatch on rank 0"
+            log("gather: %d quaternions on rank 0 match rank 0's shard" % gathered.shape[0])
         dist.destroy_process_group()
 
 

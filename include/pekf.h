@@ -40,6 +40,11 @@ extern "C" {
 /* Bit 31 of a stream record's dt word: magnetometer sample missing ("Wahba-skip"). */
 #define PEKF_MISSING_MAG_BIT 0x80000000u
 
+/* pekf_run_dev flags.  Default (0): every operation in FP64, as the reference.
+ * PEKF_RUN_MIXED_PRECISION: opt-in; the covariance recursion (P-, S^-1, K, P) in FP32, the
+ * quaternion path (RK4, Wahba, R->q, X update) in FP64.  Quaternions stay within ~1e-8 of FP64. */
+#define PEKF_RUN_MIXED_PRECISION 0x1u
+
 int pekf_abi_version(void);
 const char *pekf_last_error(void);
 
@@ -126,11 +131,12 @@ int pekf_rotmat_to_quat(int64_t n, const double *M, double *q);
  * X[batch*4], P[batch*16] (row-major, symmetric; the kernel reads the upper triangle) are
  * read at launch start and written at the end.  q, r: setQ/setR scales (:12-15).
  * A record whose dt word has PEKF_MISSING_MAG_BIT set runs Prediction only (X = z, P = P-).
- * traj (optional, NULL to skip): X after every step, [n_steps][batch][4]. */
+ * traj (optional, NULL to skip): X after every step, [n_steps][batch][4].
+ * flags: 0 or PEKF_RUN_MIXED_PRECISION. */
 int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
                  const void *plane_gd, const void *plane_am, const void *plane_my,
                  const double *refs, double *X, double *P, double q, double r, double *traj,
-                 void *stream);
+                 uint32_t flags, void *stream);
 
 /* X = [1,0,0,0], P = I for every filter (main_file.py:23,26). */
 int pekf_reset_state_dev(int64_t batch, double *X, double *P, void *stream);

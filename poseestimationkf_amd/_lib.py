@@ -19,6 +19,7 @@ PEKF_ERR_HIP = 2
 PEKF_ERR_SINGULAR = 3
 PEKF_ERR_NODEVICE = 4
 MISSING_MAG_BIT = 0x80000000
+RUN_MIXED_PRECISION = 0x1
 
 
 class PekfError(RuntimeError):
@@ -71,7 +72,7 @@ SIGNATURES = {
     "pekf_wahba_rotation": [_i64] + [_dp] * 7,
     "pekf_wahba_quaternion": [_i64] + [_dp] * 7,
     "pekf_rotmat_to_quat": [_i64, _dp, _dp],
-    "pekf_run_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp],
+    "pekf_run_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _vp, _u32, _vp],
     "pekf_reset_state_dev": [_i64, _vp, _vp, _vp],
     "pekf_synth_dev": [_i64, _i64, _i64, _u32, _int, _dp, _dbl, _vp, _vp, _vp, _vp, _vp],
 }

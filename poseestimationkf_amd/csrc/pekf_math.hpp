@@ -273,38 +273,50 @@ PEKF_DEV void rotm_to_quat_fast(const double *M, double *q) {
 // so only the symmetric S^-1 is formed (no general 4x4 products with K).
 
 // Symmetric 4x4 stored as its upper triangle: 00 01 02 03 11 12 13 22 23 33
-struct Sym4 {
-    double a00, a01, a02, a03, a11, a12, a13, a22, a23, a33;
+template <typename T>
+struct Sym4T {
+    T a00, a01, a02, a03, a11, a12, a13, a22, a23, a33;
 };
+using Sym4 = Sym4T<double>;
+
+// single-precision reciprocal for the opt-in mixed-precision covariance path: v_rcp_f32
+// (1 ulp) + one Newton step
+template <bool FAST>
+PEKF_DEV float recip(float x) {
+    if (!FAST) return 1.0f / x;
+    float r = __builtin_amdgcn_rcpf(x);
+    return fmaf(r, fmaf(-x, r, 1.0f), r);
+}
 
 // A P A^T + g (|x|^2 I - x x^T), A = Omega(h), h = w/2 (ExtendedKalmanFilter.py:44-47,52-55,61)
-PEKF_DEV Sym4 propagate_cov(const Sym4 &P, const double *h, const double *x, double g) {
-    const double w0 = h[0], w1 = h[1], w2 = h[2];
+template <typename T>
+PEKF_DEV Sym4T<T> propagate_cov(const Sym4T<T> &P, const T *h, const T *x, T g) {
+    const T w0 = h[0], w1 = h[1], w2 = h[2];
     // T = Omega P (full 4x4), rows of Omega: [0,-w0,-w1,-w2] [w0,0,w2,-w1] [w1,-w2,0,w0] [w2,w1,-w0,0]
-    const double p[4][4] = {{P.a00, P.a01, P.a02, P.a03},
+    const T p[4][4] = {{P.a00, P.a01, P.a02, P.a03},
                             {P.a01, P.a11, P.a12, P.a13},
                             {P.a02, P.a12, P.a22, P.a23},
                             {P.a03, P.a13, P.a23, P.a33}};
-    double T[4][4];
+    T t[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        T[0][j] = -w0 * p[1][j] - w1 * p[2][j] - w2 * p[3][j];
-        T[1][j] = w0 * p[0][j] + w2 * p[2][j] - w1 * p[3][j];
-        T[2][j] = w1 * p[0][j] - w2 * p[1][j] + w0 * p[3][j];
-        T[3][j] = w2 * p[0][j] + w1 * p[1][j] - w0 * p[2][j];
+        t[0][j] = -w0 * p[1][j] - w1 * p[2][j] - w2 * p[3][j];
+        t[1][j] = w0 * p[0][j] + w2 * p[2][j] - w1 * p[3][j];
+        t[2][j] = w1 * p[0][j] - w2 * p[1][j] + w0 * p[3][j];
+        t[3][j] = w2 * p[0][j] + w1 * p[1][j] - w0 * p[2][j];
     }
     // M = T Omega^T: M_ij = T_i . Omega_j
-    auto m = [&](int i, int j) -> double {
+    auto m = [&](int i, int j) -> T {
         switch (j) {
-            case 0: return -w0 * T[i][1] - w1 * T[i][2] - w2 * T[i][3];
-            case 1: return w0 * T[i][0] + w2 * T[i][2] - w1 * T[i][3];
-            case 2: return w1 * T[i][0] - w2 * T[i][1] + w0 * T[i][3];
-            default: return w2 * T[i][0] + w1 * T[i][1] - w0 * T[i][2];
+            case 0: return -w0 * t[i][1] - w1 * t[i][2] - w2 * t[i][3];
+            case 1: return w0 * t[i][0] + w2 * t[i][2] - w1 * t[i][3];
+            case 2: return w1 * t[i][0] - w2 * t[i][1] + w0 * t[i][3];
+            default: return w2 * t[i][0] + w1 * t[i][1] - w0 * t[i][2];
         }
     };
-    const double n2 = x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
-    const double gx0 = g * x[0], gx1 = g * x[1], gx2 = g * x[2], gx3 = g * x[3];
-    Sym4 o;
+    const T n2 = x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
+    const T gx0 = g * x[0], gx1 = g * x[1], gx2 = g * x[2], gx3 = g * x[3];
+    Sym4T<T> o;
     o.a00 = m(0, 0) + g * (n2 - x[0] * x[0]);
     o.a01 = m(0, 1) - gx0 * x[1];
     o.a02 = m(0, 2) - gx0 * x[2];
@@ -320,26 +332,26 @@ PEKF_DEV Sym4 propagate_cov(const Sym4 &P, const double *h, const double *x, dou
 }
 
 // Inverse of an SPD 4x4 by LDL^T (no pivoting needed: S = P- + rI, r > 0).
-template <bool FAST = true>
-PEKF_DEV Sym4 spd_inverse(const Sym4 &S) {
-    const double i0 = recip<FAST>(S.a00);
-    const double l10 = S.a01 * i0, l20 = S.a02 * i0, l30 = S.a03 * i0;
-    const double d1 = S.a11 - l10 * S.a01, i1 = recip<FAST>(d1);
-    const double a21 = S.a12 - l20 * S.a01, a31 = S.a13 - l30 * S.a01;
-    const double l21 = a21 * i1, l31 = a31 * i1;
-    const double d2 = S.a22 - l20 * S.a02 - l21 * a21, i2 = recip<FAST>(d2);
-    const double a32 = S.a23 - l30 * S.a02 - l31 * a21;
-    const double l32 = a32 * i2;
-    const double d3 = S.a33 - l30 * S.a03 - l31 * a31 - l32 * a32, i3 = recip<FAST>(d3);
+template <typename T, bool FAST = true>
+PEKF_DEV Sym4T<T> spd_inverse(const Sym4T<T> &S) {
+    const T i0 = recip<FAST>(S.a00);
+    const T l10 = S.a01 * i0, l20 = S.a02 * i0, l30 = S.a03 * i0;
+    const T d1 = S.a11 - l10 * S.a01, i1 = recip<FAST>(d1);
+    const T a21 = S.a12 - l20 * S.a01, a31 = S.a13 - l30 * S.a01;
+    const T l21 = a21 * i1, l31 = a31 * i1;
+    const T d2 = S.a22 - l20 * S.a02 - l21 * a21, i2 = recip<FAST>(d2);
+    const T a32 = S.a23 - l30 * S.a02 - l31 * a21;
+    const T l32 = a32 * i2;
+    const T d3 = S.a33 - l30 * S.a03 - l31 * a31 - l32 * a32, i3 = recip<FAST>(d3);
     // N = L^-1 (unit lower)
-    const double n10 = -l10;
-    const double n21 = -l21, n20 = -(l20 + l21 * n10);
-    const double n32 = -l32, n31 = -(l31 + l32 * n21), n30 = -(l30 + l31 * n10 + l32 * n20);
+    const T n10 = -l10;
+    const T n21 = -l21, n20 = -(l20 + l21 * n10);
+    const T n32 = -l32, n31 = -(l31 + l32 * n21), n30 = -(l30 + l31 * n10 + l32 * n20);
     // S^-1 = N^T D^-1 N
-    const double m30 = n30 * i3, m31 = n31 * i3, m32 = n32 * i3;
-    const double m20 = n20 * i2, m21 = n21 * i2;
-    const double m10 = n10 * i1;
-    Sym4 o;
+    const T m30 = n30 * i3, m31 = n31 * i3, m32 = n32 * i3;
+    const T m20 = n20 * i2, m21 = n21 * i2;
+    const T m10 = n10 * i1;
+    Sym4T<T> o;
     o.a33 = i3;
     o.a23 = m32;
     o.a22 = i2 + n32 * m32;

@@ -9,6 +9,8 @@
 // and reference vectors.  The next step's record is loaded before the current step's
 // arithmetic so its latency hides under ~600 FP64 instructions of work.
 // No MFMA: every contraction is 4x4 / 3x3 per lane.
+#include <type_traits>
+
 #include "pekf_internal.hpp"
 #include "pekf_math.hpp"
 
@@ -31,7 +33,10 @@ __device__ __forceinline__ Rec load_rec(const float4 *__restrict__ gd, const flo
     return r;
 }
 
-template <bool TRAJ>
+// MIXED = false: every operation in FP64 (the headline path).
+// MIXED = true (opt-in, PEKF_RUN_MIXED_PRECISION): the covariance recursion (P-, S^-1, K, P)
+// in FP32 while RK4, Wahba, R->q and the X update stay FP64 (~2e-8 vs FP64).
+template <bool TRAJ, bool MIXED>
 __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_steps, int64_t window,
                                                    int64_t step0, const float4 *__restrict__ gd,
                                                    const float4 *__restrict__ am,
@@ -39,6 +44,7 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
                                                    const double *__restrict__ refs,
                                                    double *__restrict__ Xio, double *__restrict__ Pio,
                                                    double qs, double rs, double *__restrict__ traj) {
+    using PT = typename std::conditional<MIXED, float, double>::type;
     const int64_t b = (int64_t)blockIdx.x * kRunBlock + threadIdx.x;
     if (b >= batch) return;
 
@@ -49,11 +55,12 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
         const double m0[3] = {refs[6 * b + 3], refs[6 * b + 4], refs[6 * b + 5]};
         make_frame<true>(a0, m0, Wf);
     }
-    const double g = 0.25 * qs;       // Jb Q Jb^T = (q/4)(|X|^2 I - X X^T)
-    const double r2 = rs * rs;
+    const PT g = (PT)(0.25 * qs);     // Jb Q Jb^T = (q/4)(|X|^2 I - X X^T)
+    const PT rp = (PT)rs, r2 = (PT)(rs * rs);
     double x[4] = {Xio[4 * b + 0], Xio[4 * b + 1], Xio[4 * b + 2], Xio[4 * b + 3]};
     const double *pp = Pio + 16 * b;
-    Sym4 P = {pp[0], pp[1], pp[2], pp[3], pp[5], pp[6], pp[7], pp[10], pp[11], pp[15]};
+    Sym4T<PT> P = {(PT)pp[0], (PT)pp[1], (PT)pp[2], (PT)pp[3], (PT)pp[5],
+                   (PT)pp[6], (PT)pp[7], (PT)pp[10], (PT)pp[11], (PT)pp[15]};
 
     int64_t row = step0 % window;
     Rec cur = load_rec(gd, am, my, row * batch + b);
@@ -68,9 +75,11 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
         const double dt_ns = (double)(word & 0x7FFFFFFFu);
 
         // ---- Prediction (ExtendedKalmanFilter.py:58-68) ----
-        const Sym4 Pm = propagate_cov(P, hw, x, g);  // Jb from the prior X (:60)
+        const PT hp[3] = {(PT)hw[0], (PT)hw[1], (PT)hw[2]};
+        const PT xp[4] = {(PT)x[0], (PT)x[1], (PT)x[2], (PT)x[3]};
+        const Sym4T<PT> Pm = propagate_cov<PT>(P, hp, xp, g);  // Jb from the prior X (:60)
         double z[4];
-        rk4_closed(x, dt_ns, hw, z);                 // (:62)
+        rk4_closed(x, dt_ns, hw, z);                            // (:62)
 
         if (word & PEKF_MISSING_MAG_BIT) {
             // Wahba-skip: no Correction for this record (X = z, P = P-)
@@ -78,9 +87,9 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
             P = Pm;
         } else {
             // S = P- + rI; K = P- S^-1 = I - r S^-1  (:63-66)
-            const Sym4 S = {Pm.a00 + rs, Pm.a01, Pm.a02, Pm.a03, Pm.a11 + rs,
-                            Pm.a12, Pm.a13, Pm.a22 + rs, Pm.a23, Pm.a33 + rs};
-            const Sym4 Si = spd_inverse<true>(S);
+            const Sym4T<PT> S = {Pm.a00 + rp, Pm.a01, Pm.a02, Pm.a03, Pm.a11 + rp,
+                                 Pm.a12, Pm.a13, Pm.a22 + rp, Pm.a23, Pm.a33 + rp};
+            const Sym4T<PT> Si = spd_inverse<PT, true>(S);
 
             // ---- Correction (ExtendedKalmanFilter.py:70-80) ----
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
@@ -94,17 +103,20 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
             const double cmp = y[0] * z[0] + y[1] * z[1] + y[2] * z[2] + y[3] * z[3];
             const double sg = cmp < 0.0 ? -1.0 : 1.0;     // (:73-75)
             y[0] *= sg; y[1] *= sg; y[2] *= sg; y[3] *= sg;
-            const double e0 = y[0] - z[0], e1 = y[1] - z[1], e2 = y[2] - z[2], e3 = y[3] - z[3];
+            const PT e0 = (PT)(y[0] - z[0]), e1 = (PT)(y[1] - z[1]);
+            const PT e2 = (PT)(y[2] - z[2]), e3 = (PT)(y[3] - z[3]);
             // X = z + K e = Y - r S^-1 e (:77), normalised (:79)
-            const double x0 = y[0] - rs * (Si.a00 * e0 + Si.a01 * e1 + Si.a02 * e2 + Si.a03 * e3);
-            const double x1 = y[1] - rs * (Si.a01 * e0 + Si.a11 * e1 + Si.a12 * e2 + Si.a13 * e3);
-            const double x2 = y[2] - rs * (Si.a02 * e0 + Si.a12 * e1 + Si.a22 * e2 + Si.a23 * e3);
-            const double x3 = y[3] - rs * (Si.a03 * e0 + Si.a13 * e1 + Si.a23 * e2 + Si.a33 * e3);
+            const double u0 = Si.a00 * e0 + Si.a01 * e1 + Si.a02 * e2 + Si.a03 * e3;
+            const double u1 = Si.a01 * e0 + Si.a11 * e1 + Si.a12 * e2 + Si.a13 * e3;
+            const double u2 = Si.a02 * e0 + Si.a12 * e1 + Si.a22 * e2 + Si.a23 * e3;
+            const double u3 = Si.a03 * e0 + Si.a13 * e1 + Si.a23 * e2 + Si.a33 * e3;
+            const double x0 = y[0] - rs * u0, x1 = y[1] - rs * u1;
+            const double x2 = y[2] - rs * u2, x3 = y[3] - rs * u3;
             const double in = rsqrt<true>(x0 * x0 + x1 * x1 + x2 * x2 + x3 * x3);
             x[0] = x0 * in; x[1] = x1 * in; x[2] = x2 * in; x[3] = x3 * in;
             // P = P- - K P- = r K = r I - r^2 S^-1 (:78)
-            P = {rs - r2 * Si.a00, -r2 * Si.a01, -r2 * Si.a02, -r2 * Si.a03, rs - r2 * Si.a11,
-                 -r2 * Si.a12, -r2 * Si.a13, rs - r2 * Si.a22, -r2 * Si.a23, rs - r2 * Si.a33};
+            P = {rp - r2 * Si.a00, -r2 * Si.a01, -r2 * Si.a02, -r2 * Si.a03, rp - r2 * Si.a11,
+                 -r2 * Si.a12, -r2 * Si.a13, rp - r2 * Si.a22, -r2 * Si.a23, rp - r2 * Si.a33};
         }
         if (TRAJ) {
             double2 *o = reinterpret_cast<double2 *>(traj + (t * batch + b) * 4);
@@ -116,11 +128,10 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     }
     Xio[4 * b + 0] = x[0]; Xio[4 * b + 1] = x[1]; Xio[4 * b + 2] = x[2]; Xio[4 * b + 3] = x[3];
     double *po = Pio + 16 * b;
-    const Sym4 &Po = P;
-    po[0] = Po.a00; po[1] = Po.a01; po[2] = Po.a02; po[3] = Po.a03;
-    po[4] = Po.a01; po[5] = Po.a11; po[6] = Po.a12; po[7] = Po.a13;
-    po[8] = Po.a02; po[9] = Po.a12; po[10] = Po.a22; po[11] = Po.a23;
-    po[12] = Po.a03; po[13] = Po.a13; po[14] = Po.a23; po[15] = Po.a33;
+    po[0] = P.a00; po[1] = P.a01; po[2] = P.a02; po[3] = P.a03;
+    po[4] = P.a01; po[5] = P.a11; po[6] = P.a12; po[7] = P.a13;
+    po[8] = P.a02; po[9] = P.a12; po[10] = P.a22; po[11] = P.a23;
+    po[12] = P.a03; po[13] = P.a13; po[14] = P.a23; po[15] = P.a33;
 }
 
 __global__ __launch_bounds__(kRunBlock) void k_reset(int64_t batch, double *X, double *P) {
@@ -140,7 +151,7 @@ extern "C" {
 int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
                  const void *plane_gd, const void *plane_am, const void *plane_my,
                  const double *refs, double *X, double *P, double q, double r, double *traj,
-                 void *stream) {
+                 uint32_t flags, void *stream) {
     PEKF_CHECK_ARG(batch >= 0 && n_steps >= 0, "negative size");
     if (batch == 0 || n_steps == 0) return PEKF_OK;
     PEKF_CHECK_ARG(window > 0 && step0 >= 0, "window must be > 0 and step0 >= 0");
@@ -153,12 +164,17 @@ int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
     const auto *gd = static_cast<const float4 *>(plane_gd);
     const auto *am = static_cast<const float4 *>(plane_am);
     const auto *my = static_cast<const float2 *>(plane_my);
-    if (traj)
-        hipLaunchKernelGGL(k_run<true>, grid, block, 0, as_stream(stream), batch, n_steps, window,
-                           step0, gd, am, my, refs, X, P, q, r, traj);
-    else
-        hipLaunchKernelGGL(k_run<false>, grid, block, 0, as_stream(stream), batch, n_steps, window,
-                           step0, gd, am, my, refs, X, P, q, r, nullptr);
+    PEKF_CHECK_ARG((flags & ~(uint32_t)PEKF_RUN_MIXED_PRECISION) == 0, "unknown flags");
+    const bool mixed = flags & PEKF_RUN_MIXED_PRECISION;
+#define PEKF_LAUNCH_RUN(TR, MX)                                                                     \
+    hipLaunchKernelGGL((k_run<TR, MX>), grid, block, 0, as_stream(stream), batch, n_steps, window, \
+                       step0, gd, am, my, refs, X, P, q, r, traj)
+    if (traj) {
+        if (mixed) PEKF_LAUNCH_RUN(true, true); else PEKF_LAUNCH_RUN(true, false);
+    } else {
+        if (mixed) PEKF_LAUNCH_RUN(false, true); else PEKF_LAUNCH_RUN(false, false);
+    }
+#undef PEKF_LAUNCH_RUN
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_run");
     return PEKF_OK;

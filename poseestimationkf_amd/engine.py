@@ -10,7 +10,7 @@ import ctypes
 import numpy as np
 
 from . import synth
-from ._lib import check, dptr, f64, lib
+from ._lib import RUN_MIXED_PRECISION, check, dptr, f64, lib
 
 
 # ------------------------------------------------------------------ device plumbing
@@ -173,9 +173,13 @@ class BatchedEKF:
     Prediction + Correction for every record.  `run` advances all filters n_steps records.
     """
 
-    def __init__(self, batch, q=1.0, r=0.1):
+    def __init__(self, batch, q=1.0, r=0.1, precision="f64"):
+        """precision: "f64" (default, as the reference) or "mixed" (covariance path in f32)."""
+        if precision not in ("f64", "mixed"):
+            raise ValueError("precision must be 'f64' or 'mixed'")
         self.batch = int(batch)
         self.q, self.r = float(q), float(r)
+        self.flags = RUN_MIXED_PRECISION if precision == "mixed" else 0
         self.X = DeviceBuffer(32 * self.batch)
         self.P = DeviceBuffer(128 * self.batch)
         self.reset()
@@ -197,7 +201,8 @@ class BatchedEKF:
         assert win.batch == self.batch
         check(lib.pekf_run_dev(self.batch, int(n_steps), win.window, int(step0), win.gd.ptr,
                                win.am.ptr, win.my.ptr, win.refs.ptr, self.X.ptr, self.P.ptr,
-                               self.q, self.r, traj.ptr if traj is not None else None, stream))
+                               self.q, self.r, traj.ptr if traj is not None else None, self.flags,
+                               stream))
 
     def run(self, win: IMUWindow, n_steps=None, step0=0, want_traj=False):
         n_steps = win.window if n_steps is None else int(n_steps)

@@ -18,7 +18,7 @@ def shard_range(global_batch, rank, world):
     return rank * per, per
 
 
-def gather_quaternions(x_local, rank, world, dst=0):
+def gather_quaternions(x_local, rank, world, dst=0, force_collective=False):
     """Gather every rank's (B_local, 4) float64 quaternion tensor to `dst`.
 
     Returns the (world*B_local, 4) tensor on dst (rows ordered by filter id) and None elsewhere.
@@ -27,7 +27,7 @@ def gather_quaternions(x_local, rank, world, dst=0):
     import torch
     import torch.distributed as dist
 
-    if world == 1:
+    if world == 1 and not force_collective:
         return x_local
     bufs = [torch.empty_like(x_local) for _ in range(world)] if rank == dst else None
     dist.gather(x_local, gather_list=bufs, dst=dst)

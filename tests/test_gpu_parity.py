@@ -105,6 +105,18 @@ def test_fused_run_matches_reference_trajectory(eng, traj, tag):
     assert err < PREC_GUARD
 
 
+@pytest.mark.parametrize("tag", ["", "miss_"])
+def test_fused_mixed_precision_within_tolerance(eng, traj, tag):
+    """Opt-in covariance-in-FP32 path: quaternions must still meet the 1e-5 contract."""
+    win = eng.IMUWindow.from_planes(traj[tag + "gd"], traj[tag + "am"], traj[tag + "my"],
+                                    traj[tag + "acc0"], traj[tag + "mag0"])
+    tr = eng.BatchedEKF(win.batch, precision="mixed").run(win, want_traj=True)
+    err = _maxerr(tr, traj[tag + "traj"])
+    print("mixed precision vs reference (%s): max |dq| = %.3e" % (tag or "full", err))
+    assert err < ATOL_Q
+    assert err < 1e-6
+
+
 def test_device_generator_bit_identical_to_host(eng):
     K, W = 1000, 48
     win = eng.IMUWindow(K, W).synthesize(seed=synth.DEFAULT_SEED, first_filter=123, missing=True)
