@@ -213,8 +213,8 @@ def main():
         value = steps_total / elapsed
         k_s = float(np.mean(kms)) / 1e3
         achieved = B * N * REC_BYTES / k_s / 1e9
-        flop = FLOP_PER_STEP
-        traffic, tsrc = measured_traffic(B, N)
+        flop = ISA_COUNTS[args.precision]["flop"]
+        traffic, tsrc = measured_traffic(B, N) if args.precision == "f64" else (None, None)
         out = {
             "metric": "EKF steps/sec (predict+Wahba+update) at batch=1M; HBM-roofline %",
             "value": value,
@@ -239,7 +239,7 @@ def main():
                                             "rocprofv3 --pmc pass of this command)") if tsrc else None,
                          "kernel": "k_run<false> (pekf_run_dev)", "kernel_ms": k_s * 1e3,
                          "bytes_per_launch": B * N * REC_BYTES},
-            "fp64_valu": {"flop_per_step": flop, "fp64_instr_per_step": FP64_INSTR_PER_STEP,
+            "fp64_valu": {"flop_per_step": flop, "fp64_instr_per_step": ISA_COUNTS[args.precision]["fp64_instr"],
                           "achieved_tflops": B * N * flop / k_s / 1e12, "peak_tflops": FP64_PEAK_TFLOPS,
                           "frac": B * N * flop / k_s / 1e12 / FP64_PEAK_TFLOPS,
                           "valu_busy_pmc": tsrc[1].get("valu_busy") if tsrc else None,
@@ -258,10 +258,12 @@ def main():
 
 
 # FP64 work per filter-step of the fused kernel, counted from its gfx950 ISA hot loop by
-# scripts/isa_count.py (DESIGN.md "FP64 budget"): 415 FP64 VALU instructions, of which the
-# arithmetic ones are 619 FLOP with an FMA counted as 2.
-FLOP_PER_STEP = 619
-FP64_INSTR_PER_STEP = 415
+# scripts/isa_count.py (DESIGN.md "FP64 budget"): FP64 VALU instructions, and the FLOP of
+# the arithmetic ones with an FMA counted as 2.
+ISA_COUNTS = {"f64": {"flop": 567, "fp64_instr": 383},
+              "mixed": {"flop": 282, "fp64_instr": 228}}  # mixed: + ~170 f32 instructions
+FLOP_PER_STEP = ISA_COUNTS["f64"]["flop"]
+FP64_INSTR_PER_STEP = ISA_COUNTS["f64"]["fp64_instr"]
 
 
 def measured_traffic(batch, records):

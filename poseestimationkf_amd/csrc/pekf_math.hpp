@@ -153,18 +153,20 @@ PEKF_DEV void rotm_to_quat(const double *M, double *q) {
 }
 
 // ------------------------------- reciprocal / rsqrt ------------------------------------------
-// FAST = false: IEEE division and sqrt (per-call kernels).  FAST = true: the hardware
-// v_rcp_f64 / v_rsq_f64 seeds plus two Newton steps each (4 FMAs / 8 ops), accurate to
-// ~1 ulp for the positive, normal operands of this model, without the scale / fixup
-// sequences of a correctly rounded division (fused kernel; DESIGN.md "FP64 budget").
+// FAST = false: IEEE division and sqrt (per-call kernels).  FAST = true (fused kernel): the
+// hardware v_rcp_f64 / v_rsq_f64 seed (measured on MI355X: <= 5.6e-8 relative) plus ONE Newton
+// step, measured <= 11 ulp (rcp) / <= 19 ulp (rsq), i.e. <= 4.2e-15 relative, over 1e-6..1e6
+// (scripts/probe_fp64.hip); a second step would give 0 / 2 ulp for 4 more FP64 ops each.
+// No scale / fixup sequences: operands here are positive and normal (DESIGN.md "FP64 budget").
+constexpr int kNewtonSteps = 1;
+
 template <bool FAST>
 PEKF_DEV double recip(double x) {
     if (!FAST) return 1.0 / x;
     double r = __builtin_amdgcn_rcp(x);
-    double e = fma(-x, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(-x, r, 1.0);
-    return fma(r, e, r);
+#pragma unroll
+    for (int it = 0; it < kNewtonSteps; ++it) r = fma(r, fma(-x, r, 1.0), r);
+    return r;
 }
 
 template <bool FAST>
@@ -172,7 +174,7 @@ PEKF_DEV double rsqrt(double x) {
     if (!FAST) return 1.0 / sqrt(x);
     double y = __builtin_amdgcn_rsq(x);
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
+    for (int it = 0; it < kNewtonSteps; ++it) {
         const double e = fma(-x * y, y, 1.0);  // 1 - x y^2
         y = fma(y, 0.5 * e, y);
     }
