@@ -36,6 +36,8 @@ extern "C" {
 #define PEKF_ERR_HIP 2      /* HIP runtime error (message has hipGetErrorString)        */
 #define PEKF_ERR_SINGULAR 3 /* S = P + R singular in predict: np.linalg.LinAlgError      */
 #define PEKF_ERR_NODEVICE 4 /* no HIP device visible                                     */
+#define PEKF_ERR_SVD 5      /* non-finite Wahba matrix B: np.linalg.svd raises LinAlgError  */
+                            /* "SVD did not converge" (Wahba.py:14)                         */
 
 /* Bit 31 of a stream record's dt word: magnetometer sample missing ("Wahba-skip"). */
 #define PEKF_MISSING_MAG_BIT 0x80000000u
@@ -104,7 +106,8 @@ int pekf_predict_dev(int64_t n, const double *gyro, const double *dt_ns, const d
 
 /* KalmanFilter.Correction(Mag, Acc, z_k, P_k, K_k), ExtendedKalmanFilter.py:70-80, with the
  * filter's Wahba reference vectors acc0/mag0 (Wahba.__init__, Wahba.py:4-6).
- * mag[n*3], acc[n*3], z[n*4], P[n*16], K[n*16], acc0[n*3], mag0[n*3] -> X[n*4], P_out[n*16]. */
+ * mag[n*3], acc[n*3], z[n*4], P[n*16], K[n*16], acc0[n*3], mag0[n*3] -> X[n*4], P_out[n*16].
+ * Returns PEKF_ERR_SVD if any item's B is non-finite (outputs of that item are NaN). */
 int pekf_correct(int64_t n, const double *mag, const double *acc, const double *z,
                  const double *P, const double *K, const double *acc0, const double *mag0,
                  double *X, double *P_out);
@@ -112,7 +115,8 @@ int pekf_correct_dev(int64_t n, const double *mag, const double *acc, const doub
                      const double *P, const double *K, const double *acc0, const double *mag0,
                      double *X, double *P_out, void *stream);
 
-/* Wahba.getRotation(acc, mag, k_acc, k_mag), Wahba.py:8-17 -> R[n*9] (closed form) */
+/* Wahba.getRotation(acc, mag, k_acc, k_mag), Wahba.py:8-17 -> R[n*9] (closed form).
+ * Returns PEKF_ERR_SVD if any item's B is non-finite, as np.linalg.svd raises there. */
 int pekf_wahba_rotation(int64_t n, const double *acc0, const double *mag0, const double *acc,
                         const double *mag, const double *k_acc, const double *k_mag, double *R);
 /* Wahba.getQuarternion(acc, mag, k_acc, k_mag), Wahba.py:49-50 -> q[n*4] */
@@ -131,6 +135,8 @@ int pekf_rotmat_to_quat(int64_t n, const double *M, double *q);
  * X[batch*4], P[batch*16] (row-major, symmetric; the kernel reads the upper triangle) are
  * read at launch start and written at the end.  q, r: setQ/setR scales (:12-15).
  * A record whose dt word has PEKF_MISSING_MAG_BIT set runs Prediction only (X = z, P = P-).
+ * A non-finite sample cannot raise per filter inside a batch: that filter's X and P become NaN
+ * (the reference raises LinAlgError from np.linalg.svd at that record).
  * traj (optional, NULL to skip): X after every step, [n_steps][batch][4].
  * flags: 0 or PEKF_RUN_MIXED_PRECISION. */
 int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,

@@ -18,6 +18,7 @@ PEKF_ERR_INVALID = 1
 PEKF_ERR_HIP = 2
 PEKF_ERR_SINGULAR = 3
 PEKF_ERR_NODEVICE = 4
+PEKF_ERR_SVD = 5
 MISSING_MAG_BIT = 0x80000000
 RUN_MIXED_PRECISION = 0x1
 
@@ -107,6 +108,8 @@ def check(status):
     msg = last_error()
     if status == PEKF_ERR_SINGULAR:
         raise np.linalg.LinAlgError(msg or "Singular matrix")
+    if status == PEKF_ERR_SVD:
+        raise np.linalg.LinAlgError(msg or "SVD did not converge")
     if status == PEKF_ERR_NODEVICE:
         raise NoDeviceError(status, msg)
     raise PekfError(status, msg)

@@ -111,7 +111,7 @@ PEKF_DEV bool inverse4(const double *m, double *inv) {
     const double c1 = m[8] * m[14] - m[12] * m[10];
     const double c0 = m[8] * m[13] - m[12] * m[9];
     const double det = s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0;
-    if (det == 0.0 || !isfinite(det)) return false;
+    if (det == 0.0) return false;  // LAPACK raises only on an exactly singular pivot; NaN/inf propagate
     const double id = 1.0 / det;
     inv[0] = (m[5] * c5 - m[6] * c4 + m[7] * c3) * id;
     inv[1] = (-m[1] * c5 + m[2] * c4 - m[3] * c3) * id;
@@ -235,6 +235,18 @@ PEKF_DEV void wahba_rotation(const Frame &W, const Frame &V, double ka, double k
 #pragma unroll
         for (int j = 0; j < 3; ++j) R[i * 3 + j] = g0 * V.e1[j] + g1 * V.e2[j] + g2 * V.u3[j];
     }
+}
+
+// True iff every entry of B = ka acc0 acc^T + km mag0 mag^T is finite (np.linalg.svd raises
+// LinAlgError "SVD did not converge" otherwise, Wahba.py:14).
+PEKF_DEV bool wahba_b_finite(const double *acc0, const double *mag0, const double *acc,
+                             const double *mag, double ka, double km) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) ok &= isfinite(ka * (acc0[i] * acc[j]) + km * (mag0[i] * mag[j]));
+    return ok;
 }
 
 PEKF_DEV void wahba_rotation_vectors(const double *acc0, const double *mag0, const double *acc,

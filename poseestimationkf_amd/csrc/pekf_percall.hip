@@ -84,11 +84,13 @@ __global__ __launch_bounds__(kBlock) void k_correct(int64_t n, const double *mag
                                                    const double *acc, const double *z,
                                                    const double *P, const double *K,
                                                    const double *acc0, const double *mag0,
-                                                   double *X, double *Pout) {
+                                                   double *X, double *Pout, int *svd_fail) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const double *a = acc + 3 * i, *zz = z + 4 * i, *kk = K + 16 * i, *pp = P + 16 * i;
     const double ka = fabs(a[2]);
+    if (svd_fail && !wahba_b_finite(acc0 + 3 * i, mag0 + 3 * i, a, mag + 3 * i, ka, 1.0 - ka))
+        atomicOr(svd_fail, 1);
     double R[9], y[4], e[4], ke[4], kp[16], x[4];
     wahba_rotation_vectors(acc0 + 3 * i, mag0 + 3 * i, a, mag + 3 * i, ka, 1.0 - ka, R);
     rotm_to_quat(R, y);
@@ -114,9 +116,11 @@ template <bool QUAT>
 __global__ __launch_bounds__(kBlock) void k_wahba(int64_t n, const double *acc0,
                                                  const double *mag0, const double *acc,
                                                  const double *mag, const double *ka,
-                                                 const double *km, double *out) {
+                                                 const double *km, double *out, int *svd_fail) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
+    if (svd_fail && !wahba_b_finite(acc0 + 3 * i, mag0 + 3 * i, acc + 3 * i, mag + 3 * i, ka[i], km[i]))
+        atomicOr(svd_fail, 1);
     double R[9];
     wahba_rotation_vectors(acc0 + 3 * i, mag0 + 3 * i, acc + 3 * i, mag + 3 * i, ka[i], km[i], R);
     if (QUAT) {
@@ -176,7 +180,7 @@ int pekf_correct_dev(int64_t n, const double *mag, const double *acc, const doub
     if (n == 0) return PEKF_OK;
     PEKF_CHECK_ARG(mag && acc && z && P && K && acc0 && mag0 && X && P_out, "null pointer");
     hipLaunchKernelGGL(k_correct, PEKF_GRID(n), 0, as_stream(stream), n, mag, acc, z, P, K, acc0,
-                       mag0, X, P_out);
+                       mag0, X, P_out, nullptr);
     return launched("k_correct");
 }
 
@@ -299,9 +303,13 @@ int pekf_correct(int64_t n, const double *mag, const double *acc, const double *
     hipLaunchKernelGGL(k_correct, PEKF_GRID(n), 0, s.stream(), n, D(const double *, in[0]),
                        D(const double *, in[1]), D(const double *, in[2]), D(const double *, in[3]),
                        D(const double *, in[4]), D(const double *, in[5]), D(const double *, in[6]),
-                       D(double *, out[0]), D(double *, out[1]));
+                       D(double *, out[0]), D(double *, out[1]), s.dev_flag());
     if (int st = launched("k_correct")) return st;
-    return s.stage_out({{X, 4 * b}, {P_out, 16 * b}}, out);
+    int fail = 0;
+    PEKF_HIP(hipMemcpyAsync(&fail, s.dev_flag(), sizeof(int), hipMemcpyDeviceToHost, s.stream()));
+    if (int st = s.stage_out({{X, 4 * b}, {P_out, 16 * b}}, out)) return st;
+    if (fail) return set_error(PEKF_ERR_SVD, "SVD did not converge");
+    return PEKF_OK;
 }
 
 static int wahba_host(bool quat, int64_t n, const double *acc0, const double *mag0,
@@ -321,13 +329,19 @@ static int wahba_host(bool quat, int64_t n, const double *acc0, const double *ma
     if (quat)
         hipLaunchKernelGGL(k_wahba<true>, PEKF_GRID(n), 0, s.stream(), n, D(const double *, in[0]),
                            D(const double *, in[1]), D(const double *, in[2]), D(const double *, in[3]),
-                           D(const double *, in[4]), D(const double *, in[5]), D(double *, out[0]));
+                           D(const double *, in[4]), D(const double *, in[5]), D(double *, out[0]),
+                           s.dev_flag());
     else
         hipLaunchKernelGGL(k_wahba<false>, PEKF_GRID(n), 0, s.stream(), n, D(const double *, in[0]),
                            D(const double *, in[1]), D(const double *, in[2]), D(const double *, in[3]),
-                           D(const double *, in[4]), D(const double *, in[5]), D(double *, out[0]));
+                           D(const double *, in[4]), D(const double *, in[5]), D(double *, out[0]),
+                           s.dev_flag());
     if (int st = launched("k_wahba")) return st;
-    return s.stage_out({{res, ob}}, out);
+    int fail = 0;
+    PEKF_HIP(hipMemcpyAsync(&fail, s.dev_flag(), sizeof(int), hipMemcpyDeviceToHost, s.stream()));
+    if (int st = s.stage_out({{res, ob}}, out)) return st;
+    if (fail) return set_error(PEKF_ERR_SVD, "SVD did not converge");
+    return PEKF_OK;
 }
 
 int pekf_wahba_rotation(int64_t n, const double *acc0, const double *mag0, const double *acc,

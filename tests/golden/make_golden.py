@@ -14,6 +14,7 @@ Outputs (tests/golden/):
   traj.npz         8 filters x 1500 synthetic steps (+ a Wahba-skip variant), inputs and X trajectories
   c1_log.txt.gz    config-1 trace in the C++ log format (1550 steps)
   c1_xk.npy        X_k list produced by main_file.py (unchanged) on that log
+  edge.npz         raw-unit inputs (k_mag < 0), zero rates, dt = 0 / 5 s, a NaN sample, general P/Q/R
 """
 from __future__ import annotations
 
@@ -187,6 +188,85 @@ def make_traj(ekf):
     return out
 
 
+def make_edge(ekf, wb):
+    """Edge cases the reference accepts: raw-unit sensor values (|acc| ~ 9.81 so k_mag = 1-|acc_z| < 0),
+    zero rates, dt = 0 and very large dt, a NaN sample (propagates), non-symmetric P and non-scalar Q/R."""
+    KF, Wahba = ekf.KalmanFilter, wb.Wahba
+    out = {}
+    # (1) raw-unit trajectories: acc in m/s^2, mag in uT, plus zero-rate and 1 s gaps
+    K, W = 4, 600
+    rec = synth.generate(np.arange(100, 100 + K), W, seed=31)
+    rec.acc[:] = rec.acc * np.float32(9.81)
+    rec.mag[:] = rec.mag * np.float32(45.0)
+    rec.gyro[100:110] = 0.0
+    rec.dtw[200] = 1_000_000_000
+    rec.dtw[201] = 0
+    trajs = []
+    for f in range(K):
+        g, d, a, m = rec.filter(f)
+        with np.errstate(all="ignore"):
+            trajs.append(run_reference_filter(ekf, g, d, a, m, rec.acc0[f], rec.mag0[f]))
+    gd, am, my = synth.pack_planes(rec)
+    out.update(raw_gd=gd, raw_am=am, raw_my=my, raw_acc0=rec.acc0, raw_mag0=rec.mag0,
+               raw_traj=np.stack(trajs, axis=1))
+    # (2) NaN sample at record 20 of filter 1: the reference's np.linalg.svd raises
+    # LinAlgError("SVD did not converge") there; record the trajectory up to that point
+    rec = synth.generate(np.arange(2), 50, seed=32)
+    rec.acc[20, 1, 0] = np.float32(np.nan)
+    g, d, a, m = rec.filter(0)
+    clean = run_reference_filter(ekf, g, d, a, m, rec.acc0[0], rec.mag0[0])
+    g, d, a, m = rec.filter(1)
+    raised_at = -1
+    try:
+        run_reference_filter(ekf, g, d, a, m, rec.acc0[1], rec.mag0[1])
+    except np.linalg.LinAlgError:
+        # re-run to the failing record to keep the partial trajectory
+        raised_at = 20
+    partial = run_reference_filter(ekf, g[:20], d[:20], a[:20], m[:20], rec.acc0[1], rec.mag0[1])
+    gd, am, my = synth.pack_planes(rec)
+    out.update(nan_gd=gd, nan_am=am, nan_my=my, nan_acc0=rec.acc0, nan_mag0=rec.mag0,
+               nan_clean_traj=clean, nan_partial_traj=partial, nan_raised_at=np.int64(raised_at))
+    # (3) Wahba on raw-unit vectors: weights |acc_z|, 1-|acc_z| with |acc_z| > 1 (k_mag < 0)
+    n = 64
+    acc0, mag0 = unit(n, 3), unit(n, 3)
+    acc, mag = unit(n, 3) * 9.81, unit(n, 3) * 45.0
+    ka = np.abs(acc[:, 2])
+    km = 1 - ka
+    R, q = [], []
+    for i in range(n):
+        wo = Wahba(acc0[i], mag0[i])
+        R.append(wo.getRotation(acc[i], mag[i], ka[i], km[i]))
+        q.append(wo.getQuarternion(acc[i], mag[i], ka[i], km[i]))
+    out.update(ew_acc0=acc0, ew_mag0=mag0, ew_acc=acc, ew_mag=mag, ew_ka=ka, ew_km=km,
+               ew_R=np.array(R), ew_q=np.array(q))
+    # (4) Prediction / Correction with general (non-symmetric P, SPD non-scalar Q/R), w = 0, dt = 0, huge dt
+    n = 32
+    G = rng.normal(scale=2.0, size=(n, 3))
+    G[:4] = 0.0
+    D = rng.integers(0, 50_000_000, size=n).astype(np.float64)
+    D[4:6] = 0.0
+    D[6:8] = 5e9
+    X = unit(n, 4)
+    P = rng.normal(scale=0.3, size=(n, 4, 4)) + np.eye(4)
+    A3 = rng.normal(size=(n, 3, 3))
+    A4 = rng.normal(size=(n, 4, 4))
+    Q = np.einsum("nij,nkj->nik", A3, A3) + 0.1 * np.eye(3)
+    Rm = np.einsum("nij,nkj->nik", A4, A4) + 0.1 * np.eye(4)
+    acc, mag = unit(n, 3), unit(n, 3)
+    acc0, mag0 = unit(n, 3), unit(n, 3)
+    zs, Pms, Ks, Xo, Po = [], [], [], [], []
+    for i in range(n):
+        kf = KF(0.0, mag0[i], acc0[i], 0.5)
+        kf.Q, kf.R = Q[i].copy(), Rm[i].copy()
+        z, Pm, Kk = kf.Prediction(G[i], D[i], X[i], P[i])
+        Xn, Pn = kf.Correction(mag[i], acc[i], z, Pm, Kk)
+        zs.append(z); Pms.append(Pm); Ks.append(Kk); Xo.append(Xn); Po.append(Pn)
+    out.update(ep_gyro=G, ep_dt=D, ep_X=X, ep_P=P, ep_Q=Q, ep_R=Rm, ep_acc=acc, ep_mag=mag,
+               ep_acc0=acc0, ep_mag0=mag0, ep_z=np.array(zs), ep_Pm=np.array(Pms), ep_K=np.array(Ks),
+               ep_Xout=np.array(Xo), ep_Pout=np.array(Po))
+    return out
+
+
 def make_c1():
     """Config 1: one filter, ~1550 steps (Results/*.png x-axis), through main_file.py UNCHANGED."""
     n = 1550
@@ -222,6 +302,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "kat.npz"), **kat)
     traj = make_traj(ekf)
     np.savez_compressed(os.path.join(HERE, "traj.npz"), **traj)
+    np.savez_compressed(os.path.join(HERE, "edge.npz"), **make_edge(ekf, wb))
     text, xk = make_c1()
     with gzip.open(os.path.join(HERE, "c1_log.txt.gz"), "wt") as fh:
         fh.write(text)
