@@ -144,6 +144,20 @@ int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
                  const double *refs, double *X, double *P, double q, double r, double *traj,
                  uint32_t flags, void *stream);
 
+/* ---------------- side outputs: what main_file.py plots beside X ----------------
+ * Pure-gyro attitude: the RK4 chain of the gyro records alone, same dt as the filter (KFS/KalmanFilter.cpp:149,
+ * logged as "q_gyro"; step = ExtendedKalmanFilter.py:25-41).  q_gyro[batch*4] in/out; traj optional. */
+int pekf_gyro_chain_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
+                        const void *plane_gd, double *q_gyro, double *traj, void *stream);
+/* Pure-Wahba attitude of every record with fixed weights (main_file.py:40: getQuarternion(acc, mag,
+ * 0.5, 0.5)), out[n_steps][batch][4], same branch/sign convention as Wahba.RotationMatrix2Quart. */
+int pekf_wahba_stream_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
+                          const void *plane_am, const void *plane_my, const double *refs, double k_acc,
+                          double k_mag, double *out, void *stream);
+/* UtilityFunctions.Quart2RPY(q), UtilityFunctions.py:3-14: q[n*4] -> rpy[n*3] in degrees. */
+int pekf_quat_to_rpy(int64_t n, const double *q, double *rpy);
+int pekf_quat_to_rpy_dev(int64_t n, const double *q, double *rpy, void *stream);
+
 /* X = [1,0,0,0], P = I for every filter (main_file.py:23,26). */
 int pekf_reset_state_dev(int64_t batch, double *X, double *P, void *stream);
 

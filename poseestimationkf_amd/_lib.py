@@ -75,6 +75,10 @@ SIGNATURES = {
     "pekf_rotmat_to_quat": [_i64, _dp, _dp],
     "pekf_run_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _vp, _u32, _vp],
     "pekf_reset_state_dev": [_i64, _vp, _vp, _vp],
+    "pekf_gyro_chain_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
+    "pekf_wahba_stream_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp],
+    "pekf_quat_to_rpy": [_i64, _dp, _dp],
+    "pekf_quat_to_rpy_dev": [_i64, _vp, _vp, _vp],
     "pekf_synth_dev": [_i64, _i64, _i64, _u32, _int, _dp, _dbl, _vp, _vp, _vp, _vp, _vp],
 }
 _RESTYPE = {"pekf_abi_version": ctypes.c_int, "pekf_last_error": ctypes.c_char_p}

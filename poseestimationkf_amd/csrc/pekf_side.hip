@@ -1,0 +1,152 @@
+// pekf_side.hip -- side outputs beside the fused filter: what main_file.py
+// plots next to the filter quaternion.
+//   k_gyro_chain   pure-gyro attitude: the RK4 chain of the gyro record alone, same dt as the
+//                  filter (KFS/KalmanFilter.cpp:149 RungeKuttaEval(Quarternion_Gyro_pure, ...),
+//                  logged as "q_gyro"; the step is ExtendedKalmanFilter.py:25-41)
+//   k_wahba_stream pure-Wahba attitude per record with fixed weights (main_file.py:40,
+//                  Wahba.getQuarternion(acc, mag, 0.5, 0.5), Wahba.py:49-50)
+//   k_rpy          UtilityFunctions.Quart2RPY (UtilityFunctions.py:3-14), degrees
+// Each reads the same resident planes as pekf_run_dev (one lane per filter, coalesced).
+#include "pekf_internal.hpp"
+#include "pekf_math.hpp"
+
+namespace pekf {
+
+constexpr int kSideBlock = 256;
+
+__global__ __launch_bounds__(kSideBlock) void k_gyro_chain(int64_t batch, int64_t n_steps, int64_t window,
+                                                           int64_t step0, const float4 *__restrict__ gd,
+                                                           double *__restrict__ q, double *__restrict__ traj) {
+    const int64_t b = (int64_t)blockIdx.x * kSideBlock + threadIdx.x;
+    if (b >= batch) return;
+    double x[4] = {q[4 * b], q[4 * b + 1], q[4 * b + 2], q[4 * b + 3]};
+    int64_t row = step0 % window;
+    for (int64_t t = 0; t < n_steps; ++t) {
+        const float4 r = gd[row * batch + b];
+        const double hw[3] = {0.5 * (double)r.x, 0.5 * (double)r.y, 0.5 * (double)r.z};
+        const double dt_ns = (double)(__float_as_uint(r.w) & 0x7FFFFFFFu);
+        double z[4];
+        rk4_closed(x, dt_ns, hw, z);
+        x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
+        if (traj) {
+            double2 *o = reinterpret_cast<double2 *>(traj + (t * batch + b) * 4);
+            o[0] = make_double2(x[0], x[1]);
+            o[1] = make_double2(x[2], x[3]);
+        }
+        row = row + 1 == window ? 0 : row + 1;
+    }
+    q[4 * b] = x[0]; q[4 * b + 1] = x[1]; q[4 * b + 2] = x[2]; q[4 * b + 3] = x[3];
+}
+
+__global__ __launch_bounds__(kSideBlock) void k_wahba_stream(int64_t batch, int64_t n_steps, int64_t window,
+                                                             int64_t step0, const float4 *__restrict__ am,
+                                                             const float2 *__restrict__ my,
+                                                             const double *__restrict__ refs, double ka,
+                                                             double km, double *__restrict__ out) {
+    const int64_t b = (int64_t)blockIdx.x * kSideBlock + threadIdx.x;
+    if (b >= batch) return;
+    Frame Wf;
+    {
+        const double a0[3] = {refs[6 * b + 0], refs[6 * b + 1], refs[6 * b + 2]};
+        const double m0[3] = {refs[6 * b + 3], refs[6 * b + 4], refs[6 * b + 5]};
+        make_frame<true>(a0, m0, Wf);
+    }
+    int64_t row = step0 % window;
+    for (int64_t t = 0; t < n_steps; ++t) {
+        const float4 a = am[row * batch + b];
+        const float2 m = my[row * batch + b];
+        const double acc[3] = {a.x, a.y, a.z}, mag[3] = {a.w, m.x, m.y};
+        Frame Vf;
+        make_frame<true>(acc, mag, Vf);
+        double R[9], y[4];
+        wahba_rotation<true>(Wf, Vf, ka, km, R);
+        rotm_to_quat_fast(R, y);  // keeps the reference's branch / sign convention
+        double2 *o = reinterpret_cast<double2 *>(out + (t * batch + b) * 4);
+        o[0] = make_double2(y[0], y[1]);
+        o[1] = make_double2(y[2], y[3]);
+        row = row + 1 == window ? 0 : row + 1;
+    }
+}
+
+// UtilityFunctions.Quart2RPY: roll = atan2(2(q0q1+q2q3), 1-2(q1^2+q2^2)), pitch = asin(2(q0q2-q3q1)),
+// yaw = atan2(2(q0q3+q1q2), 1-2(q2^2+q3^2)), times 180/pi
+__global__ __launch_bounds__(kSideBlock) void k_rpy(int64_t n, const double *__restrict__ q,
+                                                    double *__restrict__ rpy) {
+#pragma clang fp contract(off)  // round like NumPy: at gimbal lock sinp may round past 1 -> NaN there too
+    const int64_t i = (int64_t)blockIdx.x * kSideBlock + threadIdx.x;
+    if (i >= n) return;
+    const double *p = q + 4 * i;
+    const double sinr = 2 * (p[0] * p[1] + p[2] * p[3]);
+    const double cosr = 1 - 2 * (p[1] * p[1] + p[2] * p[2]);
+    const double sinp = 2 * (p[0] * p[2] - p[3] * p[1]);
+    const double siny = 2 * (p[0] * p[3] + p[1] * p[2]);
+    const double cosy = 1 - 2 * (p[2] * p[2] + p[3] * p[3]);
+    const double k = 180.0 / 3.141592653589793;
+    rpy[3 * i + 0] = atan2(sinr, cosr) * k;
+    rpy[3 * i + 1] = asin(sinp) * k;
+    rpy[3 * i + 2] = atan2(siny, cosy) * k;
+}
+
+static int launched(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, what);
+    return PEKF_OK;
+}
+
+}  // namespace pekf
+
+using namespace pekf;
+
+extern "C" {
+
+int pekf_gyro_chain_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
+                        const void *plane_gd, double *q_gyro, double *traj, void *stream) {
+    PEKF_CHECK_ARG(batch >= 0 && n_steps >= 0, "negative size");
+    if (batch == 0 || n_steps == 0) return PEKF_OK;
+    PEKF_CHECK_ARG(window > 0 && step0 >= 0, "window must be > 0 and step0 >= 0");
+    PEKF_CHECK_ARG(plane_gd && q_gyro, "null pointer");
+    hipLaunchKernelGGL(k_gyro_chain, dim3(grid_for(batch, kSideBlock)), dim3(kSideBlock), 0,
+                       as_stream(stream), batch, n_steps, window, step0,
+                       static_cast<const float4 *>(plane_gd), q_gyro, traj);
+    return launched("k_gyro_chain");
+}
+
+int pekf_wahba_stream_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
+                          const void *plane_am, const void *plane_my, const double *refs, double k_acc,
+                          double k_mag, double *out, void *stream) {
+    PEKF_CHECK_ARG(batch >= 0 && n_steps >= 0, "negative size");
+    if (batch == 0 || n_steps == 0) return PEKF_OK;
+    PEKF_CHECK_ARG(window > 0 && step0 >= 0, "window must be > 0 and step0 >= 0");
+    PEKF_CHECK_ARG(plane_am && plane_my && refs && out, "null pointer");
+    hipLaunchKernelGGL(k_wahba_stream, dim3(grid_for(batch, kSideBlock)), dim3(kSideBlock), 0,
+                       as_stream(stream), batch, n_steps, window, step0,
+                       static_cast<const float4 *>(plane_am), static_cast<const float2 *>(plane_my),
+                       refs, k_acc, k_mag, out);
+    return launched("k_wahba_stream");
+}
+
+int pekf_quat_to_rpy_dev(int64_t n, const double *q, double *rpy, void *stream) {
+    PEKF_CHECK_ARG(n >= 0, "n < 0");
+    if (n == 0) return PEKF_OK;
+    PEKF_CHECK_ARG(q && rpy, "null pointer");
+    hipLaunchKernelGGL(k_rpy, dim3(grid_for(n, kSideBlock)), dim3(kSideBlock), 0, as_stream(stream), n,
+                       q, rpy);
+    return launched("k_rpy");
+}
+
+int pekf_quat_to_rpy(int64_t n, const double *q, double *rpy) {
+    PEKF_CHECK_ARG(n >= 0, "n < 0");
+    if (n == 0) return PEKF_OK;
+    PEKF_CHECK_ARG(q && rpy, "null pointer");
+    if (int st = require_device()) return st;
+    Staging &s = Staging::get();
+    const size_t b = (size_t)n * sizeof(double);
+    void *in[1], *out[1];
+    if (int st = s.stage_in({{q, 4 * b}}, {3 * b}, in, out)) return st;
+    hipLaunchKernelGGL(k_rpy, dim3(grid_for(n, kSideBlock)), dim3(kSideBlock), 0, s.stream(), n,
+                       static_cast<const double *>(in[0]), static_cast<double *>(out[0]));
+    if (int st = launched("k_rpy")) return st;
+    return s.stage_out({{rpy, 3 * b}}, out);
+}
+
+}  // extern "C"

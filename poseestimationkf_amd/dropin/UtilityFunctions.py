@@ -1,22 +1,16 @@
 """Drop-in for the reference module ``UtilityFunctions`` (Python Kalman Filter/UtilityFunctions.py).
 
-``norm`` (the hot-path helper, :16-21) runs on the device (k_norm).  ``Quart2RPY`` (:3-14)
-and ``DimensionalSplit`` (:24-34) are the reference's display/plot helpers, off the hot
-path; they are plain host code here as there.
+``norm`` (the hot-path helper, :16-21) and ``Quart2RPY`` (:3-14) run on the device (k_norm,
+k_rpy).  ``DimensionalSplit`` (:24-34) is the reference's list-transpose plot helper, plain
+host code as there.
 """
-import math
-
 import numpy as np
 from _bootstrap import engine as _eng
 
 
 def Quart2RPY(q):
     """Quaternion [w,x,y,z] -> roll, pitch, yaw in degrees (UtilityFunctions.py:3-14)."""
-    w, x, y, z = (float(v) for v in q[:4])
-    roll = math.atan2(2 * (w * x + y * z), 1 - 2 * (x * x + y * y))
-    pitch = math.asin(2 * (w * y - z * x))
-    yaw = math.atan2(2 * (w * z + x * y), 1 - 2 * (y * y + z * z))
-    return np.asarray([roll, pitch, yaw]) * 180.0 / np.pi
+    return _eng.quat_to_rpy(np.asarray(q, dtype=np.float64)[:4])[0]
 
 
 def norm(a):

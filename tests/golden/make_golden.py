@@ -14,6 +14,7 @@ Outputs (tests/golden/):
   traj.npz         8 filters x 1500 synthetic steps (+ a Wahba-skip variant), inputs and X trajectories
   c1_log.txt.gz    config-1 trace in the C++ log format (1550 steps)
   c1_xk.npy        X_k list produced by main_file.py (unchanged) on that log
+  side.npz         pure-gyro chain, per-record 0.5/0.5 Wahba quaternion, Quart2RPY
   edge.npz         raw-unit inputs (k_mag < 0), zero rates, dt = 0 / 5 s, a NaN sample, general P/Q/R
 """
 from __future__ import annotations
@@ -267,6 +268,29 @@ def make_edge(ekf, wb):
     return out
 
 
+def make_side(ekf, wb, uf):
+    """Side outputs main_file.py plots: pure-gyro RK4 chain, per-record 0.5/0.5
+    Wahba quaternion (main_file.py:40), Quart2RPY (UtilityFunctions.py:3-14)."""
+    KF, Wahba = ekf.KalmanFilter, wb.Wahba
+    K, W = 8, 300
+    rec = synth.generate(np.arange(K), W, seed=synth.DEFAULT_SEED)  # = traj.npz's first 300 records
+    chain = np.empty((W, K, 4))
+    wq = np.empty((W, K, 4))
+    for f in range(K):
+        g, d, a, m = rec.filter(f)
+        q = np.asarray([1.0, 0.0, 0.0, 0.0])
+        wo = Wahba(rec.acc0[f], rec.mag0[f])
+        for i in range(W):
+            q = KF.RungeKutta4(q, d[i], g[i])
+            chain[i, f] = q
+            wq[i, f] = wo.getQuarternion(a[i], m[i], 0.5, 0.5)
+    qs = unit(64, 4)
+    s = np.sqrt(0.5)
+    qs = np.vstack([qs, [[1.0, 0, 0, 0], [s, 0, s, 0], [s, 0, -s, 0], [0, 1.0, 0, 0]]])
+    rpy = np.array([uf.Quart2RPY(q) for q in qs])
+    return dict(gyro_chain=chain, wahba_half=wq, rpy_q=qs, rpy_out=rpy)
+
+
 def make_c1():
     """Config 1: one filter, ~1550 steps (Results/*.png x-axis), through main_file.py UNCHANGED."""
     n = 1550
@@ -303,9 +327,11 @@ def main():
     traj = make_traj(ekf)
     np.savez_compressed(os.path.join(HERE, "traj.npz"), **traj)
     np.savez_compressed(os.path.join(HERE, "edge.npz"), **make_edge(ekf, wb))
+    np.savez_compressed(os.path.join(HERE, "side.npz"), **make_side(ekf, wb, uf))
     text, xk = make_c1()
-    with gzip.open(os.path.join(HERE, "c1_log.txt.gz"), "wt") as fh:
-        fh.write(text)
+    with open(os.path.join(HERE, "c1_log.txt.gz"), "wb") as raw, \
+            gzip.GzipFile(fileobj=raw, mode="wb", mtime=0, filename="") as gz:  # byte-stable output
+        gz.write(text.encode())
     np.save(os.path.join(HERE, "c1_xk.npy"), xk)
     for f in sorted(os.listdir(HERE)):
         print(f, os.path.getsize(os.path.join(HERE, f)))
