@@ -158,6 +158,15 @@ int pekf_wahba_stream_dev(int64_t batch, int64_t n_steps, int64_t window, int64_
 int pekf_quat_to_rpy(int64_t n, const double *q, double *rpy);
 int pekf_quat_to_rpy_dev(int64_t n, const double *q, double *rpy, void *stream);
 
+/* ---------------- recorded traces: the server's text log -> 40 B records ----------------
+ * Host-side ingest (no device work).  Tags / precedence of ReadFile.py:27-45; one record per Acc_1 line
+ * (main_file.py:38), dt_ns = T[i+1] - T[i] (ExtendedKalmanFilter.py:62; must be an integer < 2^31).
+ * pekf_log_scan gives the record count; pekf_log_read fills gyro/acc/mag[n*3] (float), dtw[n],
+ * acc0/mag0[3] (double) and t0 (first timestamp; may be NULL). */
+int pekf_log_scan(const char *path, int64_t *n_records);
+int pekf_log_read(const char *path, int64_t n_records, float *gyro, float *acc, float *mag, uint32_t *dtw,
+                  double *acc0, double *mag0, double *t0);
+
 /* X = [1,0,0,0], P = I for every filter (main_file.py:23,26). */
 int pekf_reset_state_dev(int64_t batch, double *X, double *P, void *stream);
 

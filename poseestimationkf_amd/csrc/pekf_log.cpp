@@ -1,0 +1,149 @@
+// pekf_log.cpp -- native ingest of the live server's text log into the 40 B record stream
+// (SURVEY.md §8f-1).  Host code (no device work): it feeds pekf_run_dev with recorded phone traces.
+//
+// Line tags and precedence follow the offline reader (Python Kalman Filter/ReadFile.py:27-45):
+// mag_0, acc_0, Acc_1, Mag_1, q_gyro, gyro, any line containing 'T', Wahba_quart, X_k; values are
+// the comma-separated numbers after the first ':' (strtod == Python float() for these tokens).
+// Records follow main_file.py:19-47: one per Acc_1 line, record i uses gyro[i], Mag_1[i],
+// Acc_1[i] and dt_i = T[i+1] - T[i] (float64, as ExtendedKalmanFilter.py:62 computes
+// T - previousT with previousT starting at the first timestamp).
+#include <cerrno>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pekf.h"
+
+namespace pekf {
+int set_error(int code, const char *fmt, ...);  // pekf_capi.hip
+}
+
+namespace {
+
+struct LogColumns {
+    std::vector<double> mag0, acc0, T;
+    std::vector<double> acc1, mag1, gyro;  // flattened triples
+};
+
+bool values(const char *line, std::vector<double> &dst, int want) {
+    const char *p = std::strchr(line, ':');
+    if (!p) return false;
+    ++p;
+    int got = 0;
+    while (*p) {
+        char *end = nullptr;
+        errno = 0;
+        const double v = std::strtod(p, &end);
+        if (end == p) return false;
+        dst.push_back(v);
+        ++got;
+        p = end;
+        while (*p == ' ' || *p == '\t' || *p == '\r' || *p == '\n') ++p;
+        if (*p == ',') {
+            ++p;
+        } else {
+            break;
+        }
+    }
+    return want < 0 || got == want;
+}
+
+int parse(const char *path, LogColumns &c) {
+    FILE *f = std::fopen(path, "r");
+    if (!f) return pekf::set_error(PEKF_ERR_INVALID, "cannot open log '%s': %s", path, std::strerror(errno));
+    char buf[4096];
+    int64_t lineno = 0;
+    int status = PEKF_OK;
+    while (std::fgets(buf, sizeof(buf), f)) {
+        ++lineno;
+        const char *l = buf;
+        bool ok = true;
+        if (std::strstr(l, "mag_0")) {
+            c.mag0.clear();
+            ok = values(l, c.mag0, 3);
+        } else if (std::strstr(l, "acc_0")) {
+            c.acc0.clear();
+            ok = values(l, c.acc0, 3);
+        } else if (std::strstr(l, "Acc_1")) {
+            ok = values(l, c.acc1, 3);
+        } else if (std::strstr(l, "Mag_1")) {
+            ok = values(l, c.mag1, 3);
+        } else if (std::strstr(l, "q_gyro")) {
+            std::vector<double> tmp;  // side channel, not a filter input
+            ok = values(l, tmp, -1);
+        } else if (std::strstr(l, "gyro")) {
+            ok = values(l, c.gyro, 3);
+        } else if (std::strchr(l, 'T')) {
+            std::vector<double> tmp;
+            ok = values(l, tmp, -1) && !tmp.empty();
+            if (ok) c.T.push_back(tmp[0]);
+        }  // Wahba_quart / X_k: logged side channels, not inputs
+        if (!ok) {
+            status = pekf::set_error(PEKF_ERR_INVALID, "%s:%lld: cannot parse '%.60s'", path, (long long)lineno, l);
+            break;
+        }
+    }
+    std::fclose(f);
+    return status;
+}
+
+int validate(const char *path, const LogColumns &c, int64_t *n) {
+    const int64_t nrec = (int64_t)c.acc1.size() / 3;
+    if (c.acc0.size() != 3 || c.mag0.size() != 3)
+        return pekf::set_error(PEKF_ERR_INVALID, "%s: missing acc_0 / mag_0 line", path);
+    if ((int64_t)c.gyro.size() / 3 < nrec || (int64_t)c.mag1.size() / 3 < nrec || (int64_t)c.T.size() < nrec + 1)
+        return pekf::set_error(PEKF_ERR_INVALID, "%s: %lld Acc_1 records but %zu gyro, %zu Mag_1, %zu T lines",
+                               path, (long long)nrec, c.gyro.size() / 3, c.mag1.size() / 3, c.T.size());
+    *n = nrec;
+    return PEKF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pekf_log_scan(const char *path, int64_t *n_records) {
+    if (!path || !n_records) return pekf::set_error(PEKF_ERR_INVALID, "null pointer");
+    LogColumns c;
+    if (int st = parse(path, c)) return st;
+    return validate(path, c, n_records);
+}
+
+int pekf_log_read(const char *path, int64_t n_records, float *gyro, float *acc, float *mag, uint32_t *dtw,
+                  double *acc0, double *mag0, double *t0) {
+    if (!path || !gyro || !acc || !mag || !dtw || !acc0 || !mag0)
+        return pekf::set_error(PEKF_ERR_INVALID, "null pointer");
+    LogColumns c;
+    if (int st = parse(path, c)) return st;
+    int64_t n = 0;
+    if (int st = validate(path, c, &n)) return st;
+    if (n_records > n)
+        return pekf::set_error(PEKF_ERR_INVALID, "%s has %lld records, %lld requested", path, (long long)n,
+                               (long long)n_records);
+    for (int k = 0; k < 3; ++k) {
+        acc0[k] = c.acc0[k];
+        mag0[k] = c.mag0[k];
+    }
+    if (t0) *t0 = c.T[0];
+    for (int64_t i = 0; i < n_records; ++i) {
+        for (int k = 0; k < 3; ++k) {
+            gyro[3 * i + k] = (float)c.gyro[3 * i + k];
+            acc[3 * i + k] = (float)c.acc1[3 * i + k];
+            mag[3 * i + k] = (float)c.mag1[3 * i + k];
+        }
+        const double dt = c.T[i + 1] - c.T[i];
+        if (!(dt >= 0.0 && dt < 2147483648.0 && dt == std::floor(dt)))
+            return pekf::set_error(PEKF_ERR_INVALID,
+                                   "%s: record %lld has dt = %.17g ns, not an integer in [0, 2^31) "
+                                   "(the 40 B record carries dt as a 31-bit ns count)",
+                                   path, (long long)i, dt);
+        dtw[i] = (uint32_t)dt;
+    }
+    return PEKF_OK;
+}
+
+}  // extern "C"

@@ -6,6 +6,7 @@ filter runs in the HIP kernels of libpekf.so.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -100,6 +101,25 @@ def device_name(dev=0):
     return buf.value.decode()
 
 
+# ------------------------------------------------------------------ recorded traces (host ingest)
+
+def read_log_records(path):
+    """Parse one server log natively (pekf_log_scan / pekf_log_read) into a 1-filter synth.Records.
+
+    The records are the 40 B stream format: f32 sensor values, u32 ns dt (the drop-in
+    ReadFile / logformat path keeps the parsed float64 values instead)."""
+    bpath = os.fsencode(path)
+    n = ctypes.c_int64()
+    check(lib.pekf_log_scan(bpath, ctypes.byref(n)))
+    n = n.value
+    gyro, acc, mag = (np.empty((n, 1, 3), np.float32) for _ in range(3))
+    dtw = np.empty((n, 1), np.uint32)
+    acc0, mag0, t0 = np.empty((1, 3)), np.empty((1, 3)), ctypes.c_double()
+    check(lib.pekf_log_read(bpath, n, gyro.ctypes.data, acc.ctypes.data, mag.ctypes.data, dtw.ctypes.data,
+                            dptr(acc0), dptr(mag0), ctypes.byref(t0)))
+    return synth.Records(gyro, acc, mag, dtw, acc0, mag0)
+
+
 # ------------------------------------------------------------------ resident IMU window
 
 class IMUWindow:
@@ -142,6 +162,19 @@ class IMUWindow:
         win.my.upload(np.ascontiguousarray(my, np.float32))
         win.refs.upload(synth.refs_array(acc0, mag0))
         return win
+
+    @classmethod
+    def from_logs(cls, paths, n_records=None):
+        """One filter per server log, parsed natively (pekf_log_read).
+
+        All filters of a window advance in lock-step, so the window holds the first
+        n_records records of every log (default: the shortest log's length)."""
+        recs = [read_log_records(p) for p in paths]
+        n = min(r.dtw.shape[0] for r in recs) if n_records is None else int(n_records)
+        cat = lambda name: np.concatenate([getattr(r, name)[:n] for r in recs], axis=1)  # noqa: E731
+        rec = synth.Records(cat("gyro"), cat("acc"), cat("mag"), cat("dtw"),
+                            np.concatenate([r.acc0 for r in recs]), np.concatenate([r.mag0 for r in recs]))
+        return cls.from_records(rec)
 
     def synthesize(self, seed=synth.DEFAULT_SEED, first_filter=0, missing=False,
                    params=synth.SynthParams(), stream=None):

@@ -224,6 +224,20 @@ def test_dropin_main_file_loop_on_c1_log(eng, tmp_path, monkeypatch):
     assert abs(norm(X_k[-1]) - 1.0) < 1e-14
 
 
+def test_fused_run_on_native_parsed_c1_log(eng, tmp_path):
+    """Config 1 through the batched path: log -> pekf_log_read (f32 records) -> fused kernel."""
+    log = tmp_path / "KalmanFilter.txt"
+    with gzip.open(os.path.join(GOLDEN, "c1_log.txt.gz"), "rt") as fh:
+        log.write_text(fh.read())
+    win = eng.IMUWindow.from_logs([str(log), str(log)])  # two filters, same trace
+    tr = eng.BatchedEKF(2).run(win, want_traj=True)
+    want = np.load(os.path.join(GOLDEN, "c1_xk.npy"))[1:]
+    err = _maxerr(tr[:, 0], want)
+    print("C1 via native log ingest + fused kernel: max |dq| = %.3e (inputs rounded to f32)" % err)
+    assert err < ATOL_Q
+    assert np.array_equal(tr[:, 0], tr[:, 1])
+
+
 def test_dropin_returns_fresh_arrays_and_keeps_inputs(eng, monkeypatch):
     monkeypatch.syspath_prepend(os.path.join(ROOT, "poseestimationkf_amd", "dropin"))
     for m in ("ExtendedKalmanFilter", "Wahba", "UtilityFunctions", "_bootstrap"):

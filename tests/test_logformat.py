@@ -1,0 +1,72 @@
+"""The server's text log: Python reader (drop-in ReadFile semantics) and the
+native ingest (pekf_log_scan / pekf_log_read, host code: runs without a GPU)."""
+import gzip
+import io
+import os
+
+import numpy as np
+import pytest
+
+from poseestimationkf_amd import logformat, synth
+
+from .conftest import GOLDEN
+
+
+@pytest.fixture(scope="module")
+def c1_log(tmp_path_factory):
+    p = tmp_path_factory.mktemp("log") / "KalmanFilter.txt"
+    with gzip.open(os.path.join(GOLDEN, "c1_log.txt.gz"), "rt") as fh:
+        p.write_text(fh.read())
+    return str(p)
+
+
+def test_reader_tag_precedence():
+    lines = ["mag_0 : 0.5,0,-0.8\n", "acc_0 : 0,0,1\n", "q_gyro : 1.0, 0.0, 0.0, 0.0\n",
+             "X_k : 1.0, 0.0, 0.0, 0.0\n", "Wahba_quart : 1.0, 0.0, 0.0, 0.0\n",
+             "gyro : 0.1,0.2,0.3\n", "T : 100\n", "T : 200\n", "q_gyro : 1,0,0,0\n",
+             "Mag_1 : 0.5,0.01,-0.8\n", "Acc_1 : 0.01,0.02,0.99\n"]
+    d = logformat.parse_lines(lines)
+    assert d.gyro == [[0.1, 0.2, 0.3]]                 # q_gyro lines are not gyro (ReadFile.py:36-39)
+    assert d.quart_gyro == [[1.0, 0, 0, 0], [1, 0, 0, 0]]
+    assert d.timestamp == [[100.0], [200.0]]
+    assert d.quart_xk == [[1.0, 0, 0, 0]] and d.quart_wahba == [[1.0, 0, 0, 0]]
+    g, dt, a, m, a0, m0 = logformat.log_to_arrays(d)
+    assert dt.tolist() == [100.0] and a0.tolist() == [0, 0, 1]
+
+
+def test_writer_reader_roundtrip_at_percent_f():
+    rec = synth.generate(np.arange(1), 20)
+    g, d, a, m = rec.filter(0)
+    ts = synth.c1_timestamps(d.astype(np.int64))
+    buf = io.StringIO()
+    logformat.write_log(buf, ts, g, a, m, rec.acc0[0], rec.mag0[0])
+    got = logformat.log_to_arrays(logformat.parse_lines(io.StringIO(buf.getvalue()).readlines()))
+    assert np.array_equal(got[1], d)                   # integer ns timestamps survive exactly
+    assert np.abs(got[0] - g).max() <= 5e-7            # std::to_string keeps 6 decimals
+    assert np.abs(got[2] - a).max() <= 5e-7
+
+
+def test_native_ingest_matches_python_reader(c1_log):
+    from poseestimationkf_amd import engine
+    rec = engine.read_log_records(c1_log)
+    g, dt, a, m, a0, m0 = logformat.log_to_arrays(logformat.read_log(c1_log))
+    assert rec.dtw.shape == (1550, 1)
+    assert np.array_equal(rec.dt_ns[:, 0], dt)
+    assert np.array_equal(rec.gyro[:, 0], g.astype(np.float32))
+    assert np.array_equal(rec.acc[:, 0], a.astype(np.float32))
+    assert np.array_equal(rec.mag[:, 0], m.astype(np.float32))
+    assert np.array_equal(rec.acc0[0], a0) and np.array_equal(rec.mag0[0], m0)
+
+
+def test_native_ingest_errors_are_reported(tmp_path):
+    from poseestimationkf_amd import _lib, engine
+    bad = tmp_path / "bad.txt"
+    bad.write_text("mag_0 : 1,0,0\nacc_0 : 0,0,1\ngyro : 0,0,0\nT : 0\nT : 0.5\nMag_1 : 1,0,0\nAcc_1 : 0,0,1\n")
+    with pytest.raises(_lib.PekfError, match="not an integer"):
+        engine.read_log_records(str(bad))
+    with pytest.raises(_lib.PekfError, match="cannot open"):
+        engine.read_log_records(str(tmp_path / "missing.txt"))
+    short = tmp_path / "short.txt"
+    short.write_text("mag_0 : 1,0,0\nacc_0 : 0,0,1\nMag_1 : 1,0,0\nAcc_1 : 0,0,1\n")
+    with pytest.raises(_lib.PekfError, match="Acc_1 records"):
+        engine.read_log_records(str(short))
