@@ -1,0 +1,127 @@
+// pekf_frontend.hip -- the live server's pre-processing front-end on the device:
+// raw phone events -> the 40 B records the filter consumes (what the server logs as gyro / T /
+// Mag_1 / Acc_1).  One lane per filter walks its event stream through the state machine of
+// Parser::WriteKalmanFilterMeasurement (KFS/Parser.cpp:148-219); when a gyro sample has both an
+// accelerometer and a magnetometer sample after it, ExecuteKalmanFilter (Parser.cpp:229-257)
+// interpolates both to the gyro time (:259-267), normalises them (:221-228) and low-pass filters
+// them (alpha, from a zero state: KalmanFilter.cpp:16-18,21-24,279-303); the record's dt is the
+// gyro time minus the previous record's (KalmanFilter.cpp:306-308).  Arithmetic in FP64, records
+// rounded to f32 like every record of the stream.  Event planes: EV float4 {x, y, z, bits(type)}
+// and ET int64, [n_events][batch]: 24 B per event, coalesced.
+#include "pekf_internal.hpp"
+#include "pekf_math.hpp"
+
+namespace pekf {
+
+constexpr int kFeBlock = 256;
+enum : uint32_t { kEvAcc = 0, kEvGyro = 1, kEvMag = 2 };
+
+struct V3 {
+    double x, y, z;
+};
+
+__device__ __forceinline__ V3 lerp_to(int64_t t1, int64_t t2, int64_t t3, const V3 &a, const V3 &b) {
+    const double s = ((double)t3 - (double)t1);
+    const double d = ((double)t2 - (double)t1);
+    return {(b.x - a.x) / d * s + a.x, (b.y - a.y) / d * s + a.y, (b.z - a.z) / d * s + a.z};
+}
+
+__device__ __forceinline__ V3 normalised(const V3 &v) {
+    const double n = sqrt((v.x * v.x + v.y * v.y) + v.z * v.z);
+    return {v.x / n, v.y / n, v.z / n};
+}
+
+__global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_events,
+                                                       const float4 *__restrict__ ev,
+                                                       const int64_t *__restrict__ et,
+                                                       const double *__restrict__ init,
+                                                       const int64_t *__restrict__ t_init, double alpha,
+                                                       int64_t r_max, float4 *__restrict__ gd,
+                                                       float4 *__restrict__ am, float2 *__restrict__ my,
+                                                       int32_t *__restrict__ counts, double *__restrict__ refs,
+                                                       int *__restrict__ err) {
+#pragma clang fp contract(off)  // same operation order and rounding as the C++ / the oracle
+    const int64_t b = (int64_t)blockIdx.x * kFeBlock + threadIdx.x;
+    if (b >= batch) return;
+    // phase-2 state: acc_0 / mag_0 = raw means at the initialisation time (Parser.cpp:44-53)
+    V3 acc0 = {init[6 * b + 0], init[6 * b + 1], init[6 * b + 2]};
+    V3 mag0 = {init[6 * b + 3], init[6 * b + 4], init[6 * b + 5]};
+    int64_t t_acc0 = t_init[b], t_mag0 = t_init[b], prev_t = t_init[b];
+    {   // the filter's reference vectors: normalised phase-2 means (Parser.cpp:48-49)
+        const V3 a = normalised(acc0), m = normalised(mag0);
+        refs[6 * b + 0] = a.x; refs[6 * b + 1] = a.y; refs[6 * b + 2] = a.z;
+        refs[6 * b + 3] = m.x; refs[6 * b + 4] = m.y; refs[6 * b + 5] = m.z;
+    }
+    V3 acc1 = {0, 0, 0}, mag1 = {0, 0, 0}, gyro = {0, 0, 0};
+    int64_t t_acc1 = 0, t_mag1 = 0, t_gyro = 0;
+    bool gyro_set = false, acc1_set = false, mag1_set = false;
+    V3 lpf_acc = {0, 0, 0}, lpf_mag = {0, 0, 0};
+    const double beta = 1.0 - alpha;
+    int64_t r = 0;
+    int bad = 0;
+    for (int64_t e = 0; e < n_events; ++e) {
+        const float4 v4 = ev[e * batch + b];
+        const int64_t t = et[e * batch + b];
+        const uint32_t ty = __float_as_uint(v4.w);
+        const V3 v = {v4.x, v4.y, v4.z};
+        if (!gyro_set) {
+            if (ty == kEvAcc) { acc0 = v; t_acc0 = t; }
+            else if (ty == kEvMag) { mag0 = v; t_mag0 = t; }
+            else if (ty == kEvGyro) { gyro = v; t_gyro = t; gyro_set = true; }
+        } else {
+            if (ty == kEvAcc) { acc1 = v; t_acc1 = t; acc1_set = true; }
+            else if (ty == kEvMag) { mag1 = v; t_mag1 = t; mag1_set = true; }
+            else if (ty == kEvGyro) {
+                gyro = v; t_gyro = t;
+                if (acc1_set) { acc0 = acc1; t_acc0 = t_acc1; }
+                if (mag1_set) { mag0 = mag1; t_mag0 = t_mag1; }
+                acc1_set = mag1_set = false;
+            }
+        }
+        if (acc1_set && mag1_set) {
+            gyro_set = acc1_set = mag1_set = false;
+            const V3 a = normalised(lerp_to(t_acc0, t_acc1, t_gyro, acc0, acc1));
+            const V3 m = normalised(lerp_to(t_mag0, t_mag1, t_gyro, mag0, mag1));
+            lpf_mag = {alpha * m.x + beta * lpf_mag.x, alpha * m.y + beta * lpf_mag.y, alpha * m.z + beta * lpf_mag.z};
+            lpf_acc = {alpha * a.x + beta * lpf_acc.x, alpha * a.y + beta * lpf_acc.y, alpha * a.z + beta * lpf_acc.z};
+            const int64_t dt = t_gyro - prev_t;
+            if (dt < 0 || dt >= ((int64_t)1 << 31)) bad |= 1;  // not representable in the 31-bit dt word
+            if (r < r_max) {
+                const int64_t o = r * batch + b;
+                gd[o] = make_float4((float)gyro.x, (float)gyro.y, (float)gyro.z,
+                                    __uint_as_float((uint32_t)dt & 0x7FFFFFFFu));
+                am[o] = make_float4((float)lpf_acc.x, (float)lpf_acc.y, (float)lpf_acc.z, (float)lpf_mag.x);
+                my[o] = make_float2((float)lpf_mag.y, (float)lpf_mag.z);
+            } else {
+                bad |= 2;  // more records than the output window holds
+            }
+            ++r;
+            prev_t = t_gyro;
+            acc0 = acc1; t_acc0 = t_acc1;
+            mag0 = mag1; t_mag0 = t_mag1;
+        }
+    }
+    counts[b] = (int32_t)(r < r_max ? r : r_max);
+    if (bad && err) atomicOr(err, bad);
+}
+
+}  // namespace pekf
+
+using namespace pekf;
+
+extern "C" int pekf_frontend_dev(int64_t batch, int64_t n_events, const void *ev_planes, const int64_t *ev_times,
+                                 const double *init, const int64_t *t_init, double alpha, int64_t r_max,
+                                 void *plane_gd, void *plane_am, void *plane_my, int32_t *counts, double *refs,
+                                 int *dev_error, void *stream) {
+    PEKF_CHECK_ARG(batch >= 0 && n_events >= 0 && r_max >= 0, "negative size");
+    if (batch == 0) return PEKF_OK;
+    PEKF_CHECK_ARG(ev_planes && ev_times && init && t_init && plane_gd && plane_am && plane_my && counts && refs,
+                   "null pointer");
+    hipLaunchKernelGGL(k_frontend, dim3(grid_for(batch, kFeBlock)), dim3(kFeBlock), 0, as_stream(stream), batch,
+                       n_events, static_cast<const float4 *>(ev_planes), ev_times, init, t_init, alpha, r_max,
+                       static_cast<float4 *>(plane_gd), static_cast<float4 *>(plane_am),
+                       static_cast<float2 *>(plane_my), counts, refs, dev_error);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "k_frontend");
+    return PEKF_OK;
+}

@@ -233,6 +233,76 @@ def refs_array(acc0, mag0):
     return np.ascontiguousarray(np.concatenate([acc0, mag0], axis=1), dtype=np.float64)
 
 
+# ---------------------------------------------------------------------------------------------
+# Raw phone events for the server front-end: what the Android client sends in
+# phase 3 (ASC/SensorActivities.java:50-88, wire format ASC/MessageSender.java:217-233) --
+# asynchronous accelerometer (m/s^2), gyroscope (rad/s) and magnetometer (uT) samples with
+# integer ns timestamps.  Event planes: EV float4 {x, y, z, bits(type)} and ET int64 [E][K].
+# ---------------------------------------------------------------------------------------------
+EV_ACC, EV_GYRO, EV_MAG = 0, 1, 2
+G_MS2, B_UT = 9.81, 45.0
+T_INIT_NS = 1_000_000_000_000
+
+
+def generate_events(ids, n_events, seed=DEFAULT_SEED, params=SynthParams()):
+    """Per filter: n_events events, type ~ {acc 0.4, gyro 0.4, mag 0.2}, gaps U{1..4} ms.
+
+    Returns dict(types (E,K) uint32, values (E,K,3) float32, times (E,K) int64,
+    init_acc / init_mag (K,3) float64 = raw phase-2 means, t_init (K,) int64)."""
+    ids = np.asarray(ids, dtype=np.uint64)
+    K = ids.shape[0]
+    acc0, mag0 = reference_vectors(ids, seed, params)
+    _, s_w, s_g, s_a, s_m = params.scales()
+    w = [np.zeros(K) for _ in range(3)]
+    q = [np.ones(K), np.zeros(K), np.zeros(K), np.zeros(K)]
+    types = np.empty((n_events, K), np.uint32)
+    vals = np.empty((n_events, K, 3), np.float32)
+    times = np.empty((n_events, K), np.int64)
+    t = np.full(K, T_INIT_NS, np.int64)
+    key = np.uint64(seed) ^ np.uint64(0x5EED)
+    for e in range(n_events):
+        ph = lambda slot: philox4x32(e, slot, 1, 0, key, ids)  # noqa: E731  (c2 = 1: event streams)
+        s0 = ph(0)
+        u = (s0[0] >> np.uint64(8)).astype(np.float64) * (2.0 ** -24)
+        ty = np.where(u < 0.4, EV_ACC, np.where(u < 0.8, EV_GYRO, EV_MAG)).astype(np.uint32)
+        gap = 1_000_000 + (s0[1] % np.uint64(3_000_001)).astype(np.int64)
+        t = t + gap
+        for i in range(3):
+            w[i] = 0.995 * w[i] + _noise(ph(1 + i), 0.5 * s_w)
+        h = gap.astype(np.float64) * 1e-9
+        th2 = 0.25 * ((w[0] * w[0] + w[1] * w[1]) + w[2] * w[2])
+        x = (h * h) * th2
+        ca = (1.0 - x * 0.5) + (x * x) / 24.0
+        cb = h * (1.0 - x / 6.0)
+        r = [0.5 * ((-(w[0] * q[1]) - w[1] * q[2]) - w[2] * q[3]),
+             0.5 * ((w[0] * q[0] + w[2] * q[2]) - w[1] * q[3]),
+             0.5 * ((w[1] * q[0] - w[2] * q[1]) + w[0] * q[3]),
+             0.5 * ((w[2] * q[0] + w[1] * q[1]) - w[0] * q[2])]
+        q = [ca * q[i] + cb * r[i] for i in range(4)]
+        n = np.sqrt(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3])
+        q = [c / n for c in q]
+        ba = _body(q, [acc0[:, i] for i in range(3)])
+        bm = _body(q, [mag0[:, i] for i in range(3)])
+        for i in range(3):
+            g_val = w[i] + _noise(ph(4 + i), s_g)
+            a_val = G_MS2 * (ba[i] + _noise(ph(7 + i), s_a))
+            m_val = B_UT * (bm[i] + _noise(ph(10 + i), s_m))
+            vals[e, :, i] = np.where(ty == EV_ACC, a_val, np.where(ty == EV_GYRO, g_val, m_val)).astype(np.float32)
+        types[e] = ty
+        times[e] = t
+    return dict(types=types, values=vals, times=times, init_acc=G_MS2 * acc0, init_mag=B_UT * mag0,
+                t_init=np.full(K, T_INIT_NS, np.int64))
+
+
+def pack_events(ev):
+    """generate_events dict -> (EV float4 planes (E,K,4) f32, ET (E,K) int64)."""
+    E, K = ev["types"].shape
+    planes = np.empty((E, K, 4), np.float32)
+    planes[..., :3] = ev["values"]
+    planes[..., 3] = ev["types"].view(np.float32)
+    return planes, np.ascontiguousarray(ev["times"], np.int64)
+
+
 def window_bytes(batch, window):
     return int(batch) * int(window) * 40
 

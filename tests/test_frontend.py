@@ -1,0 +1,91 @@
+"""Server front-end: raw phone events -> records -> filter.
+
+PARITY UNPINNED: the checker is oracle/frontend_numpy.py, a restatement of the C++ front-end
+(KFS/Parser.cpp, KFS/KalmanFilter.cpp), which cannot be built here (Eigen, Windows headers) and
+ships no fixtures.  The filter that consumes the records is pinned as everywhere else."""
+import numpy as np
+import pytest
+
+from oracle import frontend_numpy as fe
+from poseestimationkf_amd import synth
+
+
+def _oracle_records(ev, k):
+    return fe.run_frontend(ev["types"][:, k], ev["values"][:, k].astype(np.float64), ev["times"][:, k],
+                           ev["init_acc"][k], ev["init_mag"][k], ev["t_init"][k])
+
+
+def test_oracle_state_machine_basics():
+    # acc0/mag0 from phase 2 at t=0; gyro @10, acc @20, mag @30 -> one record interpolated to t=10
+    types = [synth.EV_GYRO, synth.EV_ACC, synth.EV_MAG]
+    vals = np.array([[0.1, 0.2, 0.3], [0.0, 0.0, 2.0], [4.0, 0.0, 0.0]])
+    g, dt, a, m = fe.run_frontend(types, vals, [10, 20, 30], [0.0, 0.0, 1.0], [2.0, 0.0, 0.0], 0)
+    assert g.tolist() == [[0.1, 0.2, 0.3]] and dt.tolist() == [10]
+    # acc at t=10 between (0,0,1)@0 and (0,0,2)@20 = (0,0,1.5) -> unit (0,0,1) -> LPF from 0: 0.1
+    assert np.allclose(a, [[0.0, 0.0, 0.1]]) and np.allclose(m, [[0.1, 0.0, 0.0]])
+    # a second gyro before the pair completes shifts acc_1 into acc_0 and restarts the pairing
+    types = [synth.EV_GYRO, synth.EV_ACC, synth.EV_GYRO, synth.EV_ACC, synth.EV_MAG]
+    vals = np.array([[0, 0, 0], [0, 0, 1.0], [9, 9, 9], [0, 0, 1.0], [1.0, 0, 0]], float)
+    g, dt, a, m = fe.run_frontend(types, vals, [1, 2, 3, 4, 5], [0, 0, 1.0], [1.0, 0, 0], 0)
+    assert g.tolist() == [[9, 9, 9]] and dt.tolist() == [3]
+
+
+def test_oracle_records_are_lpf_of_unit_vectors():
+    ev = synth.generate_events(np.arange(2), 1500)
+    g, dt, a, m = _oracle_records(ev, 0)
+    assert len(dt) > 100 and (dt > 0).all() and (dt < 2 ** 31).all()
+    assert np.linalg.norm(a, axis=1).max() <= 1.0 + 1e-12
+    assert abs(np.linalg.norm(a[0]) - 0.1) < 1e-12            # first LPF output from the zero state
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from poseestimationkf_amd import engine
+    from poseestimationkf_amd._lib import device_count
+    assert device_count() > 0, "GPU tests need a HIP device"
+    return engine
+
+
+@pytest.mark.gpu
+def test_frontend_kernel_bit_exact_vs_oracle(eng):
+    K, E = 300, 1200
+    ev = synth.generate_events(np.arange(K), E, seed=7)
+    win, counts = eng.run_frontend(ev)
+    n = int(counts.max())
+    rec = win.download_filters(np.arange(K))
+    for k in range(0, K, 37):
+        g, dt, a, m = _oracle_records(ev, k)
+        r = len(dt)
+        assert counts[k] == r
+        assert np.array_equal(rec.gyro[:r, k], g.astype(np.float32))
+        assert np.array_equal(rec.dtw[:r, k], dt.astype(np.uint32))
+        assert np.array_equal(rec.acc[:r, k], a.astype(np.float32))
+        assert np.array_equal(rec.mag[:r, k], m.astype(np.float32))
+        an = np.asarray(ev["init_acc"][k]) / np.sqrt(((ev["init_acc"][k] ** 2).sum()))
+        assert np.abs(rec.acc0[k] - an).max() < 1e-15
+    assert n <= E // 3 + 1
+
+
+@pytest.mark.gpu
+def test_events_to_filter_end_to_end(eng, oracle_c):
+    """raw events -> front-end kernel -> fused filter, vs oracle front-end -> C oracle filter."""
+    K, E = 256, 1500
+    ev = synth.generate_events(np.arange(K), E, seed=8)
+    win, counts = eng.run_frontend(ev)
+    n = int(counts.min())
+    f = eng.BatchedEKF(K)
+    f.run(win, n_steps=n)
+    X, _ = f.get_state()
+    cols = np.arange(0, K, 16)
+    gy, dtw, acc, mag = [], [], [], []
+    for k in cols:
+        g, dt, a, m = _oracle_records(ev, k)
+        gy.append(g[:n]); dtw.append(dt[:n]); acc.append(a[:n]); mag.append(m[:n])
+    refs = win.refs.download((K, 6), np.float64)[cols]
+    rec = synth.Records(np.stack(gy, 1).astype(np.float32), np.stack(acc, 1).astype(np.float32),
+                        np.stack(mag, 1).astype(np.float32), np.stack(dtw, 1).astype(np.uint32),
+                        refs[:, :3], refs[:, 3:])
+    Xo, _, _ = oracle_c.run(rec)
+    err = float(np.abs(X[cols] - Xo).max())
+    print("events -> front-end -> filter vs oracle chain: max |dq| = %.3e over %d records" % (err, n))
+    assert err < 1e-9
