@@ -102,7 +102,8 @@ int pekf_predict(int64_t n, const double *gyro, const double *dt_ns, const doubl
                  double *K);
 int pekf_predict_dev(int64_t n, const double *gyro, const double *dt_ns, const double *X,
                      const double *P, const double *Q, const double *R, double *z, double *Pm,
-                     double *K, int *dev_singular /* device int, may be NULL */, void *stream);
+                     double *K, int32_t *status /* device int32[n]: 1 = S singular; may be NULL */,
+                     void *stream);
 
 /* KalmanFilter.Correction(Mag, Acc, z_k, P_k, K_k), ExtendedKalmanFilter.py:70-80, with the
  * filter's Wahba reference vectors acc0/mag0 (Wahba.__init__, Wahba.py:4-6).

@@ -50,7 +50,6 @@ Staging::~Staging() {
 
 int Staging::reserve(size_t bytes) {
     if (!stream_) PEKF_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    if (!flag_) PEKF_HIP(hipMalloc(&flag_, 64));
     if (bytes <= cap_) return PEKF_OK;
     size_t cap = cap_ ? cap_ : (size_t)1 << 16;
     while (cap < bytes) cap *= 2;
@@ -58,9 +57,13 @@ int Staging::reserve(size_t bytes) {
     if (host_) (void)hipHostFree(host_);
     dev_ = nullptr;
     host_ = nullptr;
+    host_dev_ = nullptr;
     cap_ = 0;
     PEKF_HIP(hipMalloc(&dev_, cap));
-    PEKF_HIP(hipHostMalloc(&host_, cap, hipHostMallocDefault));
+    // coherent, mapped pinned memory: small calls run zero-copy (the kernel reads its inputs and
+    // writes its outputs over PCIe), so a call costs one launch and one synchronisation
+    PEKF_HIP(hipHostMalloc(&host_, cap, hipHostMallocMapped | hipHostMallocCoherent));
+    PEKF_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&host_dev_), host_, 0));
     cap_ = cap;
     return PEKF_OK;
 }
@@ -74,21 +77,22 @@ int Staging::stage_in(std::initializer_list<HostArg> ins, std::initializer_list<
     size_t in_total = total;
     for (size_t b : out_bytes) total += align_up(b);
     if (int st = reserve(total)) return st;
+    zero_copy_ = total <= kZeroCopyMaxBytes;
+    char *base = zero_copy_ ? host_dev_ : dev_;
     size_t off = 0;
     int i = 0;
     for (const HostArg &a : ins) {
         if (a.bytes) std::memcpy(host_ + off, a.ptr, a.bytes);
-        dev_in[i++] = dev_ + off;
+        dev_in[i++] = base + off;
         off += align_up(a.bytes);
     }
     i = 0;
     for (size_t b : out_bytes) {
-        dev_out[i++] = dev_ + off;
+        dev_out[i++] = base + off;
         off += align_up(b);
     }
     in_bytes_ = in_total;
-    if (in_total) PEKF_HIP(hipMemcpyAsync(dev_, host_, in_total, hipMemcpyHostToDevice, stream_));
-    PEKF_HIP(hipMemsetAsync(flag_, 0, sizeof(int), stream_));
+    if (!zero_copy_ && in_total) PEKF_HIP(hipMemcpyAsync(dev_, host_, in_total, hipMemcpyHostToDevice, stream_));
     return PEKF_OK;
 }
 
@@ -96,7 +100,7 @@ int Staging::stage_out(std::initializer_list<HostOut> outs, void *const *dev_out
     // outputs were laid out contiguously right after the inputs: one D2H for all of them
     size_t total = 0;
     for (const HostOut &o : outs) total += align_up(o.bytes);
-    if (total) {
+    if (total && !zero_copy_) {
         PEKF_HIP(hipMemcpyAsync(host_ + in_bytes_, dev_out[0], total, hipMemcpyDeviceToHost, stream_));
     }
     PEKF_HIP(hipStreamSynchronize(stream_));

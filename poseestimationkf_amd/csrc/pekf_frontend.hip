@@ -5,7 +5,8 @@
 // accelerometer and a magnetometer sample after it, ExecuteKalmanFilter (Parser.cpp:229-257)
 // interpolates both to the gyro time (:259-267), normalises them (:221-228) and low-pass filters
 // them (alpha, from a zero state: KalmanFilter.cpp:16-18,21-24,279-303); the record's dt is the
-// gyro time minus the previous record's (KalmanFilter.cpp:306-308).  Arithmetic in FP64, records
+// gyro time minus the previous record's (KalmanFilter.cpp:306-308).  Arithmetic in FP64 (one
+// reciprocal / rsqrt with a Newton step instead of IEEE divisions: ~1e-15 relative), records
 // rounded to f32 like every record of the stream.  Event planes: EV float4 {x, y, z, bits(type)}
 // and ET int64, [n_events][batch]: 24 B per event, coalesced.
 #include "pekf_internal.hpp"
@@ -20,15 +21,18 @@ struct V3 {
     double x, y, z;
 };
 
+// Parser::LinearInterpolationSensor (:259-267): (y2 - y1) / (t2 - t1) * (t3 - t1) + y1, with the
+// division by (t2 - t1) taken once as a reciprocal (the emit path runs for the whole wave whenever
+// any lane emits a record, so its cost is paid on almost every event)
 __device__ __forceinline__ V3 lerp_to(int64_t t1, int64_t t2, int64_t t3, const V3 &a, const V3 &b) {
-    const double s = ((double)t3 - (double)t1);
-    const double d = ((double)t2 - (double)t1);
-    return {(b.x - a.x) / d * s + a.x, (b.y - a.y) / d * s + a.y, (b.z - a.z) / d * s + a.z};
+    const double f = ((double)t3 - (double)t1) * recip<true>((double)t2 - (double)t1);
+    return {(b.x - a.x) * f + a.x, (b.y - a.y) * f + a.y, (b.z - a.z) * f + a.z};
 }
 
+// Parser::NormalizeValues (:221-228) with one rsqrt instead of a sqrt and three divisions
 __device__ __forceinline__ V3 normalised(const V3 &v) {
-    const double n = sqrt((v.x * v.x + v.y * v.y) + v.z * v.z);
-    return {v.x / n, v.y / n, v.z / n};
+    const double in = rsqrt<true>((v.x * v.x + v.y * v.y) + v.z * v.z);
+    return {v.x * in, v.y * in, v.z * in};
 }
 
 __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_events,
@@ -40,7 +44,6 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
                                                        float4 *__restrict__ am, float2 *__restrict__ my,
                                                        int32_t *__restrict__ counts, double *__restrict__ refs,
                                                        int *__restrict__ err) {
-#pragma clang fp contract(off)  // same operation order and rounding as the C++ / the oracle
     const int64_t b = (int64_t)blockIdx.x * kFeBlock + threadIdx.x;
     if (b >= batch) return;
     // phase-2 state: acc_0 / mag_0 = raw means at the initialisation time (Parser.cpp:44-53)
@@ -59,9 +62,17 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
     const double beta = 1.0 - alpha;
     int64_t r = 0;
     int bad = 0;
+    // the next event is loaded before the current one is processed; latency is covered by
+    // occupancy (small register footprint: up to 8 waves per SIMD)
+    float4 nv4 = n_events > 0 ? ev[b] : make_float4(0.f, 0.f, 0.f, 0.f);
+    int64_t nt = n_events > 0 ? et[b] : 0;
     for (int64_t e = 0; e < n_events; ++e) {
-        const float4 v4 = ev[e * batch + b];
-        const int64_t t = et[e * batch + b];
+        const float4 v4 = nv4;
+        const int64_t t = nt;
+        if (e + 1 < n_events) {
+            nv4 = ev[(e + 1) * batch + b];
+            nt = et[(e + 1) * batch + b];
+        }
         const uint32_t ty = __float_as_uint(v4.w);
         const V3 v = {v4.x, v4.y, v4.z};
         if (!gyro_set) {

@@ -31,8 +31,11 @@ inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s);
 
 inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
 
-// One host<->device transfer in each direction for a host-pointer call: inputs are
-// packed into a pinned buffer, copied once, outputs copied back once.
+// Host-pointer calls: inputs are packed into one coherent, mapped pinned buffer.  Small calls
+// (<= kZeroCopyMaxBytes of inputs + outputs, e.g. the n = 1 calls of main_file.py) run
+// zero-copy: the kernel reads and writes that buffer over PCIe, so a call is one launch and one
+// synchronisation.  Larger calls copy it to device memory once each way.
+constexpr size_t kZeroCopyMaxBytes = (size_t)1 << 16;
 struct HostArg {
     const void *ptr;
     size_t bytes;
@@ -50,7 +53,6 @@ class Staging {
                  void **dev_in, void **dev_out);
     int stage_out(std::initializer_list<HostOut> outs, void *const *dev_out);
     hipStream_t stream() const { return stream_; }
-    int *dev_flag() const { return flag_; }
     ~Staging();
 
     static Staging &get();  // per calling thread, per current device
@@ -59,9 +61,10 @@ class Staging {
     hipStream_t stream_ = nullptr;
     char *dev_ = nullptr;
     char *host_ = nullptr;
-    int *flag_ = nullptr;
+    char *host_dev_ = nullptr;  // device address of host_
     size_t cap_ = 0;
     size_t in_bytes_ = 0;
+    bool zero_copy_ = false;
     int device_ = -1;
 };
 

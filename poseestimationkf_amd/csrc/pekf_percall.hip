@@ -2,6 +2,8 @@
 //
 // These keep the reference's dense formulation (ExtendedKalmanFilter.py, Wahba.py) so
 // each call matches NumPy to rounding; the fused time-loop kernel is pekf_run.hip.
+#include <vector>
+
 #include "pekf_internal.hpp"
 #include "pekf_math.hpp"
 
@@ -51,7 +53,7 @@ __global__ __launch_bounds__(kBlock) void k_predict(int64_t n, const double *gyr
                                                    const double *dt, const double *X,
                                                    const double *P, const double *Q,
                                                    const double *R, double *z, double *Pm,
-                                                   double *K, int *singular) {
+                                                   double *K, int32_t *status) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     double A[16], At[16], Jb[12], Jbt[12], t16[16], a16[16], t12[12], b16[16], S[16], Si[16], pm[16];
@@ -70,8 +72,9 @@ __global__ __launch_bounds__(kBlock) void k_predict(int64_t n, const double *gyr
         Pm[16 * i + k] = pm[k];
     }
     rk4_literal(X + 4 * i, dt[i], gyro + 3 * i, z + 4 * i);
-    if (!inverse4(S, Si)) {
-        if (singular) atomicOr(singular, 1);
+    const bool ok = inverse4(S, Si);
+    if (status) status[i] = ok ? 0 : 1;
+    if (!ok) {
 #pragma unroll
         for (int k = 0; k < 16; ++k) K[16 * i + k] = NAN;
         return;
@@ -84,13 +87,12 @@ __global__ __launch_bounds__(kBlock) void k_correct(int64_t n, const double *mag
                                                    const double *acc, const double *z,
                                                    const double *P, const double *K,
                                                    const double *acc0, const double *mag0,
-                                                   double *X, double *Pout, int *svd_fail) {
+                                                   double *X, double *Pout, int32_t *status) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const double *a = acc + 3 * i, *zz = z + 4 * i, *kk = K + 16 * i, *pp = P + 16 * i;
     const double ka = fabs(a[2]);
-    if (svd_fail && !wahba_b_finite(acc0 + 3 * i, mag0 + 3 * i, a, mag + 3 * i, ka, 1.0 - ka))
-        atomicOr(svd_fail, 1);
+    if (status) status[i] = wahba_b_finite(acc0 + 3 * i, mag0 + 3 * i, a, mag + 3 * i, ka, 1.0 - ka) ? 0 : 1;
     double R[9], y[4], e[4], ke[4], kp[16], x[4];
     wahba_rotation_vectors(acc0 + 3 * i, mag0 + 3 * i, a, mag + 3 * i, ka, 1.0 - ka, R);
     rotm_to_quat(R, y);
@@ -116,11 +118,11 @@ template <bool QUAT>
 __global__ __launch_bounds__(kBlock) void k_wahba(int64_t n, const double *acc0,
                                                  const double *mag0, const double *acc,
                                                  const double *mag, const double *ka,
-                                                 const double *km, double *out, int *svd_fail) {
+                                                 const double *km, double *out, int32_t *status) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    if (svd_fail && !wahba_b_finite(acc0 + 3 * i, mag0 + 3 * i, acc + 3 * i, mag + 3 * i, ka[i], km[i]))
-        atomicOr(svd_fail, 1);
+    if (status)
+        status[i] = wahba_b_finite(acc0 + 3 * i, mag0 + 3 * i, acc + 3 * i, mag + 3 * i, ka[i], km[i]) ? 0 : 1;
     double R[9];
     wahba_rotation_vectors(acc0 + 3 * i, mag0 + 3 * i, acc + 3 * i, mag + 3 * i, ka[i], km[i], R);
     if (QUAT) {
@@ -164,12 +166,12 @@ int pekf_rk4_dev(int64_t n, const double *q0, const double *dt_ns, const double 
 
 int pekf_predict_dev(int64_t n, const double *gyro, const double *dt_ns, const double *X,
                      const double *P, const double *Q, const double *R, double *z, double *Pm,
-                     double *K, int *dev_singular, void *stream) {
+                     double *K, int32_t *status, void *stream) {
     PEKF_CHECK_ARG(n >= 0, "n < 0");
     if (n == 0) return PEKF_OK;
     PEKF_CHECK_ARG(gyro && dt_ns && X && P && Q && R && z && Pm && K, "null pointer");
     hipLaunchKernelGGL(k_predict, PEKF_GRID(n), 0, as_stream(stream), n, gyro, dt_ns, X, P, Q, R,
-                       z, Pm, K, dev_singular);
+                       z, Pm, K, status);
     return launched("k_predict");
 }
 
@@ -270,19 +272,20 @@ int pekf_predict(int64_t n, const double *gyro, const double *dt_ns, const doubl
     if (int st = require_device()) return st;
     Staging &s = Staging::get();
     const size_t b = (size_t)n * sizeof(double);
-    void *in[6], *out[3];
+    const size_t sb = (size_t)n * sizeof(int32_t);
+    std::vector<int32_t> status((size_t)n);
+    void *in[6], *out[4];
     if (int st = s.stage_in({{gyro, 3 * b}, {dt_ns, b}, {X, 4 * b}, {P, 16 * b}, {Q, 9 * b}, {R, 16 * b}},
-                            {4 * b, 16 * b, 16 * b}, in, out))
+                            {4 * b, 16 * b, 16 * b, sb}, in, out))
         return st;
     hipLaunchKernelGGL(k_predict, PEKF_GRID(n), 0, s.stream(), n, D(const double *, in[0]),
                        D(const double *, in[1]), D(const double *, in[2]), D(const double *, in[3]),
                        D(const double *, in[4]), D(const double *, in[5]), D(double *, out[0]),
-                       D(double *, out[1]), D(double *, out[2]), s.dev_flag());
+                       D(double *, out[1]), D(double *, out[2]), D(int32_t *, out[3]));
     if (int st = launched("k_predict")) return st;
-    int singular = 0;
-    PEKF_HIP(hipMemcpyAsync(&singular, s.dev_flag(), sizeof(int), hipMemcpyDeviceToHost, s.stream()));
-    if (int st = s.stage_out({{z, 4 * b}, {Pm, 16 * b}, {K, 16 * b}}, out)) return st;
-    if (singular) return set_error(PEKF_ERR_SINGULAR, "Singular matrix");
+    if (int st = s.stage_out({{z, 4 * b}, {Pm, 16 * b}, {K, 16 * b}, {status.data(), sb}}, out)) return st;
+    for (int32_t v : status)
+        if (v) return set_error(PEKF_ERR_SINGULAR, "Singular matrix");
     return PEKF_OK;
 }
 
@@ -295,20 +298,21 @@ int pekf_correct(int64_t n, const double *mag, const double *acc, const double *
     if (int st = require_device()) return st;
     Staging &s = Staging::get();
     const size_t b = (size_t)n * sizeof(double);
-    void *in[7], *out[2];
+    const size_t sb = (size_t)n * sizeof(int32_t);
+    std::vector<int32_t> status((size_t)n);
+    void *in[7], *out[3];
     if (int st = s.stage_in({{mag, 3 * b}, {acc, 3 * b}, {z, 4 * b}, {P, 16 * b}, {K, 16 * b},
                              {acc0, 3 * b}, {mag0, 3 * b}},
-                            {4 * b, 16 * b}, in, out))
+                            {4 * b, 16 * b, sb}, in, out))
         return st;
     hipLaunchKernelGGL(k_correct, PEKF_GRID(n), 0, s.stream(), n, D(const double *, in[0]),
                        D(const double *, in[1]), D(const double *, in[2]), D(const double *, in[3]),
                        D(const double *, in[4]), D(const double *, in[5]), D(const double *, in[6]),
-                       D(double *, out[0]), D(double *, out[1]), s.dev_flag());
+                       D(double *, out[0]), D(double *, out[1]), D(int32_t *, out[2]));
     if (int st = launched("k_correct")) return st;
-    int fail = 0;
-    PEKF_HIP(hipMemcpyAsync(&fail, s.dev_flag(), sizeof(int), hipMemcpyDeviceToHost, s.stream()));
-    if (int st = s.stage_out({{X, 4 * b}, {P_out, 16 * b}}, out)) return st;
-    if (fail) return set_error(PEKF_ERR_SVD, "SVD did not converge");
+    if (int st = s.stage_out({{X, 4 * b}, {P_out, 16 * b}, {status.data(), sb}}, out)) return st;
+    for (int32_t v : status)
+        if (v) return set_error(PEKF_ERR_SVD, "SVD did not converge");
     return PEKF_OK;
 }
 
@@ -322,25 +326,26 @@ static int wahba_host(bool quat, int64_t n, const double *acc0, const double *ma
     Staging &s = Staging::get();
     const size_t b = (size_t)n * sizeof(double);
     const size_t ob = (quat ? 4 : 9) * b;
-    void *in[6], *out[1];
+    const size_t sb = (size_t)n * sizeof(int32_t);
+    std::vector<int32_t> status((size_t)n);
+    void *in[6], *out[2];
     if (int st = s.stage_in({{acc0, 3 * b}, {mag0, 3 * b}, {acc, 3 * b}, {mag, 3 * b}, {k_acc, b}, {k_mag, b}},
-                            {ob}, in, out))
+                            {ob, sb}, in, out))
         return st;
     if (quat)
         hipLaunchKernelGGL(k_wahba<true>, PEKF_GRID(n), 0, s.stream(), n, D(const double *, in[0]),
                            D(const double *, in[1]), D(const double *, in[2]), D(const double *, in[3]),
                            D(const double *, in[4]), D(const double *, in[5]), D(double *, out[0]),
-                           s.dev_flag());
+                           D(int32_t *, out[1]));
     else
         hipLaunchKernelGGL(k_wahba<false>, PEKF_GRID(n), 0, s.stream(), n, D(const double *, in[0]),
                            D(const double *, in[1]), D(const double *, in[2]), D(const double *, in[3]),
                            D(const double *, in[4]), D(const double *, in[5]), D(double *, out[0]),
-                           s.dev_flag());
+                           D(int32_t *, out[1]));
     if (int st = launched("k_wahba")) return st;
-    int fail = 0;
-    PEKF_HIP(hipMemcpyAsync(&fail, s.dev_flag(), sizeof(int), hipMemcpyDeviceToHost, s.stream()));
-    if (int st = s.stage_out({{res, ob}}, out)) return st;
-    if (fail) return set_error(PEKF_ERR_SVD, "SVD did not converge");
+    if (int st = s.stage_out({{res, ob}, {status.data(), sb}}, out)) return st;
+    for (int32_t v : status)
+        if (v) return set_error(PEKF_ERR_SVD, "SVD did not converge");
     return PEKF_OK;
 }
 

@@ -1,0 +1,144 @@
+#!/usr/bin/env python3
+"""Measurements of the kernels beside the headline fused run (one JSON object on stdout).
+
+  frontend      pekf_frontend_dev: raw phone events -> records; HBM-bound:
+                24 B read per event + 40 B written per record
+  gyro_chain    pekf_gyro_chain_dev (§8f-3): 16 B read per filter-record
+  wahba_stream  pekf_wahba_stream_dev (§8f-3): 24 B read + 32 B written per filter-record
+  predict_dev / correct_dev   per-call operators at n = 1M items (device pointers)
+  dropin_call   host-pointer per-call latency at n = 1 (the path main_file.py takes)
+
+Kernel times are HIP events on the launch stream; run under rocprofv3 --kernel-trace --stats
+for the per-kernel summary committed in profiles/.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from poseestimationkf_amd import engine, synth  # noqa: E402
+from poseestimationkf_amd._lib import check, lib  # noqa: E402
+
+HBM = 8000.0
+
+
+def log(m):
+    print("[aux] " + m, file=sys.stderr, flush=True)
+
+
+def timed(fn, stream, reps=3):
+    e0, e1 = engine.Event(), engine.Event()
+    fn()
+    check(lib.pekf_stream_sync(stream))
+    out = []
+    for _ in range(reps):
+        e0.record(stream)
+        fn()
+        e1.record(stream)
+        e1.sync()
+        out.append(e0.elapsed_ms(e1))
+    return float(np.median(out))
+
+
+def main():
+    st = engine.Stream()
+    s = st.handle
+    res = {}
+
+    # ---- front-end: 16K generated event streams tiled x64 -> 1,048,576 filters x 1,024 events
+    K0, E, tile = 16384, 1024, 64
+    log("generating %d x %d events" % (K0, E))
+    ev = synth.generate_events(np.arange(K0), E, seed=11)
+    planes, times = synth.pack_events(ev)
+    planes = np.ascontiguousarray(np.tile(planes, (1, tile, 1)))
+    times = np.ascontiguousarray(np.tile(times, (1, tile)))
+    K = K0 * tile
+    init = np.tile(np.concatenate([ev["init_acc"], ev["init_mag"]], axis=1), (tile, 1))
+    tinit = np.tile(ev["t_init"], tile)
+    evb = engine.DeviceBuffer(planes.nbytes).upload(planes)
+    etb = engine.DeviceBuffer(times.nbytes).upload(times)
+    del planes, times
+    ib = engine.DeviceBuffer(init.nbytes).upload(init)
+    tb = engine.DeviceBuffer(tinit.nbytes).upload(tinit.astype(np.int64))
+    r_max = E // 3 + 1
+    win = engine.IMUWindow(K, r_max)
+    cnt = engine.DeviceBuffer(4 * K)
+    err = engine.DeviceBuffer(4).upload(np.zeros(1, np.int32))
+    ms = timed(lambda: check(lib.pekf_frontend_dev(K, E, evb.ptr, etb.ptr, ib.ptr, tb.ptr, 0.1, r_max, win.gd.ptr,
+                                                   win.am.ptr, win.my.ptr, cnt.ptr, win.refs.ptr, err.ptr, s)), s)
+    counts = cnt.download((K,), np.int32)
+    recs = int(counts.sum())
+    byts = K * E * 24 + recs * 40
+    res["frontend"] = {"filters": K, "events_per_filter": E, "records": recs, "kernel_ms": ms,
+                       "events_per_s": K * E / (ms * 1e-3), "gbs": byts / (ms * 1e-3) / 1e9,
+                       "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM, "bytes": byts}
+    log("frontend: %.2f ms, %.2e events/s, %.0f GB/s" % (ms, K * E / (ms * 1e-3), byts / (ms * 1e-3) / 1e9))
+    del evb, etb, win
+
+    # ---- side outputs on a config-3-sized window
+    B, W, N = 1 << 20, 1024, 10000
+    win = engine.IMUWindow(B, W).synthesize(stream=s)
+    q = engine.DeviceBuffer(32 * B).upload(np.tile([1.0, 0, 0, 0], (B, 1)))
+    ms = timed(lambda: check(lib.pekf_gyro_chain_dev(B, N, W, 0, win.gd.ptr, q.ptr, None, s)), s)
+    res["gyro_chain"] = {"filters": B, "records": N, "kernel_ms": ms, "steps_per_s": B * N / (ms * 1e-3),
+                         "gbs": B * N * 16 / (ms * 1e-3) / 1e9, "hbm_frac": B * N * 16 / (ms * 1e-3) / 1e9 / HBM}
+    log("gyro chain: %.1f ms" % ms)
+    Nw = 1024
+    out = engine.DeviceBuffer(32 * B * Nw)
+    ms = timed(lambda: check(lib.pekf_wahba_stream_dev(B, Nw, W, 0, win.am.ptr, win.my.ptr, win.refs.ptr, 0.5, 0.5,
+                                                       out.ptr, s)), s)
+    res["wahba_stream"] = {"filters": B, "records": Nw, "kernel_ms": ms, "quats_per_s": B * Nw / (ms * 1e-3),
+                           "gbs": B * Nw * 56 / (ms * 1e-3) / 1e9, "hbm_frac": B * Nw * 56 / (ms * 1e-3) / 1e9 / HBM}
+    log("wahba stream: %.1f ms" % ms)
+    del win, out
+
+    # ---- per-call operators at n = 1M (device pointers)
+    n = 1 << 20
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(n, 4))
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    bufs = {k: engine.DeviceBuffer(a.nbytes).upload(np.ascontiguousarray(a)) for k, a in dict(
+        g=rng.normal(size=(n, 3)), dt=np.full(n, 1e7), X=X, P=np.tile(np.eye(4), (n, 1, 1)),
+        Q=np.tile(np.eye(3), (n, 1, 1)), R=np.tile(np.eye(4) * 0.1, (n, 1, 1)), acc=X[:, :3].copy(),
+        mag=X[:, 1:].copy(), a0=np.tile([0, 0, 1.0], (n, 1)), m0=np.tile([0.5, 0, -0.86], (n, 1))).items()}
+    z, Pm, Kk, Xo, Po = (engine.DeviceBuffer(8 * n * k) for k in (4, 16, 16, 4, 16))
+    b = bufs
+    ms = timed(lambda: check(lib.pekf_predict_dev(n, b["g"].ptr, b["dt"].ptr, b["X"].ptr, b["P"].ptr, b["Q"].ptr,
+                                                  b["R"].ptr, z.ptr, Pm.ptr, Kk.ptr, None, s)), s)
+    byts = n * 8 * (3 + 1 + 4 + 16 + 9 + 16 + 4 + 16 + 16)
+    res["predict_dev"] = {"n": n, "kernel_ms": ms, "items_per_s": n / (ms * 1e-3), "gbs": byts / (ms * 1e-3) / 1e9,
+                          "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM}
+    ms = timed(lambda: check(lib.pekf_correct_dev(n, b["mag"].ptr, b["acc"].ptr, z.ptr, Pm.ptr, Kk.ptr, b["a0"].ptr,
+                                                  b["m0"].ptr, Xo.ptr, Po.ptr, s)), s)
+    byts = n * 8 * (3 + 3 + 4 + 16 + 16 + 3 + 3 + 4 + 16)
+    res["correct_dev"] = {"n": n, "kernel_ms": ms, "items_per_s": n / (ms * 1e-3), "gbs": byts / (ms * 1e-3) / 1e9,
+                          "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM}
+    log("per-call predict %.2f ms, correct %.2f ms at n=1M" % (res["predict_dev"]["kernel_ms"], ms))
+
+    # ---- drop-in latency at n = 1 (host pointers, what main_file.py pays per call)
+    gy, X1, P1, Q1, R1 = [0.1, 0.2, 0.3], np.array([1.0, 0, 0, 0]), np.eye(4), np.eye(3), np.eye(4) * 0.1
+    lat = {"predict": [], "correct": []}
+    for i in range(300):
+        t0 = time.perf_counter()
+        zz, pm, kk = engine.predict(gy, 1e7, X1, P1, Q1, R1)
+        t1 = time.perf_counter()
+        engine.correct([0.5, 0, -0.86], [0, 0.1, 0.99], zz, pm, kk, [0, 0, 1.0], [0.5, 0, -0.86])
+        t2 = time.perf_counter()
+        if i >= 50:
+            lat["predict"].append(t1 - t0)
+            lat["correct"].append(t2 - t1)
+    res["dropin_call_us"] = {k: float(np.median(v) * 1e6) for k, v in lat.items()}
+    log("drop-in latency: %s" % res["dropin_call_us"])
+    res["device"] = engine.device_name(0)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

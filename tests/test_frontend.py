@@ -46,8 +46,15 @@ def eng():
     return engine
 
 
+def _f32_ulps(a, b):
+    a = np.ascontiguousarray(a, np.float32).view(np.int32).astype(np.int64)
+    b = np.ascontiguousarray(b, np.float32).view(np.int32).astype(np.int64)
+    return np.abs(a - b).max(initial=0)
+
+
 @pytest.mark.gpu
-def test_frontend_kernel_bit_exact_vs_oracle(eng):
+def test_frontend_kernel_vs_oracle(eng):
+    """Records equal the oracle's up to 1 f32 ulp (the kernel divides by reciprocal / rsqrt)."""
     K, E = 300, 1200
     ev = synth.generate_events(np.arange(K), E, seed=7)
     win, counts = eng.run_frontend(ev)
@@ -59,8 +66,8 @@ def test_frontend_kernel_bit_exact_vs_oracle(eng):
         assert counts[k] == r
         assert np.array_equal(rec.gyro[:r, k], g.astype(np.float32))
         assert np.array_equal(rec.dtw[:r, k], dt.astype(np.uint32))
-        assert np.array_equal(rec.acc[:r, k], a.astype(np.float32))
-        assert np.array_equal(rec.mag[:r, k], m.astype(np.float32))
+        assert _f32_ulps(rec.acc[:r, k], a) <= 1
+        assert _f32_ulps(rec.mag[:r, k], m) <= 1
         an = np.asarray(ev["init_acc"][k]) / np.sqrt(((ev["init_acc"][k] ** 2).sum()))
         assert np.abs(rec.acc0[k] - an).max() < 1e-15
     assert n <= E // 3 + 1

@@ -178,6 +178,30 @@ def test_scale_c2_batch_sampled_against_oracle(eng, oracle_c):
     assert err < ATOL_Q and err < PREC_GUARD
 
 
+@pytest.mark.parametrize("name,batch,missing", [("C2", 65536, False), ("C3", 1 << 20, False),
+                                                ("C5", 1 << 20, True)])
+def test_full_size_configs_sampled_against_oracle(eng, oracle_c, name, batch, missing):
+    """BASELINE.json configs 2/3/5 at full size (10,000 records over a 1,024-record resident window):
+    64 filters spread over the batch re-run by the C oracle; every filter's X stays unit-norm."""
+    W, N = 1024, 10000
+    win = eng.IMUWindow(batch, W).synthesize(seed=synth.DEFAULT_SEED, missing=missing)
+    f = eng.BatchedEKF(batch)
+    f.run(win, n_steps=N)
+    X, P = f.get_state()
+    assert np.isfinite(X).all() and np.isfinite(P).all()
+    assert np.abs(np.linalg.norm(X, axis=1) - 1).max() < 1e-12
+    eig = np.linalg.eigvalsh(P[:: max(1, batch // 4096)])
+    assert eig.min() > 0                                 # covariance stays positive definite
+    if not missing:                                      # after a correction P = r I - r^2 S^-1 < r I
+        assert eig.max() < 0.1 + 1e-12
+    cols = np.linspace(0, batch - 1, 64).astype(np.int64)
+    rec = synth.generate(cols, W, seed=synth.DEFAULT_SEED, missing=missing)
+    Xo, _, _ = oracle_c.run(rec, n_steps=N)
+    err = _maxerr(X[cols], Xo)
+    print("%s full size (%d filters x %d records): sampled max |dq| = %.3e" % (name, batch, N, err))
+    assert err < ATOL_Q and err < PREC_GUARD
+
+
 def test_batch_of_one(eng, traj):
     sl = slice(0, 1)
     win = eng.IMUWindow.from_planes(traj["gd"][:, sl], traj["am"][:, sl], traj["my"][:, sl],
