@@ -174,12 +174,13 @@ int pekf_log_read(const char *path, int64_t n_records, float *gyro, float *acc, 
  * normalisation (:221-228) and the alpha low-pass from a zero state (KFS/KalmanFilter.cpp:16-18,
  * 21-24,279-303) -> records written to plane_gd / plane_am / plane_my rows 0..counts[b]-1
  * ([r_max][batch], the layout pekf_run_dev reads), dt = gyro time - previous record's (initially
- * t_init[b]).  Events: ev_planes float4 [n_events][batch] {x, y, z, bits(type: 0 acc, 1 gyro,
- * 2 mag)}, ev_times int64 ns [n_events][batch].  init[batch*6] = raw phase-2 means {acc xyz, mag
- * xyz} (Parser.cpp:44-53); refs[batch*6] receives their normalised values (the filter's acc0 /
- * mag0).  *dev_error |= 1 if a dt does not fit 31 bits, 2 if a filter had more than r_max records. */
-int pekf_frontend_dev(int64_t batch, int64_t n_events, const void *ev_planes, const int64_t *ev_times,
-                      const double *init, const int64_t *t_init, double alpha, int64_t r_max,
+ * t_init[b]).  Events: ev_planes float4 [n_events][batch] {x, y, z, bits(word)}, 16 B each, with
+ * word = (ns since the filter's previous event, first: since t_init[b]) << 2 | type (0 acc, 1 gyro,
+ * 2 mag), so gaps must be < 2^30 ns.  init[batch*6] = raw phase-2 means {acc xyz, mag xyz}
+ * (Parser.cpp:44-53); refs[batch*6] receives their normalised values (the filter's acc0 / mag0).
+ * *dev_error |= 1 if a record dt does not fit 31 bits, 2 if a filter had more than r_max records. */
+int pekf_frontend_dev(int64_t batch, int64_t n_events, const void *ev_planes, const double *init,
+                      const int64_t *t_init, double alpha, int64_t r_max,
                       void *plane_gd, void *plane_am, void *plane_my, int32_t *counts, double *refs,
                       int *dev_error, void *stream);
 

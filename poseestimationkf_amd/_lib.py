@@ -78,7 +78,7 @@ SIGNATURES = {
     "pekf_gyro_chain_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "pekf_wahba_stream_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp],
     "pekf_quat_to_rpy": [_i64, _dp, _dp],
-    "pekf_frontend_dev": [_i64, _i64, _vp, _vp, _vp, _vp, _dbl, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "pekf_frontend_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "pekf_log_scan": [ctypes.c_char_p, ctypes.POINTER(_i64)],
     "pekf_log_read": [ctypes.c_char_p, _i64, _vp, _vp, _vp, _vp, _dp, _dp, _dp],
     "pekf_quat_to_rpy_dev": [_i64, _vp, _vp, _vp],

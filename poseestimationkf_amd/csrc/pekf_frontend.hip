@@ -7,8 +7,8 @@
 // them (alpha, from a zero state: KalmanFilter.cpp:16-18,21-24,279-303); the record's dt is the
 // gyro time minus the previous record's (KalmanFilter.cpp:306-308).  Arithmetic in FP64 (one
 // reciprocal / rsqrt with a Newton step instead of IEEE divisions: ~1e-15 relative), records
-// rounded to f32 like every record of the stream.  Event planes: EV float4 {x, y, z, bits(type)}
-// and ET int64, [n_events][batch]: 24 B per event, coalesced.
+// rounded to f32 like every record of the stream.  Event plane: EV float4 {x, y, z, bits(word)},
+// word = (ns gap to the previous event << 2) | type, [n_events][batch]: 16 B per event, coalesced.
 #include "pekf_internal.hpp"
 #include "pekf_math.hpp"
 
@@ -20,6 +20,10 @@ enum : uint32_t { kEvAcc = 0, kEvGyro = 1, kEvMag = 2 };
 struct V3 {
     double x, y, z;
 };
+struct F3 {
+    float x, y, z;
+};
+__device__ __forceinline__ V3 widen(const F3 &f) { return {f.x, f.y, f.z}; }
 
 // Parser::LinearInterpolationSensor (:259-267): (y2 - y1) / (t2 - t1) * (t3 - t1) + y1, with the
 // division by (t2 - t1) taken once as a reciprocal (the emit path runs for the whole wave whenever
@@ -37,7 +41,6 @@ __device__ __forceinline__ V3 normalised(const V3 &v) {
 
 __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_events,
                                                        const float4 *__restrict__ ev,
-                                                       const int64_t *__restrict__ et,
                                                        const double *__restrict__ init,
                                                        const int64_t *__restrict__ t_init, double alpha,
                                                        int64_t r_max, float4 *__restrict__ gd,
@@ -55,7 +58,7 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
         refs[6 * b + 0] = a.x; refs[6 * b + 1] = a.y; refs[6 * b + 2] = a.z;
         refs[6 * b + 3] = m.x; refs[6 * b + 4] = m.y; refs[6 * b + 5] = m.z;
     }
-    V3 acc1 = {0, 0, 0}, mag1 = {0, 0, 0}, gyro = {0, 0, 0};
+    F3 acc1 = {0, 0, 0}, mag1 = {0, 0, 0}, gyro = {0, 0, 0};  // sensor samples: exact in f32
     int64_t t_acc1 = 0, t_mag1 = 0, t_gyro = 0;
     bool gyro_set = false, acc1_set = false, mag1_set = false;
     V3 lpf_acc = {0, 0, 0}, lpf_mag = {0, 0, 0};
@@ -63,36 +66,34 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
     int64_t r = 0;
     int bad = 0;
     // the next event is loaded before the current one is processed; latency is covered by
-    // occupancy (small register footprint: up to 8 waves per SIMD)
+    // occupancy (small register footprint)
     float4 nv4 = n_events > 0 ? ev[b] : make_float4(0.f, 0.f, 0.f, 0.f);
-    int64_t nt = n_events > 0 ? et[b] : 0;
+    int64_t t = t_init[b];
     for (int64_t e = 0; e < n_events; ++e) {
         const float4 v4 = nv4;
-        const int64_t t = nt;
-        if (e + 1 < n_events) {
-            nv4 = ev[(e + 1) * batch + b];
-            nt = et[(e + 1) * batch + b];
-        }
-        const uint32_t ty = __float_as_uint(v4.w);
-        const V3 v = {v4.x, v4.y, v4.z};
+        if (e + 1 < n_events) nv4 = ev[(e + 1) * batch + b];
+        const uint32_t word = __float_as_uint(v4.w);
+        const uint32_t ty = word & 3u;
+        t += (int64_t)(word >> 2);  // the event word carries the ns gap to the previous event
+        const F3 v = {v4.x, v4.y, v4.z};
         if (!gyro_set) {
-            if (ty == kEvAcc) { acc0 = v; t_acc0 = t; }
-            else if (ty == kEvMag) { mag0 = v; t_mag0 = t; }
+            if (ty == kEvAcc) { acc0 = widen(v); t_acc0 = t; }
+            else if (ty == kEvMag) { mag0 = widen(v); t_mag0 = t; }
             else if (ty == kEvGyro) { gyro = v; t_gyro = t; gyro_set = true; }
         } else {
             if (ty == kEvAcc) { acc1 = v; t_acc1 = t; acc1_set = true; }
             else if (ty == kEvMag) { mag1 = v; t_mag1 = t; mag1_set = true; }
             else if (ty == kEvGyro) {
                 gyro = v; t_gyro = t;
-                if (acc1_set) { acc0 = acc1; t_acc0 = t_acc1; }
-                if (mag1_set) { mag0 = mag1; t_mag0 = t_mag1; }
+                if (acc1_set) { acc0 = widen(acc1); t_acc0 = t_acc1; }
+                if (mag1_set) { mag0 = widen(mag1); t_mag0 = t_mag1; }
                 acc1_set = mag1_set = false;
             }
         }
         if (acc1_set && mag1_set) {
             gyro_set = acc1_set = mag1_set = false;
-            const V3 a = normalised(lerp_to(t_acc0, t_acc1, t_gyro, acc0, acc1));
-            const V3 m = normalised(lerp_to(t_mag0, t_mag1, t_gyro, mag0, mag1));
+            const V3 a = normalised(lerp_to(t_acc0, t_acc1, t_gyro, acc0, widen(acc1)));
+            const V3 m = normalised(lerp_to(t_mag0, t_mag1, t_gyro, mag0, widen(mag1)));
             lpf_mag = {alpha * m.x + beta * lpf_mag.x, alpha * m.y + beta * lpf_mag.y, alpha * m.z + beta * lpf_mag.z};
             lpf_acc = {alpha * a.x + beta * lpf_acc.x, alpha * a.y + beta * lpf_acc.y, alpha * a.z + beta * lpf_acc.z};
             const int64_t dt = t_gyro - prev_t;
@@ -108,8 +109,8 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
             }
             ++r;
             prev_t = t_gyro;
-            acc0 = acc1; t_acc0 = t_acc1;
-            mag0 = mag1; t_mag0 = t_mag1;
+            acc0 = widen(acc1); t_acc0 = t_acc1;
+            mag0 = widen(mag1); t_mag0 = t_mag1;
         }
     }
     counts[b] = (int32_t)(r < r_max ? r : r_max);
@@ -120,16 +121,15 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
 
 using namespace pekf;
 
-extern "C" int pekf_frontend_dev(int64_t batch, int64_t n_events, const void *ev_planes, const int64_t *ev_times,
-                                 const double *init, const int64_t *t_init, double alpha, int64_t r_max,
-                                 void *plane_gd, void *plane_am, void *plane_my, int32_t *counts, double *refs,
+extern "C" int pekf_frontend_dev(int64_t batch, int64_t n_events, const void *ev_planes, const double *init,
+                                 const int64_t *t_init, double alpha, int64_t r_max, void *plane_gd, void *plane_am, void *plane_my, int32_t *counts, double *refs,
                                  int *dev_error, void *stream) {
     PEKF_CHECK_ARG(batch >= 0 && n_events >= 0 && r_max >= 0, "negative size");
     if (batch == 0) return PEKF_OK;
-    PEKF_CHECK_ARG(ev_planes && ev_times && init && t_init && plane_gd && plane_am && plane_my && counts && refs,
+    PEKF_CHECK_ARG(ev_planes && init && t_init && plane_gd && plane_am && plane_my && counts && refs,
                    "null pointer");
     hipLaunchKernelGGL(k_frontend, dim3(grid_for(batch, kFeBlock)), dim3(kFeBlock), 0, as_stream(stream), batch,
-                       n_events, static_cast<const float4 *>(ev_planes), ev_times, init, t_init, alpha, r_max,
+                       n_events, static_cast<const float4 *>(ev_planes), init, t_init, alpha, r_max,
                        static_cast<float4 *>(plane_gd), static_cast<float4 *>(plane_am),
                        static_cast<float2 *>(plane_my), counts, refs, dev_error);
     hipError_t e = hipGetLastError();

@@ -226,17 +226,16 @@ def run_frontend(ev, alpha=0.1, r_max=None):
     Runs pekf_frontend_dev.  Every record needs a gyro, an accelerometer and a
     magnetometer event, so r_max defaults to n_events // 3 + 1.  Raises if a dt does not fit the
     31-bit record field or a filter overflows r_max."""
-    planes, times = synth.pack_events(ev)
-    E, K = times.shape
+    planes = synth.pack_events(ev)
+    E, K = planes.shape[:2]
     r_max = E // 3 + 1 if r_max is None else int(r_max)
     evb = DeviceBuffer(planes.nbytes).upload(planes)
-    etb = DeviceBuffer(times.nbytes).upload(times)
     init = DeviceBuffer(48 * K).upload(np.concatenate([ev["init_acc"], ev["init_mag"]], axis=1).astype(np.float64))
     tib = DeviceBuffer(8 * K).upload(np.ascontiguousarray(ev["t_init"], np.int64))
     win = IMUWindow(K, max(1, r_max))
     cnt = DeviceBuffer(4 * K)
     errb = DeviceBuffer(4).upload(np.zeros(1, np.int32))
-    check(lib.pekf_frontend_dev(K, E, evb.ptr, etb.ptr, init.ptr, tib.ptr, float(alpha), r_max, win.gd.ptr,
+    check(lib.pekf_frontend_dev(K, E, evb.ptr, init.ptr, tib.ptr, float(alpha), r_max, win.gd.ptr,
                                 win.am.ptr, win.my.ptr, cnt.ptr, win.refs.ptr, errb.ptr, None))
     check(lib.pekf_device_sync())
     err = int(errb.download((1,), np.int32)[0])

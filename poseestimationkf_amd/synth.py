@@ -294,13 +294,25 @@ def generate_events(ids, n_events, seed=DEFAULT_SEED, params=SynthParams()):
                 t_init=np.full(K, T_INIT_NS, np.int64))
 
 
+EV_DT_BITS = 30  # event word = (ns since the previous event << 2) | type
+
+
 def pack_events(ev):
-    """generate_events dict -> (EV float4 planes (E,K,4) f32, ET (E,K) int64)."""
+    """generate_events dict -> EV float4 plane (E,K,4) f32 {x, y, z, bits(word)}.
+
+    16 B per event: the word carries the 2-bit type and the ns gap to the filter's previous
+    event (the first one: to t_init), which must be in [0, 2^30)."""
     E, K = ev["types"].shape
+    times = np.asarray(ev["times"], np.int64)
+    prev = np.concatenate([np.asarray(ev["t_init"], np.int64)[None, :], times[:-1]], axis=0)
+    gap = times - prev
+    if E and (gap.min() < 0 or gap.max() >= (1 << EV_DT_BITS)):
+        raise ValueError("event gaps must be in [0, 2^%d) ns" % EV_DT_BITS)
+    word = ((gap.astype(np.uint64) << np.uint64(2)) | np.asarray(ev["types"], np.uint64)).astype(np.uint32)
     planes = np.empty((E, K, 4), np.float32)
     planes[..., :3] = ev["values"]
-    planes[..., 3] = ev["types"].view(np.float32)
-    return planes, np.ascontiguousarray(ev["times"], np.int64)
+    planes[..., 3] = word.view(np.float32)
+    return planes
 
 
 def window_bytes(batch, window):

@@ -2,7 +2,7 @@
 """Measurements of the kernels beside the headline fused run (one JSON object on stdout).
 
   frontend      pekf_frontend_dev: raw phone events -> records; HBM-bound:
-                24 B read per event + 40 B written per record
+                16 B read per event + 40 B written per record
   gyro_chain    pekf_gyro_chain_dev (§8f-3): 16 B read per filter-record
   wahba_stream  pekf_wahba_stream_dev (§8f-3): 24 B read + 32 B written per filter-record
   predict_dev / correct_dev   per-call operators at n = 1M items (device pointers)
@@ -56,31 +56,28 @@ def main():
     K0, E, tile = 16384, 1024, 64
     log("generating %d x %d events" % (K0, E))
     ev = synth.generate_events(np.arange(K0), E, seed=11)
-    planes, times = synth.pack_events(ev)
-    planes = np.ascontiguousarray(np.tile(planes, (1, tile, 1)))
-    times = np.ascontiguousarray(np.tile(times, (1, tile)))
+    planes = np.ascontiguousarray(np.tile(synth.pack_events(ev), (1, tile, 1)))
     K = K0 * tile
     init = np.tile(np.concatenate([ev["init_acc"], ev["init_mag"]], axis=1), (tile, 1))
     tinit = np.tile(ev["t_init"], tile)
     evb = engine.DeviceBuffer(planes.nbytes).upload(planes)
-    etb = engine.DeviceBuffer(times.nbytes).upload(times)
-    del planes, times
+    del planes
     ib = engine.DeviceBuffer(init.nbytes).upload(init)
     tb = engine.DeviceBuffer(tinit.nbytes).upload(tinit.astype(np.int64))
     r_max = E // 3 + 1
     win = engine.IMUWindow(K, r_max)
     cnt = engine.DeviceBuffer(4 * K)
     err = engine.DeviceBuffer(4).upload(np.zeros(1, np.int32))
-    ms = timed(lambda: check(lib.pekf_frontend_dev(K, E, evb.ptr, etb.ptr, ib.ptr, tb.ptr, 0.1, r_max, win.gd.ptr,
+    ms = timed(lambda: check(lib.pekf_frontend_dev(K, E, evb.ptr, ib.ptr, tb.ptr, 0.1, r_max, win.gd.ptr,
                                                    win.am.ptr, win.my.ptr, cnt.ptr, win.refs.ptr, err.ptr, s)), s)
     counts = cnt.download((K,), np.int32)
     recs = int(counts.sum())
-    byts = K * E * 24 + recs * 40
+    byts = K * E * 16 + recs * 40
     res["frontend"] = {"filters": K, "events_per_filter": E, "records": recs, "kernel_ms": ms,
                        "events_per_s": K * E / (ms * 1e-3), "gbs": byts / (ms * 1e-3) / 1e9,
                        "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM, "bytes": byts}
     log("frontend: %.2f ms, %.2e events/s, %.0f GB/s" % (ms, K * E / (ms * 1e-3), byts / (ms * 1e-3) / 1e9))
-    del evb, etb, win
+    del evb, win
 
     # ---- side outputs on a config-3-sized window
     B, W, N = 1 << 20, 1024, 10000
