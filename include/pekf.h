@@ -46,6 +46,9 @@ extern "C" {
  * PEKF_RUN_MIXED_PRECISION: opt-in; the covariance recursion (P-, S^-1, K, P) in FP32, the
  * quaternion path (RK4, Wahba, R->q, X update) in FP64.  Quaternions stay within ~1e-8 of FP64. */
 #define PEKF_RUN_MIXED_PRECISION 0x1u
+/* PEKF_RUN_STATE_SOA: X and P are in the coalesced SoA layout of pekf_state_layout_dev (for launches
+ * that cover few records, where the state read/write dominates: online serving). */
+#define PEKF_RUN_STATE_SOA 0x2u
 
 int pekf_abi_version(void);
 const char *pekf_last_error(void);
@@ -139,11 +142,18 @@ int pekf_rotmat_to_quat(int64_t n, const double *M, double *q);
  * A non-finite sample cannot raise per filter inside a batch: that filter's X and P become NaN
  * (the reference raises LinAlgError from np.linalg.svd at that record).
  * traj (optional, NULL to skip): X after every step, [n_steps][batch][4].
- * flags: 0 or PEKF_RUN_MIXED_PRECISION. */
+ * counts (optional, NULL = all n_steps): filter b applies only its first min(counts[b], n_steps)
+ *   records of this launch (ragged logs / front-end output sharing one launch); its traj rows after
+ *   that repeat its final X.
+ * flags: PEKF_RUN_MIXED_PRECISION and/or PEKF_RUN_STATE_SOA (X[4][batch], P[10][batch]). */
 int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
                  const void *plane_gd, const void *plane_am, const void *plane_my,
                  const double *refs, double *X, double *P, double q, double r, double *traj,
-                 uint32_t flags, void *stream);
+                 const int32_t *counts, uint32_t flags, void *stream);
+/* AoS state (X[batch][4], P[batch][4][4]) <-> SoA state (X[4][batch], P[10][batch] holding
+ * P00 P01 P02 P03 P11 P12 P13 P22 P23 P33).  to_soa != 0: AoS -> SoA, else SoA -> AoS. */
+int pekf_state_layout_dev(int64_t batch, double *X_aos, double *P_aos, double *X_soa, double *P_soa,
+                          int to_soa, void *stream);
 
 /* ---------------- side outputs: what main_file.py plots beside X ----------------
  * Pure-gyro attitude: the RK4 chain of the gyro records alone, same dt as the filter (KFS/KalmanFilter.cpp:149,

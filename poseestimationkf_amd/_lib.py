@@ -21,6 +21,7 @@ PEKF_ERR_NODEVICE = 4
 PEKF_ERR_SVD = 5
 MISSING_MAG_BIT = 0x80000000
 RUN_MIXED_PRECISION = 0x1
+RUN_STATE_SOA = 0x2
 
 
 class PekfError(RuntimeError):
@@ -73,8 +74,9 @@ SIGNATURES = {
     "pekf_wahba_rotation": [_i64] + [_dp] * 7,
     "pekf_wahba_quaternion": [_i64] + [_dp] * 7,
     "pekf_rotmat_to_quat": [_i64, _dp, _dp],
-    "pekf_run_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _vp, _u32, _vp],
+    "pekf_run_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp, _u32, _vp],
     "pekf_reset_state_dev": [_i64, _vp, _vp, _vp],
+    "pekf_state_layout_dev": [_i64, _vp, _vp, _vp, _vp, _int, _vp],
     "pekf_gyro_chain_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "pekf_wahba_stream_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp],
     "pekf_quat_to_rpy": [_i64, _dp, _dp],

@@ -33,20 +33,66 @@ __device__ __forceinline__ Rec load_rec(const float4 *__restrict__ gd, const flo
     return r;
 }
 
+// Filter state in HBM.  AoS (default, the ABI's natural layout): X[b][4], P[b][4][4].  SoA
+// (PEKF_RUN_STATE_SOA): X[4][batch] and the 10 unique entries of P as P[10][batch]
+// (00 01 02 03 11 12 13 22 23 33): every state load / store of a wave is one contiguous
+// 512 B access, which matters when a launch covers few records (online serving).
+template <bool SOA, typename PT>
+__device__ __forceinline__ void load_state(const double *X, const double *P, int64_t b, int64_t batch,
+                                           double *x, Sym4T<PT> &S) {
+    if (SOA) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = X[k * batch + b];
+        S = {(PT)P[0 * batch + b], (PT)P[1 * batch + b], (PT)P[2 * batch + b], (PT)P[3 * batch + b],
+             (PT)P[4 * batch + b], (PT)P[5 * batch + b], (PT)P[6 * batch + b], (PT)P[7 * batch + b],
+             (PT)P[8 * batch + b], (PT)P[9 * batch + b]};
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = X[4 * b + k];
+        const double *pp = P + 16 * b;
+        S = {(PT)pp[0], (PT)pp[1], (PT)pp[2], (PT)pp[3], (PT)pp[5],
+             (PT)pp[6], (PT)pp[7], (PT)pp[10], (PT)pp[11], (PT)pp[15]};
+    }
+}
+
+template <bool SOA, typename PT>
+__device__ __forceinline__ void store_state(double *X, double *P, int64_t b, int64_t batch, const double *x,
+                                            const Sym4T<PT> &S) {
+    if (SOA) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) X[k * batch + b] = x[k];
+        const double v[10] = {S.a00, S.a01, S.a02, S.a03, S.a11, S.a12, S.a13, S.a22, S.a23, S.a33};
+#pragma unroll
+        for (int k = 0; k < 10; ++k) P[k * batch + b] = v[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) X[4 * b + k] = x[k];
+        double *po = P + 16 * b;
+        po[0] = S.a00; po[1] = S.a01; po[2] = S.a02; po[3] = S.a03;
+        po[4] = S.a01; po[5] = S.a11; po[6] = S.a12; po[7] = S.a13;
+        po[8] = S.a02; po[9] = S.a12; po[10] = S.a22; po[11] = S.a23;
+        po[12] = S.a03; po[13] = S.a13; po[14] = S.a23; po[15] = S.a33;
+    }
+}
+
 // MIXED = false: every operation in FP64 (the headline path).
 // MIXED = true (opt-in, PEKF_RUN_MIXED_PRECISION): the covariance recursion (P-, S^-1, K, P)
 // in FP32 while RK4, Wahba, R->q and the X update stay FP64 (~2e-8 vs FP64).
-template <bool TRAJ, bool MIXED>
+// COUNTS: filter b applies only its first counts[b] records of the launch (a separate
+// instantiation so the uniform-length path carries no per-step lane predicate).
+template <bool TRAJ, bool MIXED, bool SOA, bool COUNTS>
 __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_steps, int64_t window,
                                                    int64_t step0, const float4 *__restrict__ gd,
                                                    const float4 *__restrict__ am,
                                                    const float2 *__restrict__ my,
                                                    const double *__restrict__ refs,
                                                    double *__restrict__ Xio, double *__restrict__ Pio,
-                                                   double qs, double rs, double *__restrict__ traj) {
+                                                   double qs, double rs, double *__restrict__ traj,
+                                                   const int32_t *__restrict__ counts) {
     using PT = typename std::conditional<MIXED, float, double>::type;
     const int64_t b = (int64_t)blockIdx.x * kRunBlock + threadIdx.x;
     if (b >= batch) return;
+    const int64_t my_steps = COUNTS ? (counts[b] < n_steps ? (int64_t)counts[b] : n_steps) : n_steps;
 
     // per-filter constants: the Wahba reference frame of (acc0, mag0) (Wahba.py:4-6)
     Frame Wf;
@@ -57,10 +103,9 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     }
     const PT g = (PT)(0.25 * qs);     // Jb Q Jb^T = (q/4)(|X|^2 I - X X^T)
     const PT rp = (PT)rs, r2 = (PT)(rs * rs);
-    double x[4] = {Xio[4 * b + 0], Xio[4 * b + 1], Xio[4 * b + 2], Xio[4 * b + 3]};
-    const double *pp = Pio + 16 * b;
-    Sym4T<PT> P = {(PT)pp[0], (PT)pp[1], (PT)pp[2], (PT)pp[3], (PT)pp[5],
-                   (PT)pp[6], (PT)pp[7], (PT)pp[10], (PT)pp[11], (PT)pp[15]};
+    double x[4];
+    Sym4T<PT> P;
+    load_state<SOA>(Xio, Pio, b, batch, x, P);
 
     int64_t row = step0 % window;
     Rec cur = load_rec(gd, am, my, row * batch + b);
@@ -69,6 +114,7 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
         int64_t nrow = row + 1 == window ? 0 : row + 1;
         Rec nxt;
         if (t + 1 < n_steps) nxt = load_rec(gd, am, my, nrow * batch + b);
+        if (!COUNTS || t < my_steps) {
 
         const double hw[3] = {0.5 * (double)cur.gd.x, 0.5 * (double)cur.gd.y, 0.5 * (double)cur.gd.z};
         const uint32_t word = __float_as_uint(cur.gd.w);
@@ -118,6 +164,7 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
             P = {rp - r2 * Si.a00, -r2 * Si.a01, -r2 * Si.a02, -r2 * Si.a03, rp - r2 * Si.a11,
                  -r2 * Si.a12, -r2 * Si.a13, rp - r2 * Si.a22, -r2 * Si.a23, rp - r2 * Si.a33};
         }
+        }  // t < my_steps
         if (TRAJ) {
             double2 *o = reinterpret_cast<double2 *>(traj + (t * batch + b) * 4);
             o[0] = make_double2(x[0], x[1]);
@@ -126,12 +173,23 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
         cur = nxt;
         row = nrow;
     }
-    Xio[4 * b + 0] = x[0]; Xio[4 * b + 1] = x[1]; Xio[4 * b + 2] = x[2]; Xio[4 * b + 3] = x[3];
-    double *po = Pio + 16 * b;
-    po[0] = P.a00; po[1] = P.a01; po[2] = P.a02; po[3] = P.a03;
-    po[4] = P.a01; po[5] = P.a11; po[6] = P.a12; po[7] = P.a13;
-    po[8] = P.a02; po[9] = P.a12; po[10] = P.a22; po[11] = P.a23;
-    po[12] = P.a03; po[13] = P.a13; po[14] = P.a23; po[15] = P.a33;
+    store_state<SOA>(Xio, Pio, b, batch, x, P);
+}
+
+// AoS <-> SoA state conversion (see load_state); P's 10 unique entries are the upper triangle.
+__global__ __launch_bounds__(kRunBlock) void k_state_layout(int64_t batch, const double *Xa, const double *Pa,
+                                                            double *Xs, double *Ps, int to_soa) {
+    const int64_t b = (int64_t)blockIdx.x * kRunBlock + threadIdx.x;
+    if (b >= batch) return;
+    double x[4];
+    Sym4T<double> S;
+    if (to_soa) {
+        load_state<false>(Xa, Pa, b, batch, x, S);
+        store_state<true>(Xs, Ps, b, batch, x, S);
+    } else {
+        load_state<true>(Xs, Ps, b, batch, x, S);
+        store_state<false>(const_cast<double *>(Xa), const_cast<double *>(Pa), b, batch, x, S);
+    }
 }
 
 __global__ __launch_bounds__(kRunBlock) void k_reset(int64_t batch, double *X, double *P) {
@@ -151,8 +209,9 @@ extern "C" {
 int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
                  const void *plane_gd, const void *plane_am, const void *plane_my,
                  const double *refs, double *X, double *P, double q, double r, double *traj,
-                 uint32_t flags, void *stream) {
+                 const int32_t *counts, uint32_t flags, void *stream) {
     PEKF_CHECK_ARG(batch >= 0 && n_steps >= 0, "negative size");
+    PEKF_CHECK_ARG((flags & ~(uint32_t)(PEKF_RUN_MIXED_PRECISION | PEKF_RUN_STATE_SOA)) == 0, "unknown flags");
     if (batch == 0 || n_steps == 0) return PEKF_OK;
     PEKF_CHECK_ARG(window > 0 && step0 >= 0, "window must be > 0 and step0 >= 0");
     PEKF_CHECK_ARG(plane_gd && plane_am && plane_my && refs && X && P, "null pointer");
@@ -164,16 +223,21 @@ int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
     const auto *gd = static_cast<const float4 *>(plane_gd);
     const auto *am = static_cast<const float4 *>(plane_am);
     const auto *my = static_cast<const float2 *>(plane_my);
-    PEKF_CHECK_ARG((flags & ~(uint32_t)PEKF_RUN_MIXED_PRECISION) == 0, "unknown flags");
-    const bool mixed = flags & PEKF_RUN_MIXED_PRECISION;
-#define PEKF_LAUNCH_RUN(TR, MX)                                                                     \
-    hipLaunchKernelGGL((k_run<TR, MX>), grid, block, 0, as_stream(stream), batch, n_steps, window, \
-                       step0, gd, am, my, refs, X, P, q, r, traj)
+    const bool mixed = flags & PEKF_RUN_MIXED_PRECISION, soa = flags & PEKF_RUN_STATE_SOA;
+#define PEKF_LAUNCH_RUN(TR, MX, SO, CN)                                                                     \
+    hipLaunchKernelGGL((k_run<TR, MX, SO, CN>), grid, block, 0, as_stream(stream), batch, n_steps, window, \
+                       step0, gd, am, my, refs, X, P, q, r, traj, counts)
+#define PEKF_LAUNCH_RUN1(TR, MX, SO) \
+    do { if (counts) PEKF_LAUNCH_RUN(TR, MX, SO, true); else PEKF_LAUNCH_RUN(TR, MX, SO, false); } while (0)
+#define PEKF_LAUNCH_RUN2(TR, MX) \
+    do { if (soa) PEKF_LAUNCH_RUN1(TR, MX, true); else PEKF_LAUNCH_RUN1(TR, MX, false); } while (0)
     if (traj) {
-        if (mixed) PEKF_LAUNCH_RUN(true, true); else PEKF_LAUNCH_RUN(true, false);
+        if (mixed) PEKF_LAUNCH_RUN2(true, true); else PEKF_LAUNCH_RUN2(true, false);
     } else {
-        if (mixed) PEKF_LAUNCH_RUN(false, true); else PEKF_LAUNCH_RUN(false, false);
+        if (mixed) PEKF_LAUNCH_RUN2(false, true); else PEKF_LAUNCH_RUN2(false, false);
     }
+#undef PEKF_LAUNCH_RUN2
+#undef PEKF_LAUNCH_RUN1
 #undef PEKF_LAUNCH_RUN
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_run");
@@ -188,6 +252,18 @@ int pekf_reset_state_dev(int64_t batch, double *X, double *P, void *stream) {
                        as_stream(stream), batch, X, P);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_reset");
+    return PEKF_OK;
+}
+
+int pekf_state_layout_dev(int64_t batch, double *X_aos, double *P_aos, double *X_soa, double *P_soa,
+                          int to_soa, void *stream) {
+    PEKF_CHECK_ARG(batch >= 0, "negative size");
+    if (batch == 0) return PEKF_OK;
+    PEKF_CHECK_ARG(X_aos && P_aos && X_soa && P_soa, "null pointer");
+    hipLaunchKernelGGL(k_state_layout, dim3(grid_for(batch, kRunBlock)), dim3(kRunBlock), 0,
+                       as_stream(stream), batch, X_aos, P_aos, X_soa, P_soa, to_soa);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "k_state_layout");
     return PEKF_OK;
 }
 

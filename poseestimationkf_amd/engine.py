@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 from . import synth
-from ._lib import RUN_MIXED_PRECISION, check, dptr, f64, lib
+from ._lib import RUN_MIXED_PRECISION, RUN_STATE_SOA, check, dptr, f64, lib
 
 
 # ------------------------------------------------------------------ device plumbing
@@ -137,6 +137,7 @@ class IMUWindow:
         self.am = DeviceBuffer(16 * n)
         self.my = DeviceBuffer(8 * n)
         self.refs = DeviceBuffer(48 * self.batch)
+        self.counts = None  # per-filter valid record counts when filters are ragged (logs, front-end)
 
     @property
     def nbytes(self):
@@ -167,14 +168,27 @@ class IMUWindow:
     def from_logs(cls, paths, n_records=None):
         """One filter per server log, parsed natively (pekf_log_read).
 
-        All filters of a window advance in lock-step, so the window holds the first
-        n_records records of every log (default: the shortest log's length)."""
+        Logs may differ in length: the window holds the longest log's records (n_records caps
+        it), shorter logs are zero-padded and win.counts[b] is filter b's own record count,
+        which BatchedEKF.run applies so each filter consumes exactly its own records."""
         recs = [read_log_records(p) for p in paths]
-        n = min(r.dtw.shape[0] for r in recs) if n_records is None else int(n_records)
-        cat = lambda name: np.concatenate([getattr(r, name)[:n] for r in recs], axis=1)  # noqa: E731
+        lens = np.array([r.dtw.shape[0] for r in recs], dtype=np.int64)
+        n = int(lens.max()) if n_records is None else int(n_records)
+
+        def cat(name):
+            out = []
+            for r in recs:
+                a = getattr(r, name)
+                m = min(n, a.shape[0])
+                pad = np.zeros((n,) + a.shape[1:], a.dtype)
+                pad[:m] = a[:m]
+                out.append(pad)
+            return np.concatenate(out, axis=1)
         rec = synth.Records(cat("gyro"), cat("acc"), cat("mag"), cat("dtw"),
                             np.concatenate([r.acc0 for r in recs]), np.concatenate([r.mag0 for r in recs]))
-        return cls.from_records(rec)
+        win = cls.from_records(rec)
+        win.counts = np.minimum(lens, n).astype(np.int32)
+        return win
 
     def synthesize(self, seed=synth.DEFAULT_SEED, first_filter=0, missing=False,
                    params=synth.SynthParams(), stream=None):
@@ -243,7 +257,8 @@ def run_frontend(ev, alpha=0.1, r_max=None):
         raise ValueError("a record's dt does not fit the 31-bit ns field of the stream")
     if err & 2:
         raise ValueError("more than r_max=%d records for some filter" % r_max)
-    return win, cnt.download((K,), np.int32)
+    win.counts = cnt.download((K,), np.int32)
+    return win, win.counts
 
 
 # ------------------------------------------------------------------ the batched filter
@@ -256,41 +271,78 @@ class BatchedEKF:
     Prediction + Correction for every record.  `run` advances all filters n_steps records.
     """
 
-    def __init__(self, batch, q=1.0, r=0.1, precision="f64"):
-        """precision: "f64" (default, as the reference) or "mixed" (covariance path in f32)."""
+    def __init__(self, batch, q=1.0, r=0.1, precision="f64", layout="aos"):
+        """precision: "f64" (default, as the reference) or "mixed" (covariance path in f32).
+        layout: "aos" (X[B][4], P[B][4][4]) or "soa" (X[4][B], P[10][B]: coalesced state access,
+        for launches that cover few records, e.g. online serving)."""
         if precision not in ("f64", "mixed"):
             raise ValueError("precision must be 'f64' or 'mixed'")
+        if layout not in ("aos", "soa"):
+            raise ValueError("layout must be 'aos' or 'soa'")
         self.batch = int(batch)
         self.q, self.r = float(q), float(r)
-        self.flags = RUN_MIXED_PRECISION if precision == "mixed" else 0
+        self.layout = layout
+        self.flags = (RUN_MIXED_PRECISION if precision == "mixed" else 0) | (RUN_STATE_SOA if layout == "soa" else 0)
         self.X = DeviceBuffer(32 * self.batch)
-        self.P = DeviceBuffer(128 * self.batch)
+        self.P = DeviceBuffer((80 if layout == "soa" else 128) * self.batch)
         self.reset()
 
+    def _to_layout(self, Xa, Pa, to_soa, stream=None):
+        check(lib.pekf_state_layout_dev(self.batch, Xa.ptr, Pa.ptr, self.X.ptr, self.P.ptr, int(to_soa), stream))
+
     def reset(self, stream=None):
-        check(lib.pekf_reset_state_dev(self.batch, self.X.ptr, self.P.ptr, stream))
+        if self.layout == "soa":
+            Xa, Pa = DeviceBuffer(32 * self.batch), DeviceBuffer(128 * self.batch)
+            check(lib.pekf_reset_state_dev(self.batch, Xa.ptr, Pa.ptr, stream))
+            self._to_layout(Xa, Pa, True, stream)
+        else:
+            check(lib.pekf_reset_state_dev(self.batch, self.X.ptr, self.P.ptr, stream))
         check(lib.pekf_device_sync() if stream is None else lib.pekf_stream_sync(stream))
 
     def set_state(self, X, P):
-        self.X.upload(f64(X, (self.batch, 4)))
-        self.P.upload(f64(P, (self.batch, 4, 4)))
+        """X (B, 4), P (B, 4, 4) in the reference's row-major layout, whatever self.layout is."""
+        X, P = f64(X, (self.batch, 4)), f64(P, (self.batch, 4, 4))
+        if self.layout == "soa":
+            Xa, Pa = DeviceBuffer(X.nbytes).upload(X), DeviceBuffer(P.nbytes).upload(P)
+            self._to_layout(Xa, Pa, True)
+            check(lib.pekf_device_sync())
+        else:
+            self.X.upload(X)
+            self.P.upload(P)
 
     def get_state(self):
+        """(X (B, 4), P (B, 4, 4)) in the reference's row-major layout."""
+        if self.layout == "soa":
+            Xa, Pa = DeviceBuffer(32 * self.batch), DeviceBuffer(128 * self.batch)
+            self._to_layout(Xa, Pa, False)
+            check(lib.pekf_device_sync())
+            return Xa.download((self.batch, 4), np.float64), Pa.download((self.batch, 4, 4), np.float64)
         return (self.X.download((self.batch, 4), np.float64),
                 self.P.download((self.batch, 4, 4), np.float64))
 
-    def run_async(self, win: IMUWindow, n_steps, step0=0, stream=None, traj=None):
-        """Enqueue one fused launch; traj: optional DeviceBuffer of n_steps*batch*32 bytes."""
+    def run_async(self, win: IMUWindow, n_steps, step0=0, stream=None, traj=None, counts=None):
+        """Enqueue one fused launch; traj: optional DeviceBuffer of n_steps*batch*32 bytes;
+        counts: optional DeviceBuffer of batch int32 (filter b applies its first counts[b] records)."""
         assert win.batch == self.batch
         check(lib.pekf_run_dev(self.batch, int(n_steps), win.window, int(step0), win.gd.ptr,
                                win.am.ptr, win.my.ptr, win.refs.ptr, self.X.ptr, self.P.ptr,
-                               self.q, self.r, traj.ptr if traj is not None else None, self.flags,
-                               stream))
+                               self.q, self.r, traj.ptr if traj is not None else None,
+                               counts.ptr if counts is not None else None, self.flags, stream))
 
-    def run(self, win: IMUWindow, n_steps=None, step0=0, want_traj=False):
+    def run(self, win: IMUWindow, n_steps=None, step0=0, want_traj=False, counts=None):
+        """Advance every filter n_steps records (default: the whole window) from row step0.
+
+        counts: per-filter record counts for this launch (array of batch ints or a DeviceBuffer);
+        default win.counts (ragged logs / front-end output) shifted by step0, so each filter
+        applies exactly its own records while sharing one launch."""
         n_steps = win.window if n_steps is None else int(n_steps)
         tb = DeviceBuffer(32 * n_steps * self.batch) if want_traj else None
-        self.run_async(win, n_steps, step0, None, tb)
+        if counts is None and win.counts is not None:
+            counts = np.clip(np.asarray(win.counts, np.int64) - int(step0), 0, n_steps)
+        if counts is not None and not isinstance(counts, DeviceBuffer):
+            c = np.ascontiguousarray(counts, dtype=np.int32).reshape(self.batch)
+            counts = DeviceBuffer(c.nbytes).upload(c)
+        self.run_async(win, n_steps, step0, None, tb, counts)
         check(lib.pekf_device_sync())
         if want_traj:
             return tb.download((n_steps, self.batch, 4), np.float64)

@@ -6,6 +6,7 @@
   gyro_chain    pekf_gyro_chain_dev (§8f-3): 16 B read per filter-record
   wahba_stream  pekf_wahba_stream_dev (§8f-3): 24 B read + 32 B written per filter-record
   predict_dev / correct_dev   per-call operators at n = 1M items (device pointers)
+  online_step_aos / _soa   1M filters x 1 record per launch (state through HBM every launch)
   dropin_call   host-pointer per-call latency at n = 1 (the path main_file.py takes)
 
 Kernel times are HIP events on the launch stream; run under rocprofv3 --kernel-trace --stats
@@ -95,6 +96,27 @@ def main():
                            "gbs": B * Nw * 56 / (ms * 1e-3) / 1e9, "hbm_frac": B * Nw * 56 / (ms * 1e-3) / 1e9 / HBM}
     log("wahba stream: %.1f ms" % ms)
     del win, out
+
+    # ---- online serving: every launch advances 1M filters by ONE new record; the state X, P is
+    # read and written through HBM each launch.  AoS: 40 B record + 32+128 B read (P's cache
+    # lines come whole) + 32+128 B written; SoA (X[4][B], P[10][B]): 40 + 32+80 + 32+80 B.
+    B1 = 1 << 20
+    win1 = engine.IMUWindow(B1, 8).synthesize(stream=s)
+    for layout, per in (("aos", 40 + 32 + 128 + 32 + 128), ("soa", 40 + 32 + 80 + 32 + 80)):
+        f1 = engine.BatchedEKF(B1, layout=layout)
+        k = [0]
+
+        def one_step():
+            f1.run_async(win1, 1, k[0] % 8, s)
+            k[0] += 1
+        ms = timed(one_step, s, reps=20)
+        res["online_step_" + layout] = {
+            "filters": B1, "records_per_launch": 1, "kernel_ms": ms, "steps_per_s": B1 / (ms * 1e-3),
+            "bytes_per_filter_step": per, "gbs": B1 * per / (ms * 1e-3) / 1e9,
+            "hbm_frac": B1 * per / (ms * 1e-3) / 1e9 / HBM}
+        log("online step %s (1M filters x 1 record): %.3f ms" % (layout, ms))
+        del f1
+    del win1
 
     # ---- per-call operators at n = 1M (device pointers)
     n = 1 << 20

@@ -61,9 +61,13 @@ def test_no_cpu_fallback_without_device():
 
 def test_invalid_arguments_are_reported_not_crashed():
     from poseestimationkf_amd import _lib
-    st = _lib.lib.pekf_run_dev(-1, 1, 1, 0, None, None, None, None, None, None, 1.0, 0.1, None, 0, None)
+    st = _lib.lib.pekf_run_dev(-1, 1, 1, 0, None, None, None, None, None, None, 1.0, 0.1, None, None, 0, None)
     assert st == _lib.PEKF_ERR_INVALID and "negative" in _lib.last_error()
-    st = _lib.lib.pekf_run_dev(4, 1, 1, 0, None, None, None, None, None, None, 1.0, 0.1, None, 0, None)
+    st = _lib.lib.pekf_run_dev(4, 1, 1, 0, None, None, None, None, None, None, 1.0, 0.1, None, None, 0, None)
+    assert st == _lib.PEKF_ERR_INVALID and "null" in _lib.last_error()
+    st = _lib.lib.pekf_run_dev(4, 1, 1, 0, None, None, None, None, None, None, 1.0, 0.1, None, None, 0x4, None)
+    assert st == _lib.PEKF_ERR_INVALID and "flags" in _lib.last_error()
+    st = _lib.lib.pekf_state_layout_dev(4, None, None, None, None, 1, None)
     assert st == _lib.PEKF_ERR_INVALID and "null" in _lib.last_error()
 
 

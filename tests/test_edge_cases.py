@@ -140,4 +140,4 @@ def test_fused_empty_launches_are_noops(eng):
     f.run(win, n_steps=0)
     X1, P1 = f.get_state()
     assert np.array_equal(X0, X1) and np.array_equal(P0, P1)
-    assert lib.pekf_run_dev(0, 10, 4, 0, None, None, None, None, None, None, 1.0, 0.1, None, 0, None) == 0
+    assert lib.pekf_run_dev(0, 10, 4, 0, None, None, None, None, None, None, 1.0, 0.1, None, None, 0, None) == 0

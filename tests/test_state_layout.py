@@ -1,0 +1,140 @@
+"""SoA state layout (PEKF_RUN_STATE_SOA) and per-filter record counts of pekf_run_dev.
+
+Both are launch-shape options, not numerics: every result here must be BIT-IDENTICAL to the
+default AoS, uniform-length launch on the same records (which test_gpu_parity.py pins to the
+oracle).  Ragged logs end-to-end are checked against the reference's own C1 trajectory.
+"""
+from __future__ import annotations
+
+import gzip
+import os
+
+import numpy as np
+import pytest
+
+from poseestimationkf_amd import synth
+
+from .conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from poseestimationkf_amd import engine
+    from poseestimationkf_amd._lib import device_count
+    assert device_count() > 0, "GPU tests need a HIP device"
+    return engine
+
+
+def _same(a, b):
+    return np.array_equal(np.asarray(a).view(np.uint64), np.asarray(b).view(np.uint64))
+
+
+@pytest.mark.parametrize("precision", ["f64", "mixed"])
+def test_soa_layout_bit_identical_to_aos(eng, precision):
+    K, W = 300, 48
+    rec = synth.generate(np.arange(K), W, seed=21, missing=True)
+    win = eng.IMUWindow.from_records(rec)
+    a = eng.BatchedEKF(K, precision=precision)
+    s = eng.BatchedEKF(K, precision=precision, layout="soa")
+    assert s.P.nbytes == 80 * K
+    ta = a.run(win, n_steps=30, want_traj=True)
+    ts = s.run(win, n_steps=30, want_traj=True)
+    assert _same(ta, ts)
+    # resume from the stored state in both layouts
+    a.run(win, n_steps=18, step0=30)
+    s.run(win, n_steps=18, step0=30)
+    (Xa, Pa), (Xs, Ps) = a.get_state(), s.get_state()
+    assert _same(Xa, Xs) and _same(Pa, Ps)
+
+
+def test_soa_online_single_record_launches(eng):
+    """Online serving: one launch per new record equals one launch over all records."""
+    K, W, N = 513, 8, 21
+    rec = synth.generate(np.arange(K), W, seed=4)
+    win = eng.IMUWindow.from_records(rec)
+    ref = eng.BatchedEKF(K)
+    ref.run(win, n_steps=N)
+    s = eng.BatchedEKF(K, layout="soa")
+    for t in range(N):
+        s.run_async(win, 1, t)
+    Xr, Pr = ref.get_state()
+    Xs, Ps = s.get_state()
+    assert _same(Xr, Xs) and _same(Pr, Ps)
+
+
+def test_state_layout_roundtrip(eng):
+    K = 70
+    rng = np.random.default_rng(3)
+    X = rng.normal(size=(K, 4))
+    A = rng.normal(size=(K, 4, 4))
+    P = A @ A.transpose(0, 2, 1)  # symmetric: SoA keeps the upper triangle only
+    s = eng.BatchedEKF(K, layout="soa")
+    s.set_state(X, P)
+    Xs, Ps = s.get_state()
+    assert _same(Xs, X) and _same(Ps, P)
+    raw = s.P.download((10, K), np.float64)
+    iu = np.triu_indices(4)
+    assert _same(raw.T, P[:, iu[0], iu[1]])
+
+
+@pytest.mark.parametrize("layout", ["aos", "soa"])
+def test_per_filter_counts_equal_truncated_launches(eng, layout):
+    K, W, N = 260, 40, 40
+    rec = synth.generate(np.arange(K), W, seed=8, missing=True)
+    win = eng.IMUWindow.from_records(rec)
+    choices = np.array([0, 1, 7, 33, N, N + 5])
+    counts = choices[np.arange(K) % len(choices)].astype(np.int32)
+    f = eng.BatchedEKF(K, layout=layout)
+    tr = f.run(win, n_steps=N, want_traj=True, counts=counts)
+    X, P = f.get_state()
+    for c in np.unique(np.minimum(counts, N)):
+        sel = np.minimum(counts, N) == c
+        g = eng.BatchedEKF(K)
+        tg = g.run(win, n_steps=int(c), want_traj=True) if c else None
+        Xg, Pg = g.get_state()
+        assert _same(X[sel], Xg[sel]) and _same(P[sel], Pg[sel]), c
+        if c:
+            assert _same(tr[:c, sel], tg[:, sel])
+        assert _same(tr[c:, sel], np.broadcast_to(Xg[sel], (N - c,) + Xg[sel].shape))
+
+
+def test_ragged_logs_share_one_launch(eng, tmp_path):
+    """Two server logs of different lengths in one window: each filter consumes its own records."""
+    with gzip.open(os.path.join(GOLDEN, "c1_log.txt.gz"), "rt") as fh:
+        lines = fh.read().splitlines(keepends=True)
+    full, short = tmp_path / "full.txt", tmp_path / "short.txt"
+    full.write_text("".join(lines))
+    short.write_text("".join(lines[: len(lines) * 3 // 5]))
+    win = eng.IMUWindow.from_logs([str(full), str(short)])
+    n_full = eng.read_log_records(str(full)).dtw.shape[0]
+    n_short = eng.read_log_records(str(short)).dtw.shape[0]
+    assert n_short < n_full and list(win.counts) == [n_full, n_short] and win.window == n_full
+    tr = eng.BatchedEKF(2).run(win, want_traj=True)
+    alone = eng.BatchedEKF(1).run(eng.IMUWindow.from_logs([str(short)]), want_traj=True)
+    assert _same(tr[:n_short, 1], alone[:, 0])
+    want = np.load(os.path.join(GOLDEN, "c1_xk.npy"))[1:]
+    assert float(np.abs(tr[:, 0] - want).max()) < 1e-5
+
+
+def test_frontend_ragged_output_full_length(eng, oracle_c):
+    """Front-end output (ragged per filter) through one counted launch, every filter to its own end."""
+    from oracle import frontend_numpy as fe
+    K, E = 128, 900
+    ev = synth.generate_events(np.arange(K), E, seed=12)
+    win, counts = eng.run_frontend(ev)
+    assert counts.min() < counts.max()
+    f = eng.BatchedEKF(K)
+    f.run(win)  # win.counts applied
+    X, _ = f.get_state()
+    refs = win.refs.download((K, 6), np.float64)
+    for k in range(0, K, 9):
+        g, dt, a, m = fe.run_frontend(ev["types"][:, k], ev["values"][:, k].astype(np.float64), ev["times"][:, k],
+                                      ev["init_acc"][k], ev["init_mag"][k], ev["t_init"][k])
+        assert len(dt) == counts[k]
+        rec = synth.Records(g[:, None].astype(np.float32), a[:, None].astype(np.float32),
+                            m[:, None].astype(np.float32), dt[:, None].astype(np.uint32),
+                            refs[k:k + 1, :3], refs[k:k + 1, 3:])
+        Xo, _, _ = oracle_c.run(rec)
+        assert float(np.abs(X[k] - Xo[0]).max()) < 1e-9, k
