@@ -260,8 +260,9 @@ def main():
 # FP64 work per filter-step of the fused kernel, counted from its gfx950 ISA hot loop by
 # scripts/isa_count.py (DESIGN.md "FP64 budget"): FP64 VALU instructions, and the FLOP of
 # the arithmetic ones with an FMA counted as 2.
-ISA_COUNTS = {"f64": {"flop": 567, "fp64_instr": 383},
-              "mixed": {"flop": 282, "fp64_instr": 228}}  # mixed: + ~170 f32 instructions
+# per filter-step, from scripts/isa_count.py on the hot loop of k_run (make -C .../csrc asm)
+ISA_COUNTS = {"f64": {"flop": 567, "fp64_instr": 386, "valu_instr": 432},
+              "mixed": {"flop": 278, "fp64_instr": 227, "valu_instr": 447}}  # mixed: + ~220 f32 instructions
 FLOP_PER_STEP = ISA_COUNTS["f64"]["flop"]
 FP64_INSTR_PER_STEP = ISA_COUNTS["f64"]["fp64_instr"]
 

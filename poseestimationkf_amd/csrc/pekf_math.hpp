@@ -212,15 +212,15 @@ PEKF_DEV void make_frame(const double *a, const double *m, Frame &F) {
 // W = frame of the reference pair (acc0, mag0), V = frame of the current pair (acc, mag).
 template <bool FAST = false>
 PEKF_DEV void wahba_rotation(const Frame &W, const Frame &V, double ka, double km, double *R) {
-    const double c00 = ka * W.alpha * V.alpha + km * W.beta1 * V.beta1;
-    const double c01 = km * W.beta1 * V.beta2;
-    const double c10 = km * W.beta2 * V.beta1;
-    const double c11 = km * W.beta2 * V.beta2;
+    // C = [[c00, c01], [c10, c11]]: c00 = ka aW aV + km b1W b1V, c01 = km b1W b2V,
+    // c10 = km b2W b1V, c11 = km b2W b2V.
     // det C = ka km alpha_W alpha_V beta2_W beta2_V exactly; alpha, beta2 >= 0
     const bool proper = ka * km >= 0.0;
-    double p, s;
-    if (proper) { p = c00 + c11; s = c10 - c01; }
-    else        { p = c00 - c11; s = c01 + c10; }
+    // polar factor of C from (p, s) = (c00 + c11, c10 - c01) (rotation) or (c00 - c11, c01 + c10)
+    // (reflection); the sign goes into km' so each is one expression (contracted alike everywhere)
+    const double kw = km * W.beta2, kn = proper ? kw : -kw, kb = km * W.beta1;
+    double p = ka * W.alpha * V.alpha + kb * V.beta1 + kn * V.beta2;
+    double s = kw * V.beta1 - (proper ? kb : -kb) * V.beta2;
     const double ih = rsqrt<FAST>(p * p + s * s);
     p *= ih;
     s *= ih;
@@ -331,16 +331,16 @@ PEKF_DEV Sym4T<T> propagate_cov(const Sym4T<T> &P, const T *h, const T *x, T g) 
     const T n2 = x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
     const T gx0 = g * x[0], gx1 = g * x[1], gx2 = g * x[2], gx3 = g * x[3];
     Sym4T<T> o;
-    o.a00 = m(0, 0) + g * (n2 - x[0] * x[0]);
+    o.a00 = fma(g, n2 - x[0] * x[0], m(0, 0));
     o.a01 = m(0, 1) - gx0 * x[1];
     o.a02 = m(0, 2) - gx0 * x[2];
     o.a03 = m(0, 3) - gx0 * x[3];
-    o.a11 = m(1, 1) + g * (n2 - x[1] * x[1]);
+    o.a11 = fma(g, n2 - x[1] * x[1], m(1, 1));
     o.a12 = m(1, 2) - gx1 * x[2];
     o.a13 = m(1, 3) - gx1 * x[3];
-    o.a22 = m(2, 2) + g * (n2 - x[2] * x[2]);
+    o.a22 = fma(g, n2 - x[2] * x[2], m(2, 2));
     o.a23 = m(2, 3) - gx2 * x[3];
-    o.a33 = m(3, 3) + g * (n2 - x[3] * x[3]);
+    o.a33 = fma(g, n2 - x[3] * x[3], m(3, 3));
     (void)gx3;
     return o;
 }

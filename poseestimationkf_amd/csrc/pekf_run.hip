@@ -24,15 +24,6 @@ struct Rec {
     float2 my;  // my, mz
 };
 
-__device__ __forceinline__ Rec load_rec(const float4 *__restrict__ gd, const float4 *__restrict__ am,
-                                        const float2 *__restrict__ my, int64_t idx) {
-    Rec r;
-    r.gd = gd[idx];
-    r.am = am[idx];
-    r.my = my[idx];
-    return r;
-}
-
 // Filter state in HBM.  AoS (default, the ABI's natural layout): X[b][4], P[b][4][4].  SoA
 // (PEKF_RUN_STATE_SOA): X[4][batch] and the 10 unique entries of P as P[10][batch]
 // (00 01 02 03 11 12 13 22 23 33): every state load / store of a wave is one contiguous
@@ -107,13 +98,20 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     Sym4T<PT> P;
     load_state<SOA>(Xio, Pio, b, batch, x, P);
 
-    int64_t row = step0 % window;
-    Rec cur = load_rec(gd, am, my, row * batch + b);
-    for (int64_t t = 0; t < n_steps; ++t) {
-        // prefetch the next record (wraps around the resident window)
-        int64_t nrow = row + 1 == window ? 0 : row + 1;
-        Rec nxt;
-        if (t + 1 < n_steps) nxt = load_rec(gd, am, my, nrow * batch + b);
+    // Record of stream row r: the row base (r * batch) is wave-uniform (scalar registers); the
+    // lane adds only its 32-bit filter index (batch < 2^28 is checked on the host).
+    const uint32_t lane = (uint32_t)b;
+    auto load_row = [&](int64_t r) -> Rec {
+        const int64_t base = r * batch;
+        Rec v;
+        v.gd = (gd + base)[lane];
+        v.am = (am + base)[lane];
+        v.my = (my + base)[lane];
+        return v;
+    };
+
+    // One record: Prediction + Correction (main_file.py:42-45) on (x, P) in registers.
+    auto step = [&](const Rec &cur, int64_t t) {
         if (!COUNTS || t < my_steps) {
 
         const double hw[3] = {0.5 * (double)cur.gd.x, 0.5 * (double)cur.gd.y, 0.5 * (double)cur.gd.z};
@@ -166,12 +164,27 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
         }
         }  // t < my_steps
         if (TRAJ) {
-            double2 *o = reinterpret_cast<double2 *>(traj + (t * batch + b) * 4);
+            double2 *o = reinterpret_cast<double2 *>(traj + t * batch * 4) + 2 * (int64_t)lane;
             o[0] = make_double2(x[0], x[1]);
             o[1] = make_double2(x[2], x[3]);
         }
-        cur = nxt;
-        row = nrow;
+    };
+
+    // Time loop, unrolled by two with ping-pong records: the next row's record is always in
+    // flight while the current one is processed, and no registers are copied between steps.
+    // The prefetch is unconditional (the row wraps inside the resident window, so it is always
+    // a valid address); n_steps >= 1 here.
+    int64_t row = step0 % window;
+    Rec ra = load_row(row), rb;
+    for (int64_t t = 0;;) {
+        row = row + 1 == window ? 0 : row + 1;
+        rb = load_row(row);
+        step(ra, t);
+        if (++t == n_steps) break;
+        row = row + 1 == window ? 0 : row + 1;
+        ra = load_row(row);
+        step(rb, t);
+        if (++t == n_steps) break;
     }
     store_state<SOA>(Xio, Pio, b, batch, x, P);
 }
@@ -214,6 +227,7 @@ int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
     PEKF_CHECK_ARG((flags & ~(uint32_t)(PEKF_RUN_MIXED_PRECISION | PEKF_RUN_STATE_SOA)) == 0, "unknown flags");
     if (batch == 0 || n_steps == 0) return PEKF_OK;
     PEKF_CHECK_ARG(window > 0 && step0 >= 0, "window must be > 0 and step0 >= 0");
+    PEKF_CHECK_ARG(batch < ((int64_t)1 << 28), "batch must be < 2^28 filters per launch");
     PEKF_CHECK_ARG(plane_gd && plane_am && plane_my && refs && X && P, "null pointer");
     PEKF_CHECK_ARG(((uintptr_t)plane_gd % 16 == 0) && ((uintptr_t)plane_am % 16 == 0) &&
                        ((uintptr_t)plane_my % 8 == 0) && ((uintptr_t)traj % 16 == 0),

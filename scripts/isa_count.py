@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Count instructions of one kernel in a hipcc -S listing, split into the hot loop and the rest.
 
-usage: scripts/isa_count.py <file.s> <kernel-substring>
-The hot loop is taken as the largest block between a label and a backward branch to it.
+usage: scripts/isa_count.py <file.s> <kernel-substring> [steps-per-iteration]
+The hot loop is taken as the largest block between a label and a backward branch to it;
+k_run's time loop is unrolled by two, so its counts are divided by 2 (the default).
 """
 import collections
 import re
@@ -26,6 +27,7 @@ def is_insn(l):
 
 def main():
     path, name = sys.argv[1], sys.argv[2]
+    spi = int(sys.argv[3]) if len(sys.argv) > 3 else 2
     body = kernel_lines(path, name)
     labels = {LABEL.match(l.strip()).group(1): i for i, l in enumerate(body) if LABEL.match(l.strip())}
     best = (0, 0)
@@ -41,9 +43,10 @@ def main():
     f64 = {k: v for k, v in c.items() if "_f64" in k}
     flops = sum(v * (2 if "fma" in k else 1) for k, v in f64.items()
                 if any(t in k for t in ("fma", "mul_f64", "add_f64", "rcp", "rsq", "sqrt")))
-    print("kernel instructions: %d, hot loop: %d" % (len(allc), len(loop)))
+    print("kernel instructions: %d, hot loop: %d (%d steps per iteration)" % (len(allc), len(loop), spi))
     print("loop FP64 VALU: %d  (%s)" % (sum(f64.values()), ", ".join("%s %d" % kv for kv in sorted(f64.items(), key=lambda x: -x[1]))))
-    print("loop FP64 FLOP (fma=2; add/mul/rcp/rsq=1): %d per wave-iteration = per filter-step" % flops)
+    print("per filter-step: FP64 VALU %.1f, FP64 FLOP (fma=2; add/mul/rcp/rsq=1) %.1f, all VALU %.1f"
+          % (sum(f64.values()) / spi, flops / spi, sum(v for k, v in c.items() if k.startswith("v_")) / spi))
     groups = collections.Counter()
     for k, v in c.items():
         g = ("v_f64" if "_f64" in k else "v_mfma" if "mfma" in k else "v_other" if k.startswith("v_")
