@@ -54,7 +54,7 @@ def _cpu_worker(args):
     return len(ids) * n_rec, time.perf_counter() - t0
 
 
-def cpu_baseline(seed, missing, filters_per_core=16, n_rec=1500):
+def cpu_baseline(seed, missing, filters_per_core=160, n_rec=1500):
     import multiprocessing as mp
     cores = len(os.sched_getaffinity(0))
     workers = max(1, min(16, cores))
