@@ -197,6 +197,37 @@ int pekf_frontend_dev(int64_t batch, int64_t n_events, const void *ev_planes, co
 /* X = [1,0,0,0], P = I for every filter (main_file.py:23,26). */
 int pekf_reset_state_dev(int64_t batch, double *X, double *P, void *stream);
 
+/* ---------------- filter handle: the batched core of SURVEY.md §8b ----------------
+ * One handle = `batch` KalmanFilter objects (ExtendedKalmanFilter.py:6-15): it owns, on the
+ * current device, each filter's Wahba reference (acc0, mag0), Q = q I, R = r I, previousT and
+ * the state X = [1,0,0,0], P = I (main_file.py:23,26), which stays device-resident between calls.
+ * flags: PEKF_RUN_MIXED_PRECISION and/or PEKF_RUN_STATE_SOA (device layout of the state).
+ * acc0 / mag0: host [batch*3]; t0_ns: host [batch] initial previousT (NULL = 0). */
+typedef struct pekf_filter pekf_filter;
+int pekf_filter_create(int64_t batch, const double *acc0, const double *mag0, double q, double r,
+                       const int64_t *t0_ns, uint32_t flags, pekf_filter **out);
+int pekf_filter_destroy(pekf_filter *f);
+/* Host copies of the state in the reference layout: X[batch*4], P[batch*16] (P may be NULL). */
+int pekf_filter_set_state(pekf_filter *f, const double *X, const double *P);
+int pekf_filter_get_state(pekf_filter *f, double *X, double *P);
+/* previousT of every filter (host [batch]); the stream path (pekf_filter_run) uses dt records and
+ * leaves it untouched, so set it before switching back to pekf_filter_update. */
+int pekf_filter_set_time(pekf_filter *f, const int64_t *t_ns);
+/* Device addresses of the state (layout per flags) and refs[batch*6], e.g. for a collective. */
+int pekf_filter_device_state(pekf_filter *f, double **X, double **P, double **refs);
+/* One record per filter, FP64: Prediction(gyro, t_ns) then Correction(mag, acc) (main_file.py:42-45),
+ * dt = t_ns - previousT.  gyro/acc/mag [batch*3], t_ns [batch], mag_missing [batch] (NULL = none
+ * missing; nonzero = Wahba-skip), X_out [batch*4] (NULL to skip).  Host pointers, synchronous. */
+int pekf_filter_update(pekf_filter *f, const double *gyro, const int64_t *t_ns, const double *acc,
+                       const double *mag, const uint8_t *mag_missing, double *X_out);
+/* Same with device pointers, enqueued on `stream`. */
+int pekf_filter_update_dev(pekf_filter *f, const double *gyro, const int64_t *t_ns, const double *acc,
+                           const double *mag, const uint8_t *mag_missing, double *X_out, void *stream);
+/* pekf_run_dev on the handle's state and references (stream planes, traj, counts as there). */
+int pekf_filter_run(pekf_filter *f, int64_t n_steps, int64_t window, int64_t step0, const void *plane_gd,
+                    const void *plane_am, const void *plane_my, double *traj, const int32_t *counts,
+                    void *stream);
+
 /* ---------------- synthetic IMU streams (device mirror of poseestimationkf_amd/synth.py) --------
  * Filters first_filter .. first_filter+batch-1, window steps, bit-identical to the host
  * generator.  scales[5] = sqrt(3)*sigma for {ref, w, gyro, acc, mag}; ar_w = AR(1) factor.

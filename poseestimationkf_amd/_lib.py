@@ -77,6 +77,15 @@ SIGNATURES = {
     "pekf_run_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp, _u32, _vp],
     "pekf_reset_state_dev": [_i64, _vp, _vp, _vp],
     "pekf_state_layout_dev": [_i64, _vp, _vp, _vp, _vp, _int, _vp],
+    "pekf_filter_create": [_i64, _vp, _vp, _dbl, _dbl, _vp, _u32, ctypes.POINTER(_vp)],
+    "pekf_filter_destroy": [_vp],
+    "pekf_filter_set_state": [_vp, _vp, _vp],
+    "pekf_filter_get_state": [_vp, _vp, _vp],
+    "pekf_filter_set_time": [_vp, _vp],
+    "pekf_filter_device_state": [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp)],
+    "pekf_filter_update": [_vp] * 7,
+    "pekf_filter_update_dev": [_vp] * 8,
+    "pekf_filter_run": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "pekf_gyro_chain_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "pekf_wahba_stream_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp],
     "pekf_quat_to_rpy": [_i64, _dp, _dp],

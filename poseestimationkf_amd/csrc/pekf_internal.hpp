@@ -68,4 +68,9 @@ class Staging {
     int device_ = -1;
 };
 
+// Filter-handle update kernel launcher (pekf_run.hip): one FP64 record per filter.
+int launch_update(int64_t batch, const double *gyro, const int64_t *t_ns, const double *acc, const double *mag,
+                  const uint8_t *missing, const double *refs, int64_t *prev_t, double *X, double *P, double q,
+                  double r, double *x_out, uint32_t flags, hipStream_t stream);
+
 }  // namespace pekf

@@ -66,6 +66,58 @@ __device__ __forceinline__ void store_state(double *X, double *P, int64_t b, int
     }
 }
 
+// One record of main_file.py:42-45 -- Prediction(gyro, T) then Correction(mag, acc) -- on the
+// lane's state (x, P) in registers.  hw = gyro / 2, dt_ns = T - previousT, missing: the record
+// has no magnetometer sample (Wahba-skip, X = z, P = P-).  Shared by the fused stream kernel and
+// the handle's per-record update, so both give bit-identical results for the same inputs.
+template <typename PT>
+__device__ __forceinline__ void ekf_record_step(double *x, Sym4T<PT> &P, const Frame &Wf, PT g, PT rp, PT r2,
+                                                double rs, const double *hw, double dt_ns, bool missing,
+                                                const double *acc, const double *mag) {
+    // ---- Prediction (ExtendedKalmanFilter.py:58-68) ----
+    const PT hp[3] = {(PT)hw[0], (PT)hw[1], (PT)hw[2]};
+    const PT xp[4] = {(PT)x[0], (PT)x[1], (PT)x[2], (PT)x[3]};
+    const Sym4T<PT> Pm = propagate_cov<PT>(P, hp, xp, g);  // Jb from the prior X (:60)
+    double z[4];
+    rk4_closed(x, dt_ns, hw, z);                            // (:62)
+
+    if (missing) {
+        // Wahba-skip: no Correction for this record (X = z, P = P-)
+        x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
+        P = Pm;
+    } else {
+        // S = P- + rI; K = P- S^-1 = I - r S^-1  (:63-66)
+        const Sym4T<PT> S = {Pm.a00 + rp, Pm.a01, Pm.a02, Pm.a03, Pm.a11 + rp,
+                             Pm.a12, Pm.a13, Pm.a22 + rp, Pm.a23, Pm.a33 + rp};
+        const Sym4T<PT> Si = spd_inverse<PT, true>(S);
+
+        // ---- Correction (ExtendedKalmanFilter.py:70-80) ----
+        const double ka = fabs(acc[2]);              // (:71)
+        Frame Vf;
+        make_frame<true>(acc, mag, Vf);
+        double R[9], y[4];
+        wahba_rotation<true>(Wf, Vf, ka, 1.0 - ka, R);  // Wahba.py:8-17
+        rotm_to_quat_fast(R, y);                      // Wahba.py:19-47
+        const double cmp = y[0] * z[0] + y[1] * z[1] + y[2] * z[2] + y[3] * z[3];
+        const double sg = cmp < 0.0 ? -1.0 : 1.0;     // (:73-75)
+        y[0] *= sg; y[1] *= sg; y[2] *= sg; y[3] *= sg;
+        const PT e0 = (PT)(y[0] - z[0]), e1 = (PT)(y[1] - z[1]);
+        const PT e2 = (PT)(y[2] - z[2]), e3 = (PT)(y[3] - z[3]);
+        // X = z + K e = Y - r S^-1 e (:77), normalised (:79)
+        const double u0 = Si.a00 * e0 + Si.a01 * e1 + Si.a02 * e2 + Si.a03 * e3;
+        const double u1 = Si.a01 * e0 + Si.a11 * e1 + Si.a12 * e2 + Si.a13 * e3;
+        const double u2 = Si.a02 * e0 + Si.a12 * e1 + Si.a22 * e2 + Si.a23 * e3;
+        const double u3 = Si.a03 * e0 + Si.a13 * e1 + Si.a23 * e2 + Si.a33 * e3;
+        const double x0 = y[0] - rs * u0, x1 = y[1] - rs * u1;
+        const double x2 = y[2] - rs * u2, x3 = y[3] - rs * u3;
+        const double in = rsqrt<true>(x0 * x0 + x1 * x1 + x2 * x2 + x3 * x3);
+        x[0] = x0 * in; x[1] = x1 * in; x[2] = x2 * in; x[3] = x3 * in;
+        // P = P- - K P- = r K = r I - r^2 S^-1 (:78)
+        P = {rp - r2 * Si.a00, -r2 * Si.a01, -r2 * Si.a02, -r2 * Si.a03, rp - r2 * Si.a11,
+             -r2 * Si.a12, -r2 * Si.a13, rp - r2 * Si.a22, -r2 * Si.a23, rp - r2 * Si.a33};
+    }
+}
+
 // MIXED = false: every operation in FP64 (the headline path).
 // MIXED = true (opt-in, PEKF_RUN_MIXED_PRECISION): the covariance recursion (P-, S^-1, K, P)
 // in FP32 while RK4, Wahba, R->q and the X update stay FP64 (~2e-8 vs FP64).
@@ -113,56 +165,13 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     // One record: Prediction + Correction (main_file.py:42-45) on (x, P) in registers.
     auto step = [&](const Rec &cur, int64_t t) {
         if (!COUNTS || t < my_steps) {
-
-        const double hw[3] = {0.5 * (double)cur.gd.x, 0.5 * (double)cur.gd.y, 0.5 * (double)cur.gd.z};
-        const uint32_t word = __float_as_uint(cur.gd.w);
-        const double dt_ns = (double)(word & 0x7FFFFFFFu);
-
-        // ---- Prediction (ExtendedKalmanFilter.py:58-68) ----
-        const PT hp[3] = {(PT)hw[0], (PT)hw[1], (PT)hw[2]};
-        const PT xp[4] = {(PT)x[0], (PT)x[1], (PT)x[2], (PT)x[3]};
-        const Sym4T<PT> Pm = propagate_cov<PT>(P, hp, xp, g);  // Jb from the prior X (:60)
-        double z[4];
-        rk4_closed(x, dt_ns, hw, z);                            // (:62)
-
-        if (word & PEKF_MISSING_MAG_BIT) {
-            // Wahba-skip: no Correction for this record (X = z, P = P-)
-            x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
-            P = Pm;
-        } else {
-            // S = P- + rI; K = P- S^-1 = I - r S^-1  (:63-66)
-            const Sym4T<PT> S = {Pm.a00 + rp, Pm.a01, Pm.a02, Pm.a03, Pm.a11 + rp,
-                                 Pm.a12, Pm.a13, Pm.a22 + rp, Pm.a23, Pm.a33 + rp};
-            const Sym4T<PT> Si = spd_inverse<PT, true>(S);
-
-            // ---- Correction (ExtendedKalmanFilter.py:70-80) ----
+            const double hw[3] = {0.5 * (double)cur.gd.x, 0.5 * (double)cur.gd.y, 0.5 * (double)cur.gd.z};
+            const uint32_t word = __float_as_uint(cur.gd.w);
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
-            const double ka = fabs(acc[2]);              // (:71)
-            Frame Vf;
-            make_frame<true>(acc, mag, Vf);
-            double R[9], y[4];
-            wahba_rotation<true>(Wf, Vf, ka, 1.0 - ka, R);  // Wahba.py:8-17
-            rotm_to_quat_fast(R, y);                      // Wahba.py:19-47
-            const double cmp = y[0] * z[0] + y[1] * z[1] + y[2] * z[2] + y[3] * z[3];
-            const double sg = cmp < 0.0 ? -1.0 : 1.0;     // (:73-75)
-            y[0] *= sg; y[1] *= sg; y[2] *= sg; y[3] *= sg;
-            const PT e0 = (PT)(y[0] - z[0]), e1 = (PT)(y[1] - z[1]);
-            const PT e2 = (PT)(y[2] - z[2]), e3 = (PT)(y[3] - z[3]);
-            // X = z + K e = Y - r S^-1 e (:77), normalised (:79)
-            const double u0 = Si.a00 * e0 + Si.a01 * e1 + Si.a02 * e2 + Si.a03 * e3;
-            const double u1 = Si.a01 * e0 + Si.a11 * e1 + Si.a12 * e2 + Si.a13 * e3;
-            const double u2 = Si.a02 * e0 + Si.a12 * e1 + Si.a22 * e2 + Si.a23 * e3;
-            const double u3 = Si.a03 * e0 + Si.a13 * e1 + Si.a23 * e2 + Si.a33 * e3;
-            const double x0 = y[0] - rs * u0, x1 = y[1] - rs * u1;
-            const double x2 = y[2] - rs * u2, x3 = y[3] - rs * u3;
-            const double in = rsqrt<true>(x0 * x0 + x1 * x1 + x2 * x2 + x3 * x3);
-            x[0] = x0 * in; x[1] = x1 * in; x[2] = x2 * in; x[3] = x3 * in;
-            // P = P- - K P- = r K = r I - r^2 S^-1 (:78)
-            P = {rp - r2 * Si.a00, -r2 * Si.a01, -r2 * Si.a02, -r2 * Si.a03, rp - r2 * Si.a11,
-                 -r2 * Si.a12, -r2 * Si.a13, rp - r2 * Si.a22, -r2 * Si.a23, rp - r2 * Si.a33};
+            ekf_record_step<PT>(x, P, Wf, g, rp, r2, rs, hw, (double)(word & 0x7FFFFFFFu),
+                                (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
         }
-        }  // t < my_steps
         if (TRAJ) {
             double2 *o = reinterpret_cast<double2 *>(traj + t * batch * 4) + 2 * (int64_t)lane;
             o[0] = make_double2(x[0], x[1]);
@@ -211,6 +220,65 @@ __global__ __launch_bounds__(kRunBlock) void k_reset(int64_t batch, double *X, d
     X[4 * b] = 1.0; X[4 * b + 1] = 0.0; X[4 * b + 2] = 0.0; X[4 * b + 3] = 0.0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) P[16 * b + k] = (k % 5 == 0) ? 1.0 : 0.0;
+}
+
+// One record per filter from FP64 arrays (the filter handle's online update,
+// pekf_filter_update): dt = t - previousT per filter (ExtendedKalmanFilter.py:62,67), then the
+// same ekf_record_step as the stream kernel.  Record arrays are filter-major ([batch][3]).
+template <bool MIXED, bool SOA>
+__global__ __launch_bounds__(kRunBlock) void k_update(int64_t batch, const double *__restrict__ gyro,
+                                                      const int64_t *__restrict__ t_ns,
+                                                      const double *__restrict__ acc,
+                                                      const double *__restrict__ mag,
+                                                      const uint8_t *__restrict__ missing,
+                                                      const double *__restrict__ refs, int64_t *__restrict__ prev_t,
+                                                      double *__restrict__ Xio, double *__restrict__ Pio, double qs,
+                                                      double rs, double *__restrict__ x_out) {
+    using PT = typename std::conditional<MIXED, float, double>::type;
+    const int64_t b = (int64_t)blockIdx.x * kRunBlock + threadIdx.x;
+    if (b >= batch) return;
+    Frame Wf;
+    {
+        const double a0[3] = {refs[6 * b + 0], refs[6 * b + 1], refs[6 * b + 2]};
+        const double m0[3] = {refs[6 * b + 3], refs[6 * b + 4], refs[6 * b + 5]};
+        make_frame<true>(a0, m0, Wf);
+    }
+    double x[4];
+    Sym4T<PT> P;
+    load_state<SOA>(Xio, Pio, b, batch, x, P);
+    const int64_t t = t_ns[b];
+    const double dt_ns = (double)(t - prev_t[b]);
+    prev_t[b] = t;
+    const double hw[3] = {0.5 * gyro[3 * b], 0.5 * gyro[3 * b + 1], 0.5 * gyro[3 * b + 2]};
+    const double a[3] = {acc[3 * b], acc[3 * b + 1], acc[3 * b + 2]};
+    const double m[3] = {mag[3 * b], mag[3 * b + 1], mag[3 * b + 2]};
+    ekf_record_step<PT>(x, P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), rs, hw, dt_ns,
+                        missing && missing[b], a, m);
+    store_state<SOA>(Xio, Pio, b, batch, x, P);
+    if (x_out) {
+        double2 *o = reinterpret_cast<double2 *>(x_out) + 2 * b;
+        o[0] = make_double2(x[0], x[1]);
+        o[1] = make_double2(x[2], x[3]);
+    }
+}
+
+int launch_update(int64_t batch, const double *gyro, const int64_t *t_ns, const double *acc, const double *mag,
+                  const uint8_t *missing, const double *refs, int64_t *prev_t, double *X, double *P, double q,
+                  double r, double *x_out, uint32_t flags, hipStream_t stream) {
+    const dim3 grid(grid_for(batch, kRunBlock)), block(kRunBlock);
+    const bool mixed = flags & PEKF_RUN_MIXED_PRECISION, soa = flags & PEKF_RUN_STATE_SOA;
+#define PEKF_LAUNCH_UPDATE(MX, SO)                                                                \
+    hipLaunchKernelGGL((k_update<MX, SO>), grid, block, 0, stream, batch, gyro, t_ns, acc, mag, missing, \
+                       refs, prev_t, X, P, q, r, x_out)
+    if (mixed) {
+        if (soa) PEKF_LAUNCH_UPDATE(true, true); else PEKF_LAUNCH_UPDATE(true, false);
+    } else {
+        if (soa) PEKF_LAUNCH_UPDATE(false, true); else PEKF_LAUNCH_UPDATE(false, false);
+    }
+#undef PEKF_LAUNCH_UPDATE
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "k_update");
+    return PEKF_OK;
 }
 
 }  // namespace pekf

@@ -349,6 +349,82 @@ class BatchedEKF:
         return None
 
 
+class FilterHandle:
+    """B KalmanFilter objects behind one native handle (pekf_filter_*).
+
+    The handle owns what the reference object owns (ExtendedKalmanFilter.py:6-15): the Wahba
+    reference (acc0, mag0), Q = q I, R = r I and previousT, plus the state X, P, which stays in
+    device memory.  `update` is one main_file.py:42-45 iteration for every filter from FP64
+    host arrays (online serving); `run` advances the same state through a resident stream window.
+    """
+
+    def __init__(self, acc0, mag0, q=1.0, r=0.1, t0_ns=None, precision="f64", layout="aos"):
+        acc0 = np.ascontiguousarray(acc0, np.float64).reshape(-1, 3)
+        mag0 = np.ascontiguousarray(mag0, np.float64).reshape(-1, 3)
+        self.batch = acc0.shape[0]
+        assert mag0.shape[0] == self.batch
+        flags = (RUN_MIXED_PRECISION if precision == "mixed" else 0) | (RUN_STATE_SOA if layout == "soa" else 0)
+        t0 = None if t0_ns is None else np.ascontiguousarray(t0_ns, np.int64).reshape(self.batch)
+        h = ctypes.c_void_p()
+        check(lib.pekf_filter_create(self.batch, acc0.ctypes.data, mag0.ctypes.data, float(q), float(r),
+                                     t0.ctypes.data if t0 is not None else None, flags, ctypes.byref(h)))
+        self.h = h.value
+
+    def update(self, gyro, t_ns, acc, mag, missing=None, want_x=True):
+        """One record per filter: Prediction(gyro, t_ns) + Correction(mag, acc). Returns X (B, 4)."""
+        B = self.batch
+        g, a, m = (np.ascontiguousarray(v, np.float64).reshape(B, 3) for v in (gyro, acc, mag))
+        t = np.ascontiguousarray(t_ns, np.int64).reshape(B)
+        miss = None if missing is None else np.ascontiguousarray(missing, np.uint8).reshape(B)
+        X = np.empty((B, 4)) if want_x else None
+        check(lib.pekf_filter_update(self.h, g.ctypes.data, t.ctypes.data, a.ctypes.data, m.ctypes.data,
+                                     miss.ctypes.data if miss is not None else None,
+                                     X.ctypes.data if X is not None else None))
+        return X
+
+    def run(self, win: IMUWindow, n_steps=None, step0=0, want_traj=False, counts=None):
+        """pekf_filter_run over a resident window (the window's refs are not used: the handle's are)."""
+        n_steps = win.window if n_steps is None else int(n_steps)
+        assert win.batch == self.batch
+        tb = DeviceBuffer(32 * n_steps * self.batch) if want_traj else None
+        if counts is None and win.counts is not None:
+            counts = np.clip(np.asarray(win.counts, np.int64) - int(step0), 0, n_steps)
+        cb = None
+        if counts is not None:
+            c = np.ascontiguousarray(counts, dtype=np.int32).reshape(self.batch)
+            cb = DeviceBuffer(c.nbytes).upload(c)
+        check(lib.pekf_filter_run(self.h, n_steps, win.window, int(step0), win.gd.ptr, win.am.ptr, win.my.ptr,
+                                  tb.ptr if tb is not None else None, cb.ptr if cb is not None else None, None))
+        check(lib.pekf_device_sync())
+        return tb.download((n_steps, self.batch, 4), np.float64) if want_traj else None
+
+    def set_state(self, X=None, P=None):
+        Xa = None if X is None else f64(X, (self.batch, 4))
+        Pa = None if P is None else f64(P, (self.batch, 4, 4))
+        check(lib.pekf_filter_set_state(self.h, Xa.ctypes.data if Xa is not None else None,
+                                        Pa.ctypes.data if Pa is not None else None))
+
+    def get_state(self):
+        X, P = np.empty((self.batch, 4)), np.empty((self.batch, 4, 4))
+        check(lib.pekf_filter_get_state(self.h, X.ctypes.data, P.ctypes.data))
+        return X, P
+
+    def set_time(self, t_ns):
+        t = np.ascontiguousarray(t_ns, np.int64).reshape(self.batch)
+        check(lib.pekf_filter_set_time(self.h, t.ctypes.data))
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.pekf_filter_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 # ------------------------------------------------------------------ batched per-call operators
 # NumPy-level wrappers over the host-pointer entry points (one GPU thread per item).
 

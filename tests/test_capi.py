@@ -54,6 +54,8 @@ def test_no_cpu_fallback_without_device():
         engine.rk4(np.array([1.0, 0, 0, 0]), 1e7, np.zeros(3))
     with pytest.raises(_lib.NoDeviceError):
         engine.BatchedEKF(4)
+    with pytest.raises(_lib.NoDeviceError):
+        engine.FilterHandle(np.zeros((4, 3)), np.zeros((4, 3)))
     p = ctypes.c_void_p()
     assert _lib.lib.pekf_malloc(ctypes.byref(p), 64) == _lib.PEKF_ERR_NODEVICE
     assert "no HIP device" in _lib.last_error()
@@ -69,6 +71,14 @@ def test_invalid_arguments_are_reported_not_crashed():
     assert st == _lib.PEKF_ERR_INVALID and "flags" in _lib.last_error()
     st = _lib.lib.pekf_state_layout_dev(4, None, None, None, None, 1, None)
     assert st == _lib.PEKF_ERR_INVALID and "null" in _lib.last_error()
+    h = ctypes.c_void_p()
+    st = _lib.lib.pekf_filter_create(0, None, None, 1.0, 0.1, None, 0, ctypes.byref(h))
+    assert st == _lib.PEKF_ERR_INVALID and "batch" in _lib.last_error() and not h.value
+    st = _lib.lib.pekf_filter_create(4, None, None, 1.0, 0.1, None, 0, ctypes.byref(h))
+    assert st == _lib.PEKF_ERR_INVALID and "null" in _lib.last_error()
+    assert _lib.lib.pekf_filter_destroy(None) == _lib.PEKF_OK
+    st = _lib.lib.pekf_filter_update(None, None, None, None, None, None, None)
+    assert st == _lib.PEKF_ERR_INVALID and "handle" in _lib.last_error()
 
 
 def test_product_package_never_imports_the_oracle():
