@@ -261,7 +261,10 @@ PEKF_DEV void wahba_rotation_vectors(const double *acc0, const double *mag0, con
 // (Wahba.py:28,35, strict '>', else branch 3) is made by selects, then ONE rsqrt gives both
 // 1/S = 0.5/sqrt(t) and 0.25*S = 0.5*t/sqrt(t).  Agrees with rotm_to_quat to ~1 ulp; at an
 // exact identity both give NaNs (which the filter update propagates identically).
-PEKF_DEV void rotm_to_quat_fast(const double *M, double *q) {
+// Scaled form: q = v * inv_s with inv_s = 1/S > 0 (the branch's own component of v is t, since
+// S/4 = t/S), so a caller that only needs q up to a positive scale first (the hemisphere test
+// of ExtendedKalmanFilter.py:73-75) folds the sign into the one scale factor.
+PEKF_DEV void rotm_to_quat_scaled(const double *M, double *v, double &inv_s) {
     const double t1 = ((1.0 + M[0]) - M[4]) - M[8];
     const double t2 = ((1.0 - M[0]) + M[4]) - M[8];
     const double t3 = ((1.0 - M[0]) - M[4]) + M[8];
@@ -269,14 +272,19 @@ PEKF_DEV void rotm_to_quat_fast(const double *M, double *q) {
     const bool b2 = !b1 && (t2 > t1) && (t2 > t3);
     const bool b3 = !b1 && !b2;
     const double t = b1 ? t1 : (b2 ? t2 : t3);
-    const double rs = rsqrt<true>(t);
-    const double inv_s = 0.5 * rs, quarter_s = 0.5 * (t * rs);
+    inv_s = 0.5 * rsqrt<true>(t);
     const double dw1 = M[7] - M[5], dw2 = M[2] - M[6], dw3 = M[3] - M[1];
     const double sxy = M[1] + M[3], sxz = M[2] + M[6], syz = M[5] + M[7];
-    q[0] = (b1 ? dw1 : (b2 ? dw2 : dw3)) * inv_s;
-    q[1] = b1 ? quarter_s : (b2 ? sxy : sxz) * inv_s;
-    q[2] = b2 ? quarter_s : (b1 ? sxy : syz) * inv_s;
-    q[3] = b3 ? quarter_s : (b1 ? sxz : syz) * inv_s;
+    v[0] = b1 ? dw1 : (b2 ? dw2 : dw3);
+    v[1] = b1 ? t : (b2 ? sxy : sxz);
+    v[2] = b2 ? t : (b1 ? sxy : syz);
+    v[3] = b3 ? t : (b1 ? sxz : syz);
+}
+
+PEKF_DEV void rotm_to_quat_fast(const double *M, double *q) {
+    double v[4], inv_s;
+    rotm_to_quat_scaled(M, v, inv_s);
+    q[0] = v[0] * inv_s; q[1] = v[1] * inv_s; q[2] = v[2] * inv_s; q[3] = v[3] * inv_s;
 }
 
 // ------------------------------- fused-step forms --------------------------------------------
@@ -376,6 +384,41 @@ PEKF_DEV Sym4T<T> spd_inverse(const Sym4T<T> &S) {
     o.a02 = m20 + n30 * m32;
     o.a01 = m10 + n20 * m21 + n30 * m31;
     o.a00 = i0 + n10 * m10 + n20 * m20 + n30 * m30;
+    return o;
+}
+
+// Inverse of an SPD 4x4 by 2x2 blocks, S = [[A, B], [B^T, D]]: A^-1 by its adjugate, the Schur
+// complement C = D - B^T A^-1 B (SPD) likewise, then
+//   S^-1 = [[A^-1 + X C^-1 X^T, -X C^-1], [-C^-1 X^T, C^-1]],  X = A^-1 B.
+// Two reciprocals instead of LDL^T's four (a v_rcp_f64 issues at 3x an FMA on gfx950,
+// scripts/probe_rates.hip): 38 plain operations + 2 Newton-refined reciprocals.
+template <typename T, bool FAST = true>
+PEKF_DEV Sym4T<T> spd_inverse_schur(const Sym4T<T> &S) {
+    const T ia = recip<FAST>(S.a00 * S.a11 - S.a01 * S.a01);
+    const T p00 = S.a11 * ia, p01 = -S.a01 * ia, p11 = S.a00 * ia;  // A^-1
+    // X = A^-1 B, B = [[a02, a03], [a12, a13]]
+    const T x00 = p00 * S.a02 + p01 * S.a12, x01 = p00 * S.a03 + p01 * S.a13;
+    const T x10 = p01 * S.a02 + p11 * S.a12, x11 = p01 * S.a03 + p11 * S.a13;
+    // C = D - B^T X
+    const T c00 = S.a22 - S.a02 * x00 - S.a12 * x10;
+    const T c01 = S.a23 - S.a02 * x01 - S.a12 * x11;
+    const T c11 = S.a33 - S.a03 * x01 - S.a13 * x11;
+    const T ic = recip<FAST>(c00 * c11 - c01 * c01);
+    const T q00 = c11 * ic, q01 = -c01 * ic, q11 = c00 * ic;        // C^-1
+    // off-diagonal block O = -X C^-1, top-left A^-1 - O X^T
+    const T o00 = -(x00 * q00 + x01 * q01), o01 = -(x00 * q01 + x01 * q11);
+    const T o10 = -(x10 * q00 + x11 * q01), o11 = -(x10 * q01 + x11 * q11);
+    Sym4T<T> o;
+    o.a00 = p00 - o00 * x00 - o01 * x01;
+    o.a01 = p01 - o00 * x10 - o01 * x11;
+    o.a11 = p11 - o10 * x10 - o11 * x11;
+    o.a02 = o00;
+    o.a03 = o01;
+    o.a12 = o10;
+    o.a13 = o11;
+    o.a22 = q00;
+    o.a23 = q01;
+    o.a33 = q11;
     return o;
 }
 

@@ -89,18 +89,19 @@ __device__ __forceinline__ void ekf_record_step(double *x, Sym4T<PT> &P, const F
         // S = P- + rI; K = P- S^-1 = I - r S^-1  (:63-66)
         const Sym4T<PT> S = {Pm.a00 + rp, Pm.a01, Pm.a02, Pm.a03, Pm.a11 + rp,
                              Pm.a12, Pm.a13, Pm.a22 + rp, Pm.a23, Pm.a33 + rp};
-        const Sym4T<PT> Si = spd_inverse<PT, true>(S);
+        const Sym4T<PT> Si = spd_inverse_schur<PT, true>(S);
 
         // ---- Correction (ExtendedKalmanFilter.py:70-80) ----
         const double ka = fabs(acc[2]);              // (:71)
         Frame Vf;
         make_frame<true>(acc, mag, Vf);
-        double R[9], y[4];
+        double R[9], y[4], inv_s;
         wahba_rotation<true>(Wf, Vf, ka, 1.0 - ka, R);  // Wahba.py:8-17
-        rotm_to_quat_fast(R, y);                      // Wahba.py:19-47
+        rotm_to_quat_scaled(R, y, inv_s);             // Wahba.py:19-47, Y = y * inv_s, inv_s > 0
+        // hemisphere flip (:73-75): sign(Y.z) = sign(y.z), so the flip goes into the scale
         const double cmp = y[0] * z[0] + y[1] * z[1] + y[2] * z[2] + y[3] * z[3];
-        const double sg = cmp < 0.0 ? -1.0 : 1.0;     // (:73-75)
-        y[0] *= sg; y[1] *= sg; y[2] *= sg; y[3] *= sg;
+        const double sc = cmp < 0.0 ? -inv_s : inv_s;
+        y[0] *= sc; y[1] *= sc; y[2] *= sc; y[3] *= sc;
         const PT e0 = (PT)(y[0] - z[0]), e1 = (PT)(y[1] - z[1]);
         const PT e2 = (PT)(y[2] - z[2]), e3 = (PT)(y[3] - z[3]);
         // X = z + K e = Y - r S^-1 e (:77), normalised (:79)
