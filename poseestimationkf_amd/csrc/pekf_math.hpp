@@ -185,55 +185,56 @@ PEKF_DEV double rsqrt(double x) {
 
 // Orthonormal frame of a vector pair (a, m): e1 = a/|a|, e2 = GramSchmidt(m), u3 = e1 x e2,
 // with the coordinates of a and m in it: a = alpha e1, m = beta1 e1 + beta2 e2.
+// sg = -1 gives the frame [e1, -e2, -u3] (beta2 -> -beta2), still proper: see wahba_rotation.
 struct Frame {
     double e1[3], e2[3], u3[3];
     double alpha, beta1, beta2;
 };
 
 template <bool FAST = false>
-PEKF_DEV void make_frame(const double *a, const double *m, Frame &F) {
+PEKF_DEV void make_frame(const double *a, const double *m, Frame &F, double sg = 1.0) {
     const double sa = a[0] * a[0] + a[1] * a[1] + a[2] * a[2];
     const double ia = rsqrt<FAST>(sa);
     F.e1[0] = a[0] * ia; F.e1[1] = a[1] * ia; F.e1[2] = a[2] * ia;
     const double b1 = F.e1[0] * m[0] + F.e1[1] * m[1] + F.e1[2] * m[2];
     const double t0 = m[0] - b1 * F.e1[0], t1 = m[1] - b1 * F.e1[1], t2 = m[2] - b1 * F.e1[2];
     const double sb = t0 * t0 + t1 * t1 + t2 * t2;
-    const double ib = rsqrt<FAST>(sb);
+    const double ib = sg * rsqrt<FAST>(sb);
     F.e2[0] = t0 * ib; F.e2[1] = t1 * ib; F.e2[2] = t2 * ib;
     F.u3[0] = F.e1[1] * F.e2[2] - F.e1[2] * F.e2[1];
     F.u3[1] = F.e1[2] * F.e2[0] - F.e1[0] * F.e2[2];
     F.u3[2] = F.e1[0] * F.e2[1] - F.e1[1] * F.e2[0];
     F.alpha = FAST ? sa * ia : sqrt(sa);
     F.beta1 = b1;
-    F.beta2 = FAST ? sb * ib : sqrt(sb);
+    F.beta2 = FAST ? sb * ib : sg * sqrt(sb);
 }
 
+// sign(det C) of the Wahba core below for weights (ka, km): +1 rotation, -1 reflection case.
+PEKF_DEV double wahba_sign(double ka, double km) { return ka * km >= 0.0 ? 1.0 : -1.0; }
+
 // R = argmax_{R in SO(3)} tr(R^T B), B = ka acc0 acc^T + km mag0 mag^T (Wahba.py:8-17):
-// W = frame of the reference pair (acc0, mag0), V = frame of the current pair (acc, mag).
+// W = frame of the reference pair (acc0, mag0), V = frame of the current pair (acc, mag) built
+// with sg = wahba_sign(ka, km).
+//   C = Fw^T B Fv = [[c00, c01], [c10, c11]]: c00 = ka aW aV + km b1W b1V, c01 = km b1W b2V,
+//   c10 = km b2W b1V, c11 = km b2W b2V, and det C = ka km aW aV b2W b2V exactly (a, b2 >= 0).
+// For det C < 0 the optimum is Fw diag(P2r, -1) Fv^T with P2r the reflection polar factor;
+// with the current frame flipped to Fv' = [e1, -e2, -u3] (V.beta2 -> -beta2) this is the
+// rotation form R = Fw diag(P2, 1) Fv'^T, P2 = [[p, -s], [s, p]] the polar factor of
+// C' = C diag(1, sg): (p, s) = (c00 + c11', c10 - c01'), one formula for both cases.
 template <bool FAST = false>
 PEKF_DEV void wahba_rotation(const Frame &W, const Frame &V, double ka, double km, double *R) {
-    // C = [[c00, c01], [c10, c11]]: c00 = ka aW aV + km b1W b1V, c01 = km b1W b2V,
-    // c10 = km b2W b1V, c11 = km b2W b2V.
-    // det C = ka km alpha_W alpha_V beta2_W beta2_V exactly; alpha, beta2 >= 0
-    const bool proper = ka * km >= 0.0;
-    // polar factor of C from (p, s) = (c00 + c11, c10 - c01) (rotation) or (c00 - c11, c01 + c10)
-    // (reflection); the sign goes into km' so each is one expression (contracted alike everywhere)
-    const double kw = km * W.beta2, kn = proper ? kw : -kw, kb = km * W.beta1;
-    double p = ka * W.alpha * V.alpha + kb * V.beta1 + kn * V.beta2;
-    double s = kw * V.beta1 - (proper ? kb : -kb) * V.beta2;
+    const double kw = km * W.beta2, kb = km * W.beta1;
+    double p = ka * W.alpha * V.alpha + kb * V.beta1 + kw * V.beta2;
+    double s = kw * V.beta1 - kb * V.beta2;
     const double ih = rsqrt<FAST>(p * p + s * s);
     p *= ih;
     s *= ih;
-    // P2 = [[p, -s], [s, p]] (rotation) or [[p, s], [s, -p]] (reflection); c = +1 / -1
-    const double p00 = p, p01 = proper ? -s : s, p10 = s, p11 = proper ? p : -p;
-    const double c = proper ? 1.0 : -1.0;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        const double g0 = W.e1[i] * p00 + W.e2[i] * p10;
-        const double g1 = W.e1[i] * p01 + W.e2[i] * p11;
-        const double g2 = c * W.u3[i];
+        const double g0 = W.e1[i] * p + W.e2[i] * s;     // Fw P2, column 0
+        const double g1 = W.e2[i] * p - W.e1[i] * s;     // Fw P2, column 1
 #pragma unroll
-        for (int j = 0; j < 3; ++j) R[i * 3 + j] = g0 * V.e1[j] + g1 * V.e2[j] + g2 * V.u3[j];
+        for (int j = 0; j < 3; ++j) R[i * 3 + j] = g0 * V.e1[j] + g1 * V.e2[j] + W.u3[i] * V.u3[j];
     }
 }
 
@@ -253,7 +254,7 @@ PEKF_DEV void wahba_rotation_vectors(const double *acc0, const double *mag0, con
                                      const double *mag, double ka, double km, double *R) {
     Frame W, V;
     make_frame(acc0, mag0, W);
-    make_frame(acc, mag, V);
+    make_frame(acc, mag, V, wahba_sign(ka, km));
     wahba_rotation(W, V, ka, km, R);
 }
 

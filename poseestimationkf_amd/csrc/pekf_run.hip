@@ -7,7 +7,7 @@
 // (10 f64) and the filter's Wahba reference frame live in VGPRs for the whole launch;
 // HBM traffic is the 40 B/filter-step input record plus, once per launch, the state
 // and reference vectors.  The next step's record is loaded before the current step's
-// arithmetic so its latency hides under ~600 FP64 instructions of work.
+// arithmetic so its latency hides under ~400 VALU instructions of work.
 // No MFMA: every contraction is 4x4 / 3x3 per lane.
 #include <type_traits>
 
@@ -94,7 +94,7 @@ __device__ __forceinline__ void ekf_record_step(double *x, Sym4T<PT> &P, const F
         // ---- Correction (ExtendedKalmanFilter.py:70-80) ----
         const double ka = fabs(acc[2]);              // (:71)
         Frame Vf;
-        make_frame<true>(acc, mag, Vf);
+        make_frame<true>(acc, mag, Vf, wahba_sign(ka, 1.0 - ka));
         double R[9], y[4], inv_s;
         wahba_rotation<true>(Wf, Vf, ka, 1.0 - ka, R);  // Wahba.py:8-17
         rotm_to_quat_scaled(R, y, inv_s);             // Wahba.py:19-47, Y = y * inv_s, inv_s > 0

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kSideBlock) void k_wahba_stream(int64_t batch, int6
         const float2 m = my[row * batch + b];
         const double acc[3] = {a.x, a.y, a.z}, mag[3] = {a.w, m.x, m.y};
         Frame Vf;
-        make_frame<true>(acc, mag, Vf);
+        make_frame<true>(acc, mag, Vf, wahba_sign(ka, km));
         double R[9], y[4];
         wahba_rotation<true>(Wf, Vf, ka, km, R);
         rotm_to_quat_fast(R, y);  // keeps the reference's branch / sign convention
