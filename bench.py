@@ -214,7 +214,10 @@ def main():
         k_s = float(np.mean(kms)) / 1e3
         achieved = B * N * REC_BYTES / k_s / 1e9
         flop = ISA_COUNTS[args.precision]["flop"]
+        valu = ISA_COUNTS[args.precision]["valu_instr"]
         traffic, tsrc = measured_traffic(B, N) if args.precision == "f64" else (None, None)
+        clk = tsrc[1].get("effective_clock_ghz") if tsrc else None
+        issue_frac = (4.0 * (B / 64.0) * N * valu / (1024 * clk * 1e9 * k_s)) if clk else None
         out = {
             "metric": "EKF steps/sec (predict+Wahba+update) at batch=1M; HBM-roofline %",
             "value": value,
@@ -240,11 +243,13 @@ def main():
                          "kernel": "k_run<false> (pekf_run_dev)", "kernel_ms": k_s * 1e3,
                          "bytes_per_launch": B * N * REC_BYTES},
             "fp64_valu": {"flop_per_step": flop, "fp64_instr_per_step": ISA_COUNTS[args.precision]["fp64_instr"],
+                          "valu_instr_per_step": valu,
                           "achieved_tflops": B * N * flop / k_s / 1e12, "peak_tflops": FP64_PEAK_TFLOPS,
                           "frac": B * N * flop / k_s / 1e12 / FP64_PEAK_TFLOPS,
                           "valu_busy_pmc": tsrc[1].get("valu_busy") if tsrc else None,
-                          "note": "the kernel is FP64-VALU-issue-bound (valu_busy ~0.96); "
-                                  "HBM frac is capped by it"},
+                          "issue_frac": issue_frac,
+                          "note": "the kernel is VALU-issue-bound: issue_frac = 4 cycles x wave-instructions / "
+                                  "(1024 SIMDs x PMC effective clock x kernel time); HBM frac is capped by it"},
             "cpu_baseline": cpu,
             "parity": parity,
         }
@@ -261,8 +266,8 @@ def main():
 # scripts/isa_count.py (DESIGN.md "FP64 budget"): FP64 VALU instructions, and the FLOP of
 # the arithmetic ones with an FMA counted as 2.
 # per filter-step, from scripts/isa_count.py on the hot loop of k_run (make -C .../csrc asm)
-ISA_COUNTS = {"f64": {"flop": 567, "fp64_instr": 386, "valu_instr": 432},
-              "mixed": {"flop": 278, "fp64_instr": 227, "valu_instr": 447}}  # mixed: + ~220 f32 instructions
+ISA_COUNTS = {"f64": {"flop": 551, "fp64_instr": 376, "valu_instr": 405},
+              "mixed": {"flop": 272, "fp64_instr": 221, "valu_instr": 420}}  # mixed: + ~200 f32 instructions
 FLOP_PER_STEP = ISA_COUNTS["f64"]["flop"]
 FP64_INSTR_PER_STEP = ISA_COUNTS["f64"]["fp64_instr"]
 
