@@ -14,26 +14,47 @@ namespace pekf {
 
 constexpr int kSideBlock = 256;
 
+// Both stream kernels are HBM-bound (a few dozen FP64 ops per 16-24 B record), so each lane keeps
+// kDepth records in flight: a register ring filled kDepth rows ahead, the time loop unrolled by
+// kDepth so every ring index is static.  The prefetch row wraps inside the resident window, so
+// the loads past the last step read valid (unused) records and need no predicate.
+constexpr int kDepth = 8;
+
+__device__ __forceinline__ int64_t next_row(int64_t r, int64_t window) { return r + 1 == window ? 0 : r + 1; }
+
 __global__ __launch_bounds__(kSideBlock) void k_gyro_chain(int64_t batch, int64_t n_steps, int64_t window,
                                                            int64_t step0, const float4 *__restrict__ gd,
                                                            double *__restrict__ q, double *__restrict__ traj) {
     const int64_t b = (int64_t)blockIdx.x * kSideBlock + threadIdx.x;
     if (b >= batch) return;
+    const uint32_t lane = (uint32_t)b;
     double x[4] = {q[4 * b], q[4 * b + 1], q[4 * b + 2], q[4 * b + 3]};
-    int64_t row = step0 % window;
-    for (int64_t t = 0; t < n_steps; ++t) {
-        const float4 r = gd[row * batch + b];
-        const double hw[3] = {0.5 * (double)r.x, 0.5 * (double)r.y, 0.5 * (double)r.z};
-        const double dt_ns = (double)(__float_as_uint(r.w) & 0x7FFFFFFFu);
-        double z[4];
-        rk4_closed(x, dt_ns, hw, z);
-        x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
-        if (traj) {
-            double2 *o = reinterpret_cast<double2 *>(traj + (t * batch + b) * 4);
-            o[0] = make_double2(x[0], x[1]);
-            o[1] = make_double2(x[2], x[3]);
+    float4 ring[kDepth];
+    int64_t pf = step0 % window;  // next row to prefetch
+#pragma unroll
+    for (int k = 0; k < kDepth; ++k) {
+        ring[k] = (gd + pf * batch)[lane];
+        pf = next_row(pf, window);
+    }
+    for (int64_t t0 = 0; t0 < n_steps; t0 += kDepth) {
+#pragma unroll
+        for (int k = 0; k < kDepth; ++k) {
+            const int64_t t = t0 + k;
+            if (t >= n_steps) break;
+            const float4 r = ring[k];
+            ring[k] = (gd + pf * batch)[lane];
+            pf = next_row(pf, window);
+            const double hw[3] = {0.5 * (double)r.x, 0.5 * (double)r.y, 0.5 * (double)r.z};
+            const double dt_ns = (double)(__float_as_uint(r.w) & 0x7FFFFFFFu);
+            double z[4];
+            rk4_closed(x, dt_ns, hw, z);
+            x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
+            if (traj) {
+                double2 *o = reinterpret_cast<double2 *>(traj + t * batch * 4) + 2 * (int64_t)lane;
+                o[0] = make_double2(x[0], x[1]);
+                o[1] = make_double2(x[2], x[3]);
+            }
         }
-        row = row + 1 == window ? 0 : row + 1;
     }
     q[4 * b] = x[0]; q[4 * b + 1] = x[1]; q[4 * b + 2] = x[2]; q[4 * b + 3] = x[3];
 }
@@ -45,26 +66,43 @@ __global__ __launch_bounds__(kSideBlock) void k_wahba_stream(int64_t batch, int6
                                                              double km, double *__restrict__ out) {
     const int64_t b = (int64_t)blockIdx.x * kSideBlock + threadIdx.x;
     if (b >= batch) return;
+    const uint32_t lane = (uint32_t)b;
     Frame Wf;
     {
         const double a0[3] = {refs[6 * b + 0], refs[6 * b + 1], refs[6 * b + 2]};
         const double m0[3] = {refs[6 * b + 3], refs[6 * b + 4], refs[6 * b + 5]};
         make_frame<true>(a0, m0, Wf);
     }
-    int64_t row = step0 % window;
-    for (int64_t t = 0; t < n_steps; ++t) {
-        const float4 a = am[row * batch + b];
-        const float2 m = my[row * batch + b];
-        const double acc[3] = {a.x, a.y, a.z}, mag[3] = {a.w, m.x, m.y};
-        Frame Vf;
-        make_frame<true>(acc, mag, Vf, wahba_sign(ka, km));
-        double R[9], y[4];
-        wahba_rotation<true>(Wf, Vf, ka, km, R);
-        rotm_to_quat_fast(R, y);  // keeps the reference's branch / sign convention
-        double2 *o = reinterpret_cast<double2 *>(out + (t * batch + b) * 4);
-        o[0] = make_double2(y[0], y[1]);
-        o[1] = make_double2(y[2], y[3]);
-        row = row + 1 == window ? 0 : row + 1;
+    const double sg = wahba_sign(ka, km);
+    float4 ra[kDepth];
+    float2 rm[kDepth];
+    int64_t pf = step0 % window;
+#pragma unroll
+    for (int k = 0; k < kDepth; ++k) {
+        ra[k] = (am + pf * batch)[lane];
+        rm[k] = (my + pf * batch)[lane];
+        pf = next_row(pf, window);
+    }
+    for (int64_t t0 = 0; t0 < n_steps; t0 += kDepth) {
+#pragma unroll
+        for (int k = 0; k < kDepth; ++k) {
+            const int64_t t = t0 + k;
+            if (t >= n_steps) break;
+            const float4 a = ra[k];
+            const float2 m = rm[k];
+            ra[k] = (am + pf * batch)[lane];
+            rm[k] = (my + pf * batch)[lane];
+            pf = next_row(pf, window);
+            const double acc[3] = {a.x, a.y, a.z}, mag[3] = {a.w, m.x, m.y};
+            Frame Vf;
+            make_frame<true>(acc, mag, Vf, sg);
+            double R[9], y[4];
+            wahba_rotation<true>(Wf, Vf, ka, km, R);
+            rotm_to_quat_fast(R, y);  // keeps the reference's branch / sign convention
+            double2 *o = reinterpret_cast<double2 *>(out + t * batch * 4) + 2 * (int64_t)lane;
+            o[0] = make_double2(y[0], y[1]);
+            o[1] = make_double2(y[2], y[3]);
+        }
     }
 }
 
@@ -104,6 +142,7 @@ int pekf_gyro_chain_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t 
     PEKF_CHECK_ARG(batch >= 0 && n_steps >= 0, "negative size");
     if (batch == 0 || n_steps == 0) return PEKF_OK;
     PEKF_CHECK_ARG(window > 0 && step0 >= 0, "window must be > 0 and step0 >= 0");
+    PEKF_CHECK_ARG(batch < ((int64_t)1 << 28), "batch must be < 2^28 filters per launch");
     PEKF_CHECK_ARG(plane_gd && q_gyro, "null pointer");
     hipLaunchKernelGGL(k_gyro_chain, dim3(grid_for(batch, kSideBlock)), dim3(kSideBlock), 0,
                        as_stream(stream), batch, n_steps, window, step0,
@@ -117,6 +156,7 @@ int pekf_wahba_stream_dev(int64_t batch, int64_t n_steps, int64_t window, int64_
     PEKF_CHECK_ARG(batch >= 0 && n_steps >= 0, "negative size");
     if (batch == 0 || n_steps == 0) return PEKF_OK;
     PEKF_CHECK_ARG(window > 0 && step0 >= 0, "window must be > 0 and step0 >= 0");
+    PEKF_CHECK_ARG(batch < ((int64_t)1 << 28), "batch must be < 2^28 filters per launch");
     PEKF_CHECK_ARG(plane_am && plane_my && refs && out, "null pointer");
     hipLaunchKernelGGL(k_wahba_stream, dim3(grid_for(batch, kSideBlock)), dim3(kSideBlock), 0,
                        as_stream(stream), batch, n_steps, window, step0,

@@ -160,6 +160,18 @@ def test_set_state_roundtrip_and_resume(eng, oracle_c):
     assert _maxerr(f.get_state()[0], Xo) < PREC_GUARD
 
 
+@pytest.mark.parametrize("q,r", [(0.37, 2.5), (4.0, 0.01), (1e-3, 1.0)])
+def test_fused_run_other_noise_scales(eng, oracle_c, q, r):
+    """setQ(q) / setR(r) other than main_file.py's (1, 0.1): the fused algebra uses Q = qI, R = rI."""
+    K, W = 128, 300
+    rec = synth.generate(np.arange(K), W, seed=17, missing=True)
+    f = eng.BatchedEKF(K, q=q, r=r)
+    tr = f.run(eng.IMUWindow.from_records(rec), want_traj=True)
+    Xo, Po, to = oracle_c.run(rec, q=q, r=r, want_traj=True)
+    assert _maxerr(tr.transpose(1, 0, 2), to) < PREC_GUARD
+    assert _maxerr(f.get_state()[1], Po) < PREC_GUARD * max(1.0, r)
+
+
 def test_scale_c2_batch_sampled_against_oracle(eng, oracle_c):
     """Config-2 batch (65,536 filters) on a device-generated window; 64 sampled filters re-run on the host."""
     B, W, N = 65536, 128, 384
