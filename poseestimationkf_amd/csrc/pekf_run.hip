@@ -124,7 +124,7 @@ __device__ __forceinline__ void ekf_record_step(double *x, Sym4T<PT> &P, const F
 // in FP32 while RK4, Wahba, R->q and the X update stay FP64 (~2e-8 vs FP64).
 // COUNTS: filter b applies only its first counts[b] records of the launch (a separate
 // instantiation so the uniform-length path carries no per-step lane predicate).
-template <bool TRAJ, bool MIXED, bool SOA, bool COUNTS>
+template <bool TRAJ, bool MIXED, bool SOA, bool COUNTS, bool ONE>
 __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_steps, int64_t window,
                                                    int64_t step0, const float4 *__restrict__ gd,
                                                    const float4 *__restrict__ am,
@@ -183,9 +183,15 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     // Time loop, unrolled by two with ping-pong records: the next row's record is always in
     // flight while the current one is processed, and no registers are copied between steps.
     // The prefetch is unconditional (the row wraps inside the resident window, so it is always
-    // a valid address); n_steps >= 1 here.
+    // a valid address); n_steps >= 1 here.  One-record launches (online serving) use the ONE
+    // instantiation, which has no prefetch: there its 40 B would be an eighth of the traffic.
     int64_t row = step0 % window;
     Rec ra = load_row(row), rb;
+    if constexpr (ONE) {
+        step(ra, 0);
+        store_state<SOA>(Xio, Pio, b, batch, x, P);
+        return;
+    }
     for (int64_t t = 0;;) {
         row = row + 1 == window ? 0 : row + 1;
         rb = load_row(row);
@@ -307,9 +313,11 @@ int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
     const auto *am = static_cast<const float4 *>(plane_am);
     const auto *my = static_cast<const float2 *>(plane_my);
     const bool mixed = flags & PEKF_RUN_MIXED_PRECISION, soa = flags & PEKF_RUN_STATE_SOA;
-#define PEKF_LAUNCH_RUN(TR, MX, SO, CN)                                                                     \
-    hipLaunchKernelGGL((k_run<TR, MX, SO, CN>), grid, block, 0, as_stream(stream), batch, n_steps, window, \
+#define PEKF_LAUNCH_RUN0(TR, MX, SO, CN, ON)                                                                  \
+    hipLaunchKernelGGL((k_run<TR, MX, SO, CN, ON>), grid, block, 0, as_stream(stream), batch, n_steps, window, \
                        step0, gd, am, my, refs, X, P, q, r, traj, counts)
+#define PEKF_LAUNCH_RUN(TR, MX, SO, CN) \
+    do { if (n_steps == 1) PEKF_LAUNCH_RUN0(TR, MX, SO, CN, true); else PEKF_LAUNCH_RUN0(TR, MX, SO, CN, false); } while (0)
 #define PEKF_LAUNCH_RUN1(TR, MX, SO) \
     do { if (counts) PEKF_LAUNCH_RUN(TR, MX, SO, true); else PEKF_LAUNCH_RUN(TR, MX, SO, false); } while (0)
 #define PEKF_LAUNCH_RUN2(TR, MX) \
@@ -322,6 +330,7 @@ int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
 #undef PEKF_LAUNCH_RUN2
 #undef PEKF_LAUNCH_RUN1
 #undef PEKF_LAUNCH_RUN
+#undef PEKF_LAUNCH_RUN0
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_run");
     return PEKF_OK;
