@@ -27,9 +27,11 @@ __device__ __forceinline__ V3 widen(const F3 &f) { return {f.x, f.y, f.z}; }
 
 // Parser::LinearInterpolationSensor (:259-267): (y2 - y1) / (t2 - t1) * (t3 - t1) + y1, with the
 // division by (t2 - t1) taken once as a reciprocal (the emit path runs for the whole wave whenever
-// any lane emits a record, so its cost is paid on almost every event)
-__device__ __forceinline__ V3 lerp_to(int64_t t1, int64_t t2, int64_t t3, const V3 &a, const V3 &b) {
-    const double f = ((double)t3 - (double)t1) * recip<true>((double)t2 - (double)t1);
+// any lane emits a record, so its cost is paid on almost every event).  Timestamps are integer
+// nanoseconds held in doubles (exact below 2^53 ns), so t3 - t1 is the exact difference that
+// (double)t3 - (double)t1 gives, without int64 <-> double conversions.
+__device__ __forceinline__ V3 lerp_to(double t1, double t2, double t3, const V3 &a, const V3 &b) {
+    const double f = (t3 - t1) * recip<true>(t2 - t1);
     return {(b.x - a.x) * f + a.x, (b.y - a.y) * f + a.y, (b.z - a.z) * f + a.z};
 }
 
@@ -52,14 +54,15 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
     // phase-2 state: acc_0 / mag_0 = raw means at the initialisation time (Parser.cpp:44-53)
     V3 acc0 = {init[6 * b + 0], init[6 * b + 1], init[6 * b + 2]};
     V3 mag0 = {init[6 * b + 3], init[6 * b + 4], init[6 * b + 5]};
-    int64_t t_acc0 = t_init[b], t_mag0 = t_init[b], prev_t = t_init[b];
+    const double t_start = (double)t_init[b];
+    double t_acc0 = t_start, t_mag0 = t_start, prev_t = t_start;
     {   // the filter's reference vectors: normalised phase-2 means (Parser.cpp:48-49)
         const V3 a = normalised(acc0), m = normalised(mag0);
         refs[6 * b + 0] = a.x; refs[6 * b + 1] = a.y; refs[6 * b + 2] = a.z;
         refs[6 * b + 3] = m.x; refs[6 * b + 4] = m.y; refs[6 * b + 5] = m.z;
     }
     F3 acc1 = {0, 0, 0}, mag1 = {0, 0, 0}, gyro = {0, 0, 0};  // sensor samples: exact in f32
-    int64_t t_acc1 = 0, t_mag1 = 0, t_gyro = 0;
+    double t_acc1 = 0, t_mag1 = 0, t_gyro = 0;
     bool gyro_set = false, acc1_set = false, mag1_set = false;
     V3 lpf_acc = {0, 0, 0}, lpf_mag = {0, 0, 0};
     const double beta = 1.0 - alpha;
@@ -68,13 +71,13 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
     // the next event is loaded before the current one is processed; latency is covered by
     // occupancy (small register footprint)
     float4 nv4 = n_events > 0 ? ev[b] : make_float4(0.f, 0.f, 0.f, 0.f);
-    int64_t t = t_init[b];
+    double t = t_start;
     for (int64_t e = 0; e < n_events; ++e) {
         const float4 v4 = nv4;
         if (e + 1 < n_events) nv4 = ev[(e + 1) * batch + b];
         const uint32_t word = __float_as_uint(v4.w);
         const uint32_t ty = word & 3u;
-        t += (int64_t)(word >> 2);  // the event word carries the ns gap to the previous event
+        t += (double)(word >> 2);  // the event word carries the ns gap to the previous event
         const F3 v = {v4.x, v4.y, v4.z};
         if (!gyro_set) {
             if (ty == kEvAcc) { acc0 = widen(v); t_acc0 = t; }
@@ -96,12 +99,12 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
             const V3 m = normalised(lerp_to(t_mag0, t_mag1, t_gyro, mag0, widen(mag1)));
             lpf_mag = {alpha * m.x + beta * lpf_mag.x, alpha * m.y + beta * lpf_mag.y, alpha * m.z + beta * lpf_mag.z};
             lpf_acc = {alpha * a.x + beta * lpf_acc.x, alpha * a.y + beta * lpf_acc.y, alpha * a.z + beta * lpf_acc.z};
-            const int64_t dt = t_gyro - prev_t;
-            if (dt < 0 || dt >= ((int64_t)1 << 31)) bad |= 1;  // not representable in the 31-bit dt word
+            const double dt = t_gyro - prev_t;
+            if (!(dt >= 0.0 && dt < 2147483648.0)) bad |= 1;  // not representable in the 31-bit dt word
             if (r < r_max) {
                 const int64_t o = r * batch + b;
                 gd[o] = make_float4((float)gyro.x, (float)gyro.y, (float)gyro.z,
-                                    __uint_as_float((uint32_t)dt & 0x7FFFFFFFu));
+                                    __uint_as_float((uint32_t)fmin(fmax(dt, 0.0), 2147483647.0)));
                 am[o] = make_float4((float)lpf_acc.x, (float)lpf_acc.y, (float)lpf_acc.z, (float)lpf_mag.x);
                 my[o] = make_float2((float)lpf_mag.y, (float)lpf_mag.z);
             } else {
