@@ -61,19 +61,19 @@ SIGNATURES = {
     "pekf_event_record": [_vp, _vp],
     "pekf_event_sync": [_vp],
     "pekf_event_elapsed_ms": [ctypes.POINTER(ctypes.c_float), _vp, _vp],
-    "pekf_rk4": [_i64, _dp, _dp, _dp, _dp],
+    "pekf_rk4": [_i64, _vp, _vp, _vp, _vp],
     "pekf_rk4_dev": [_i64, _vp, _vp, _vp, _vp, _vp],
-    "pekf_norm": [_i64, _i64, _dp, _dp],
-    "pekf_jacobian_a": [_i64, _dp, _dp],
-    "pekf_jacobian_b": [_i64, _dp, _dp],
-    "pekf_comparator": [_i64, _dp, _dp, _dp],
-    "pekf_predict": [_i64] + [_dp] * 9,
+    "pekf_norm": [_i64, _i64, _vp, _vp],
+    "pekf_jacobian_a": [_i64, _vp, _vp],
+    "pekf_jacobian_b": [_i64, _vp, _vp],
+    "pekf_comparator": [_i64, _vp, _vp, _vp],
+    "pekf_predict": [_i64] + [_vp] * 9,
     "pekf_predict_dev": [_i64] + [_vp] * 9 + [_vp, _vp],
-    "pekf_correct": [_i64] + [_dp] * 9,
+    "pekf_correct": [_i64] + [_vp] * 9,
     "pekf_correct_dev": [_i64] + [_vp] * 9 + [_vp],
-    "pekf_wahba_rotation": [_i64] + [_dp] * 7,
-    "pekf_wahba_quaternion": [_i64] + [_dp] * 7,
-    "pekf_rotmat_to_quat": [_i64, _dp, _dp],
+    "pekf_wahba_rotation": [_i64] + [_vp] * 7,
+    "pekf_wahba_quaternion": [_i64] + [_vp] * 7,
+    "pekf_rotmat_to_quat": [_i64, _vp, _vp],
     "pekf_run_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp, _u32, _vp],
     "pekf_reset_state_dev": [_i64, _vp, _vp, _vp],
     "pekf_state_layout_dev": [_i64, _vp, _vp, _vp, _vp, _int, _vp],
@@ -88,7 +88,7 @@ SIGNATURES = {
     "pekf_filter_run": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "pekf_gyro_chain_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "pekf_wahba_stream_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp],
-    "pekf_quat_to_rpy": [_i64, _dp, _dp],
+    "pekf_quat_to_rpy": [_i64, _vp, _vp],
     "pekf_frontend_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "pekf_log_scan": [ctypes.c_char_p, ctypes.POINTER(_i64)],
     "pekf_log_read": [ctypes.c_char_p, _i64, _vp, _vp, _vp, _vp, _dp, _dp, _dp],

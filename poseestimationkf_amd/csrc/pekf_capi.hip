@@ -1,6 +1,7 @@
 // pekf_capi.hip -- host plumbing of the C ABI: error reporting, device / memory / stream /
 // event helpers (so the Python host needs no PyTorch), and the per-thread staging
 // workspace used by the host-pointer per-call entry points.
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -50,6 +51,11 @@ Staging::~Staging() {
 
 int Staging::reserve(size_t bytes) {
     if (!stream_) PEKF_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    if (!flag_) {
+        PEKF_HIP(hipHostMalloc(reinterpret_cast<void **>(&flag_), 256, hipHostMallocMapped | hipHostMallocCoherent));
+        PEKF_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&flag_dev_), flag_, 0));
+        __atomic_store_n(flag_, seq_, __ATOMIC_RELAXED);
+    }
     if (bytes <= cap_) return PEKF_OK;
     size_t cap = cap_ ? cap_ : (size_t)1 << 16;
     while (cap < bytes) cap *= 2;
@@ -92,7 +98,31 @@ int Staging::stage_in(std::initializer_list<HostArg> ins, std::initializer_list<
         off += align_up(b);
     }
     in_bytes_ = in_total;
+    signalled_ = false;
     if (!zero_copy_ && in_total) PEKF_HIP(hipMemcpyAsync(dev_, host_, in_total, hipMemcpyHostToDevice, stream_));
+    return PEKF_OK;
+}
+
+Done Staging::done(unsigned blocks) {
+    // only a zero-copy launch of ONE block can signal completion with one flag store
+    if (!zero_copy_ || blocks != 1 || !flag_dev_) return kNoSignal;
+    signalled_ = true;
+    return Done{flag_dev_, ++seq_};
+}
+
+// Wait for the launch since stage_in(): spin on the completion flag when the kernel signals,
+// falling back to hipStreamSynchronize (which also reports a faulted kernel) after 20 ms.
+int Staging::wait() {
+    if (signalled_) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned it = 0;; ++it) {
+            if (__atomic_load_n(flag_, __ATOMIC_ACQUIRE) == seq_) return PEKF_OK;
+            if ((it & 1023u) == 1023u &&
+                std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20))
+                break;
+        }
+    }
+    PEKF_HIP(hipStreamSynchronize(stream_));
     return PEKF_OK;
 }
 
@@ -103,7 +133,7 @@ int Staging::stage_out(std::initializer_list<HostOut> outs, void *const *dev_out
     if (total && !zero_copy_) {
         PEKF_HIP(hipMemcpyAsync(host_ + in_bytes_, dev_out[0], total, hipMemcpyDeviceToHost, stream_));
     }
-    PEKF_HIP(hipStreamSynchronize(stream_));
+    if (int st = wait()) return st;
     size_t off = in_bytes_;
     for (const HostOut &o : outs) {
         if (o.bytes) std::memcpy(o.ptr, host_ + off, o.bytes);

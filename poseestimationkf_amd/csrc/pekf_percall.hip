@@ -11,51 +11,74 @@ namespace pekf {
 
 constexpr int kBlock = 256;
 
-__global__ __launch_bounds__(kBlock) void k_rk4(int64_t n, const double *q0, const double *dt,
+__device__ __forceinline__ void d_rk4(int64_t i, const double *q0, const double *dt,
                                                const double *w, double *out) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
     rk4_literal(q0 + 4 * i, dt[i], w + 3 * i, out + 4 * i);
 }
 
-__global__ __launch_bounds__(kBlock) void k_norm(int64_t n, int64_t len, const double *a,
-                                                double *out) {
+__global__ __launch_bounds__(kBlock) void k_rk4(int64_t n, const double *q0, const double *dt,
+                                               const double *w, double *out, Done done) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
+    if (i < n) d_rk4(i, q0, dt, w, out);
+    done.signal();  // the whole block reaches this point (no early return)
+}
+
+__device__ __forceinline__ void d_norm(int64_t i, int64_t len, const double *a,
+                                                double *out) {
     double s = 0.0;
     for (int64_t k = 0; k < len; ++k) s += a[i * len + k] * a[i * len + k];
     out[i] = sqrt(s);
 }
 
-__global__ __launch_bounds__(kBlock) void k_jac_a(int64_t n, const double *w, double *A) {
+__global__ __launch_bounds__(kBlock) void k_norm(int64_t n, int64_t len, const double *a,
+                                                double *out, Done done) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) omega_half(w + 3 * i, A + 16 * i);
+    if (i < n) d_norm(i, len, a, out);
+    done.signal();  // the whole block reaches this point (no early return)
 }
 
-__global__ __launch_bounds__(kBlock) void k_jac_b(int64_t n, const double *q, double *J) {
+__device__ __forceinline__ void d_jac_a(int64_t i, const double *w, double *A) {
+    omega_half(w + 3 * i, A + 16 * i);
+}
+
+__global__ __launch_bounds__(kBlock) void k_jac_a(int64_t n, const double *w, double *A, Done done) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) xi_half(q + 4 * i, J + 12 * i);
+    if (i < n) d_jac_a(i, w, A);
+    done.signal();  // the whole block reaches this point (no early return)
+}
+
+__device__ __forceinline__ void d_jac_b(int64_t i, const double *q, double *J) {
+    xi_half(q + 4 * i, J + 12 * i);
+}
+
+__global__ __launch_bounds__(kBlock) void k_jac_b(int64_t n, const double *q, double *J, Done done) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) d_jac_b(i, q, J);
+    done.signal();  // the whole block reaches this point (no early return)
 }
 
 // conj(q1) (x) q2 as the reference's 4x4 left-multiplication (ExtendedKalmanFilter.py:16-23)
-__global__ __launch_bounds__(kBlock) void k_comparator(int64_t n, const double *q1,
+__device__ __forceinline__ void d_comparator(int64_t i, const double *q1,
                                                       const double *q2, double *out) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
     const double *a = q1 + 4 * i, *b = q2 + 4 * i;
     const double c0 = a[0], c1 = -a[1], c2 = -a[2], c3 = -a[3];
     const double L[16] = {c0, -c1, -c2, -c3, c1, c0, -c3, c2, c2, c3, c0, -c1, c3, -c2, c1, c0};
     matmul<4, 4, 1>(L, b, out + 4 * i);
 }
 
+__global__ __launch_bounds__(kBlock) void k_comparator(int64_t n, const double *q1,
+                                                      const double *q2, double *out, Done done) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) d_comparator(i, q1, q2, out);
+    done.signal();  // the whole block reaches this point (no early return)
+}
+
 // KalmanFilter.Prediction (ExtendedKalmanFilter.py:58-68)
-__global__ __launch_bounds__(kBlock) void k_predict(int64_t n, const double *gyro,
+__device__ __forceinline__ void d_predict(int64_t i, const double *gyro,
                                                    const double *dt, const double *X,
                                                    const double *P, const double *Q,
                                                    const double *R, double *z, double *Pm,
                                                    double *K, int32_t *status) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
     double A[16], At[16], Jb[12], Jbt[12], t16[16], a16[16], t12[12], b16[16], S[16], Si[16], pm[16];
     omega_half(gyro + 3 * i, A);
     xi_half(X + 4 * i, Jb);
@@ -82,14 +105,22 @@ __global__ __launch_bounds__(kBlock) void k_predict(int64_t n, const double *gyr
     matmul<4, 4, 4>(pm, Si, K + 16 * i);
 }
 
+__global__ __launch_bounds__(kBlock) void k_predict(int64_t n, const double *gyro,
+                                                   const double *dt, const double *X,
+                                                   const double *P, const double *Q,
+                                                   const double *R, double *z, double *Pm,
+                                                   double *K, int32_t *status, Done done) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) d_predict(i, gyro, dt, X, P, Q, R, z, Pm, K, status);
+    done.signal();  // the whole block reaches this point (no early return)
+}
+
 // KalmanFilter.Correction (ExtendedKalmanFilter.py:70-80)
-__global__ __launch_bounds__(kBlock) void k_correct(int64_t n, const double *mag,
+__device__ __forceinline__ void d_correct(int64_t i, const double *mag,
                                                    const double *acc, const double *z,
                                                    const double *P, const double *K,
                                                    const double *acc0, const double *mag0,
                                                    double *X, double *Pout, int32_t *status) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
     const double *a = acc + 3 * i, *zz = z + 4 * i, *kk = K + 16 * i, *pp = P + 16 * i;
     const double ka = fabs(a[2]);
     if (status) status[i] = wahba_b_finite(acc0 + 3 * i, mag0 + 3 * i, a, mag + 3 * i, ka, 1.0 - ka) ? 0 : 1;
@@ -114,13 +145,21 @@ __global__ __launch_bounds__(kBlock) void k_correct(int64_t n, const double *mag
     for (int k = 0; k < 4; ++k) X[4 * i + k] = x[k] / nrm;
 }
 
+__global__ __launch_bounds__(kBlock) void k_correct(int64_t n, const double *mag,
+                                                   const double *acc, const double *z,
+                                                   const double *P, const double *K,
+                                                   const double *acc0, const double *mag0,
+                                                   double *X, double *Pout, int32_t *status, Done done) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) d_correct(i, mag, acc, z, P, K, acc0, mag0, X, Pout, status);
+    done.signal();  // the whole block reaches this point (no early return)
+}
+
 template <bool QUAT>
-__global__ __launch_bounds__(kBlock) void k_wahba(int64_t n, const double *acc0,
+__device__ __forceinline__ void d_wahba(int64_t i, const double *acc0,
                                                  const double *mag0, const double *acc,
                                                  const double *mag, const double *ka,
                                                  const double *km, double *out, int32_t *status) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
     if (status)
         status[i] = wahba_b_finite(acc0 + 3 * i, mag0 + 3 * i, acc + 3 * i, mag + 3 * i, ka[i], km[i]) ? 0 : 1;
     double R[9];
@@ -133,9 +172,24 @@ __global__ __launch_bounds__(kBlock) void k_wahba(int64_t n, const double *acc0,
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_r2q(int64_t n, const double *M, double *q) {
+template <bool QUAT>
+__global__ __launch_bounds__(kBlock) void k_wahba(int64_t n, const double *acc0,
+                                                 const double *mag0, const double *acc,
+                                                 const double *mag, const double *ka,
+                                                 const double *km, double *out, int32_t *status, Done done) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) rotm_to_quat(M + 9 * i, q + 4 * i);
+    if (i < n) d_wahba<QUAT>(i, acc0, mag0, acc, mag, ka, km, out, status);
+    done.signal();  // the whole block reaches this point (no early return)
+}
+
+__device__ __forceinline__ void d_r2q(int64_t i, const double *M, double *q) {
+    rotm_to_quat(M + 9 * i, q + 4 * i);
+}
+
+__global__ __launch_bounds__(kBlock) void k_r2q(int64_t n, const double *M, double *q, Done done) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) d_r2q(i, M, q);
+    done.signal();  // the whole block reaches this point (no early return)
 }
 
 static int launched(const char *what) {
@@ -160,7 +214,7 @@ int pekf_rk4_dev(int64_t n, const double *q0, const double *dt_ns, const double 
     PEKF_CHECK_ARG(n >= 0, "n < 0");
     if (n == 0) return PEKF_OK;
     PEKF_CHECK_ARG(q0 && dt_ns && w && q_out, "null pointer");
-    hipLaunchKernelGGL(k_rk4, PEKF_GRID(n), 0, as_stream(stream), n, q0, dt_ns, w, q_out);
+    hipLaunchKernelGGL(k_rk4, PEKF_GRID(n), 0, as_stream(stream), n, q0, dt_ns, w, q_out, kNoSignal);
     return launched("k_rk4");
 }
 
@@ -171,7 +225,7 @@ int pekf_predict_dev(int64_t n, const double *gyro, const double *dt_ns, const d
     if (n == 0) return PEKF_OK;
     PEKF_CHECK_ARG(gyro && dt_ns && X && P && Q && R && z && Pm && K, "null pointer");
     hipLaunchKernelGGL(k_predict, PEKF_GRID(n), 0, as_stream(stream), n, gyro, dt_ns, X, P, Q, R,
-                       z, Pm, K, status);
+                       z, Pm, K, status, kNoSignal);
     return launched("k_predict");
 }
 
@@ -182,7 +236,7 @@ int pekf_correct_dev(int64_t n, const double *mag, const double *acc, const doub
     if (n == 0) return PEKF_OK;
     PEKF_CHECK_ARG(mag && acc && z && P && K && acc0 && mag0 && X && P_out, "null pointer");
     hipLaunchKernelGGL(k_correct, PEKF_GRID(n), 0, as_stream(stream), n, mag, acc, z, P, K, acc0,
-                       mag0, X, P_out, nullptr);
+                       mag0, X, P_out, nullptr, kNoSignal);
     return launched("k_correct");
 }
 
@@ -198,7 +252,7 @@ int pekf_rk4(int64_t n, const double *q0, const double *dt_ns, const double *w, 
     void *in[3], *out[1];
     if (int st = s.stage_in({{q0, 4 * b}, {dt_ns, b}, {w, 3 * b}}, {4 * b}, in, out)) return st;
     hipLaunchKernelGGL(k_rk4, PEKF_GRID(n), 0, s.stream(), n, D(const double *, in[0]),
-                       D(const double *, in[1]), D(const double *, in[2]), D(double *, out[0]));
+                       D(const double *, in[1]), D(const double *, in[2]), D(double *, out[0]), s.done(grid_for(n, kBlock)));
     if (int st = launched("k_rk4")) return st;
     return s.stage_out({{q_out, 4 * b}}, out);
 }
@@ -213,7 +267,7 @@ int pekf_norm(int64_t n, int64_t len, const double *a, double *res) {
     void *in[1], *out[1];
     if (int st = s.stage_in({{a, (size_t)len * b}}, {b}, in, out)) return st;
     hipLaunchKernelGGL(k_norm, PEKF_GRID(n), 0, s.stream(), n, len, D(const double *, in[0]),
-                       D(double *, out[0]));
+                       D(double *, out[0]), s.done(grid_for(n, kBlock)));
     if (int st = launched("k_norm")) return st;
     return s.stage_out({{res, b}}, out);
 }
@@ -228,7 +282,7 @@ int pekf_jacobian_a(int64_t n, const double *w, double *A) {
     void *in[1], *out[1];
     if (int st = s.stage_in({{w, 3 * b}}, {16 * b}, in, out)) return st;
     hipLaunchKernelGGL(k_jac_a, PEKF_GRID(n), 0, s.stream(), n, D(const double *, in[0]),
-                       D(double *, out[0]));
+                       D(double *, out[0]), s.done(grid_for(n, kBlock)));
     if (int st = launched("k_jac_a")) return st;
     return s.stage_out({{A, 16 * b}}, out);
 }
@@ -243,7 +297,7 @@ int pekf_jacobian_b(int64_t n, const double *q, double *Jb) {
     void *in[1], *out[1];
     if (int st = s.stage_in({{q, 4 * b}}, {12 * b}, in, out)) return st;
     hipLaunchKernelGGL(k_jac_b, PEKF_GRID(n), 0, s.stream(), n, D(const double *, in[0]),
-                       D(double *, out[0]));
+                       D(double *, out[0]), s.done(grid_for(n, kBlock)));
     if (int st = launched("k_jac_b")) return st;
     return s.stage_out({{Jb, 12 * b}}, out);
 }
@@ -258,7 +312,7 @@ int pekf_comparator(int64_t n, const double *q1, const double *q2, double *res) 
     void *in[2], *out[1];
     if (int st = s.stage_in({{q1, 4 * b}, {q2, 4 * b}}, {4 * b}, in, out)) return st;
     hipLaunchKernelGGL(k_comparator, PEKF_GRID(n), 0, s.stream(), n, D(const double *, in[0]),
-                       D(const double *, in[1]), D(double *, out[0]));
+                       D(const double *, in[1]), D(double *, out[0]), s.done(grid_for(n, kBlock)));
     if (int st = launched("k_comparator")) return st;
     return s.stage_out({{res, 4 * b}}, out);
 }
@@ -281,7 +335,7 @@ int pekf_predict(int64_t n, const double *gyro, const double *dt_ns, const doubl
     hipLaunchKernelGGL(k_predict, PEKF_GRID(n), 0, s.stream(), n, D(const double *, in[0]),
                        D(const double *, in[1]), D(const double *, in[2]), D(const double *, in[3]),
                        D(const double *, in[4]), D(const double *, in[5]), D(double *, out[0]),
-                       D(double *, out[1]), D(double *, out[2]), D(int32_t *, out[3]));
+                       D(double *, out[1]), D(double *, out[2]), D(int32_t *, out[3]), s.done(grid_for(n, kBlock)));
     if (int st = launched("k_predict")) return st;
     if (int st = s.stage_out({{z, 4 * b}, {Pm, 16 * b}, {K, 16 * b}, {status.data(), sb}}, out)) return st;
     for (int32_t v : status)
@@ -308,7 +362,7 @@ int pekf_correct(int64_t n, const double *mag, const double *acc, const double *
     hipLaunchKernelGGL(k_correct, PEKF_GRID(n), 0, s.stream(), n, D(const double *, in[0]),
                        D(const double *, in[1]), D(const double *, in[2]), D(const double *, in[3]),
                        D(const double *, in[4]), D(const double *, in[5]), D(const double *, in[6]),
-                       D(double *, out[0]), D(double *, out[1]), D(int32_t *, out[2]));
+                       D(double *, out[0]), D(double *, out[1]), D(int32_t *, out[2]), s.done(grid_for(n, kBlock)));
     if (int st = launched("k_correct")) return st;
     if (int st = s.stage_out({{X, 4 * b}, {P_out, 16 * b}, {status.data(), sb}}, out)) return st;
     for (int32_t v : status)
@@ -336,12 +390,12 @@ static int wahba_host(bool quat, int64_t n, const double *acc0, const double *ma
         hipLaunchKernelGGL(k_wahba<true>, PEKF_GRID(n), 0, s.stream(), n, D(const double *, in[0]),
                            D(const double *, in[1]), D(const double *, in[2]), D(const double *, in[3]),
                            D(const double *, in[4]), D(const double *, in[5]), D(double *, out[0]),
-                           D(int32_t *, out[1]));
+                           D(int32_t *, out[1]), s.done(grid_for(n, kBlock)));
     else
         hipLaunchKernelGGL(k_wahba<false>, PEKF_GRID(n), 0, s.stream(), n, D(const double *, in[0]),
                            D(const double *, in[1]), D(const double *, in[2]), D(const double *, in[3]),
                            D(const double *, in[4]), D(const double *, in[5]), D(double *, out[0]),
-                           D(int32_t *, out[1]));
+                           D(int32_t *, out[1]), s.done(grid_for(n, kBlock)));
     if (int st = launched("k_wahba")) return st;
     if (int st = s.stage_out({{res, ob}, {status.data(), sb}}, out)) return st;
     for (int32_t v : status)
@@ -369,7 +423,7 @@ int pekf_rotmat_to_quat(int64_t n, const double *M, double *q) {
     void *in[1], *out[1];
     if (int st = s.stage_in({{M, 9 * b}}, {4 * b}, in, out)) return st;
     hipLaunchKernelGGL(k_r2q, PEKF_GRID(n), 0, s.stream(), n, D(const double *, in[0]),
-                       D(double *, out[0]));
+                       D(double *, out[0]), s.done(grid_for(n, kBlock)));
     if (int st = launched("k_r2q")) return st;
     return s.stage_out({{q, 4 * b}}, out);
 }

@@ -108,11 +108,8 @@ __global__ __launch_bounds__(kSideBlock) void k_wahba_stream(int64_t batch, int6
 
 // UtilityFunctions.Quart2RPY: roll = atan2(2(q0q1+q2q3), 1-2(q1^2+q2^2)), pitch = asin(2(q0q2-q3q1)),
 // yaw = atan2(2(q0q3+q1q2), 1-2(q2^2+q3^2)), times 180/pi
-__global__ __launch_bounds__(kSideBlock) void k_rpy(int64_t n, const double *__restrict__ q,
-                                                    double *__restrict__ rpy) {
+__device__ __forceinline__ void d_rpy(int64_t i, const double *__restrict__ q, double *__restrict__ rpy) {
 #pragma clang fp contract(off)  // round like NumPy: at gimbal lock sinp may round past 1 -> NaN there too
-    const int64_t i = (int64_t)blockIdx.x * kSideBlock + threadIdx.x;
-    if (i >= n) return;
     const double *p = q + 4 * i;
     const double sinr = 2 * (p[0] * p[1] + p[2] * p[3]);
     const double cosr = 1 - 2 * (p[1] * p[1] + p[2] * p[2]);
@@ -123,6 +120,13 @@ __global__ __launch_bounds__(kSideBlock) void k_rpy(int64_t n, const double *__r
     rpy[3 * i + 0] = atan2(sinr, cosr) * k;
     rpy[3 * i + 1] = asin(sinp) * k;
     rpy[3 * i + 2] = atan2(siny, cosy) * k;
+}
+
+__global__ __launch_bounds__(kSideBlock) void k_rpy(int64_t n, const double *__restrict__ q,
+                                                    double *__restrict__ rpy, Done done) {
+    const int64_t i = (int64_t)blockIdx.x * kSideBlock + threadIdx.x;
+    if (i < n) d_rpy(i, q, rpy);
+    done.signal();
 }
 
 static int launched(const char *what) {
@@ -170,7 +174,7 @@ int pekf_quat_to_rpy_dev(int64_t n, const double *q, double *rpy, void *stream) 
     if (n == 0) return PEKF_OK;
     PEKF_CHECK_ARG(q && rpy, "null pointer");
     hipLaunchKernelGGL(k_rpy, dim3(grid_for(n, kSideBlock)), dim3(kSideBlock), 0, as_stream(stream), n,
-                       q, rpy);
+                       q, rpy, kNoSignal);
     return launched("k_rpy");
 }
 
@@ -184,7 +188,8 @@ int pekf_quat_to_rpy(int64_t n, const double *q, double *rpy) {
     void *in[1], *out[1];
     if (int st = s.stage_in({{q, 4 * b}}, {3 * b}, in, out)) return st;
     hipLaunchKernelGGL(k_rpy, dim3(grid_for(n, kSideBlock)), dim3(kSideBlock), 0, s.stream(), n,
-                       static_cast<const double *>(in[0]), static_cast<double *>(out[0]));
+                       static_cast<const double *>(in[0]), static_cast<double *>(out[0]),
+                       s.done(grid_for(n, kSideBlock)));
     if (int st = launched("k_rpy")) return st;
     return s.stage_out({{rpy, 3 * b}}, out);
 }

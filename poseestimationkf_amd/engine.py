@@ -428,77 +428,85 @@ class FilterHandle:
 # ------------------------------------------------------------------ batched per-call operators
 # NumPy-level wrappers over the host-pointer entry points (one GPU thread per item).
 
+def _in(a, shape):
+    """Read-only C-contiguous float64 view of an input (copied only if it is not one already):
+    the host-pointer entry points never write their inputs."""
+    return np.ascontiguousarray(a, dtype=np.float64).reshape(shape)
+
+
 def _n(a, k):
-    a = np.asarray(a, dtype=np.float64)
-    return a.size // k
+    return np.size(a) // k
+
+
+def _p(a):
+    return a.ctypes.data
 
 
 def rk4(q0, dt_ns, w):
     n = _n(q0, 4)
-    q0, dt, w = f64(q0, (n, 4)), f64(dt_ns, (n,)), f64(w, (n, 3))
+    q0, dt, w = _in(q0, (n, 4)), _in(dt_ns, (n,)), _in(w, (n, 3))
     out = np.empty((n, 4))
-    check(lib.pekf_rk4(n, dptr(q0), dptr(dt), dptr(w), dptr(out)))
+    check(lib.pekf_rk4(n, _p(q0), _p(dt), _p(w), _p(out)))
     return out
 
 
 def norm(a):
     """Row norms of a (n, len) array, sequential sum of squares (UtilityFunctions.py:16-21)."""
-    a = np.atleast_2d(np.asarray(a, dtype=np.float64))
+    a = np.atleast_2d(np.ascontiguousarray(a, dtype=np.float64))
     n, k = a.shape
-    a = f64(a, (n, k))
     out = np.empty(n)
-    check(lib.pekf_norm(n, k, dptr(a), dptr(out)))
+    check(lib.pekf_norm(n, k, _p(a), _p(out)))
     return out
 
 
 def jacobian_a(w):
     n = _n(w, 3)
-    w = f64(w, (n, 3))
+    w = _in(w, (n, 3))
     out = np.empty((n, 4, 4))
-    check(lib.pekf_jacobian_a(n, dptr(w), dptr(out)))
+    check(lib.pekf_jacobian_a(n, _p(w), _p(out)))
     return out
 
 
 def jacobian_b(q):
     n = _n(q, 4)
-    q = f64(q, (n, 4))
+    q = _in(q, (n, 4))
     out = np.empty((n, 4, 3))
-    check(lib.pekf_jacobian_b(n, dptr(q), dptr(out)))
+    check(lib.pekf_jacobian_b(n, _p(q), _p(out)))
     return out
 
 
 def comparator(q1, q2):
     n = _n(q1, 4)
-    a, b = f64(q1, (n, 4)), f64(q2, (n, 4))
+    a, b = _in(q1, (n, 4)), _in(q2, (n, 4))
     out = np.empty((n, 4))
-    check(lib.pekf_comparator(n, dptr(a), dptr(b), dptr(out)))
+    check(lib.pekf_comparator(n, _p(a), _p(b), _p(out)))
     return out
 
 
 def predict(gyro, dt_ns, X, P, Q, R):
     n = _n(X, 4)
-    args = [f64(gyro, (n, 3)), f64(dt_ns, (n,)), f64(X, (n, 4)), f64(P, (n, 4, 4)),
-            f64(Q, (n, 3, 3)), f64(R, (n, 4, 4))]
+    args = (_in(gyro, (n, 3)), _in(dt_ns, (n,)), _in(X, (n, 4)), _in(P, (n, 4, 4)),
+            _in(Q, (n, 3, 3)), _in(R, (n, 4, 4)))
     z, Pm, K = np.empty((n, 4)), np.empty((n, 4, 4)), np.empty((n, 4, 4))
-    check(lib.pekf_predict(n, *[dptr(a) for a in args], dptr(z), dptr(Pm), dptr(K)))
+    check(lib.pekf_predict(n, *[_p(a) for a in args], _p(z), _p(Pm), _p(K)))
     return z, Pm, K
 
 
 def correct(mag, acc, z, P, K, acc0, mag0):
     n = _n(z, 4)
-    args = [f64(mag, (n, 3)), f64(acc, (n, 3)), f64(z, (n, 4)), f64(P, (n, 4, 4)), f64(K, (n, 4, 4)),
-            f64(acc0, (n, 3)), f64(mag0, (n, 3))]
+    args = (_in(mag, (n, 3)), _in(acc, (n, 3)), _in(z, (n, 4)), _in(P, (n, 4, 4)), _in(K, (n, 4, 4)),
+            _in(acc0, (n, 3)), _in(mag0, (n, 3)))
     X, Po = np.empty((n, 4)), np.empty((n, 4, 4))
-    check(lib.pekf_correct(n, *[dptr(a) for a in args], dptr(X), dptr(Po)))
+    check(lib.pekf_correct(n, *[_p(a) for a in args], _p(X), _p(Po)))
     return X, Po
 
 
 def _wahba(fn, k, acc0, mag0, acc, mag, k_acc, k_mag):
     n = _n(acc, 3)
-    args = [f64(acc0, (n, 3)), f64(mag0, (n, 3)), f64(acc, (n, 3)), f64(mag, (n, 3)),
-            f64(k_acc, (n,)), f64(k_mag, (n,))]
+    args = (_in(acc0, (n, 3)), _in(mag0, (n, 3)), _in(acc, (n, 3)), _in(mag, (n, 3)),
+            _in(k_acc, (n,)), _in(k_mag, (n,)))
     out = np.empty((n,) + k)
-    check(fn(n, *[dptr(a) for a in args], dptr(out)))
+    check(fn(n, *[_p(a) for a in args], _p(out)))
     return out
 
 
@@ -513,15 +521,15 @@ def wahba_quaternion(acc0, mag0, acc, mag, k_acc, k_mag):
 def quat_to_rpy(q):
     """UtilityFunctions.Quart2RPY for each row of q (n,4): roll, pitch, yaw in degrees."""
     n = _n(q, 4)
-    q = f64(q, (n, 4))
+    q = _in(q, (n, 4))
     out = np.empty((n, 3))
-    check(lib.pekf_quat_to_rpy(n, dptr(q), dptr(out)))
+    check(lib.pekf_quat_to_rpy(n, _p(q), _p(out)))
     return out
 
 
 def rotmat_to_quat(M):
     n = _n(M, 9)
-    M = f64(M, (n, 3, 3))
+    M = _in(M, (n, 3, 3))
     out = np.empty((n, 4))
-    check(lib.pekf_rotmat_to_quat(n, dptr(M), dptr(out)))
+    check(lib.pekf_rotmat_to_quat(n, _p(M), _p(out)))
     return out
