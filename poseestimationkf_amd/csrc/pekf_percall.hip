@@ -2,6 +2,7 @@
 //
 // These keep the reference's dense formulation (ExtendedKalmanFilter.py, Wahba.py) so
 // each call matches NumPy to rounding; the fused time-loop kernel is pekf_run.hip.
+#include <cstring>
 #include <vector>
 
 #include "pekf_internal.hpp"
@@ -192,6 +193,32 @@ __global__ __launch_bounds__(kBlock) void k_r2q(int64_t n, const double *M, doub
     done.signal();  // the whole block reaches this point (no early return)
 }
 
+// n = 1 calls (what main_file.py makes, one record at a time): the inputs travel by value in the
+// kernel-argument segment with the dispatch itself instead of being read over PCIe from pinned
+// host memory, so the kernel starts with its operands in hand.  The body is the same device
+// function as the batched kernel, on a private copy (promoted to registers after inlining).
+constexpr int kBlobDoubles = 64;
+struct Blob {
+    double v[kBlobDoubles];
+};
+enum : int { kCallPredict = 0, kCallCorrect = 1, kCallWahbaQuat = 2 };
+
+template <int OP>
+__global__ __launch_bounds__(64) void k_call1(Blob b, double *out, int32_t *status, Done done) {
+    if (threadIdx.x == 0) {
+        double v[kBlobDoubles];
+#pragma unroll
+        for (int k = 0; k < kBlobDoubles; ++k) v[k] = b.v[k];
+        if (OP == kCallPredict)  // gyro 3, dt 1, X 4, P 16, Q 9, R 16 -> z 4, Pm 16, K 16
+            d_predict(0, v, v + 3, v + 4, v + 8, v + 24, v + 33, out, out + 4, out + 20, status);
+        else if (OP == kCallCorrect)  // mag 3, acc 3, z 4, P 16, K 16, acc0 3, mag0 3 -> X 4, P 16
+            d_correct(0, v, v + 3, v + 6, v + 10, v + 26, v + 42, v + 45, out, out + 4, status);
+        else  // acc0 3, mag0 3, acc 3, mag 3, ka 1, km 1 -> q 4
+            d_wahba<true>(0, v, v + 3, v + 6, v + 9, v + 12, v + 13, out, status);
+    }
+    done.signal();
+}
+
 static int launched(const char *what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, what);
@@ -199,6 +226,35 @@ static int launched(const char *what) {
 }
 
 #define PEKF_GRID(n) dim3(grid_for((n), kBlock)), dim3(kBlock)
+
+// Host side of k_call1: packs the inputs (in order) into the Blob, runs the call with zero-copy
+// outputs and returns them (in order) plus the status word.
+template <int OP>
+static int call1(std::initializer_list<HostArg> ins, std::initializer_list<HostOut> outs, int32_t *status) {
+    Blob b;
+    size_t off = 0;
+    for (const HostArg &a : ins) {
+        std::memcpy(reinterpret_cast<char *>(b.v) + off, a.ptr, a.bytes);
+        off += a.bytes;
+    }
+    size_t ob = 0;
+    for (const HostOut &o : outs) ob += o.bytes;
+    double tmp[kBlobDoubles];
+    Staging &s = Staging::get();
+    void *out[2];
+    if (int st = s.stage_in({}, {ob, sizeof(int32_t)}, nullptr, out)) return st;
+    hipLaunchKernelGGL(k_call1<OP>, dim3(1), dim3(64), 0, s.stream(), b, static_cast<double *>(out[0]),
+                       static_cast<int32_t *>(out[1]), s.done(1));
+    if (int st = launched("k_call1")) return st;
+    if (int st = s.stage_out({{tmp, ob}, {status, sizeof(int32_t)}}, out)) return st;
+    off = 0;
+    for (const HostOut &o : outs) {
+        std::memcpy(o.ptr, reinterpret_cast<char *>(tmp) + off, o.bytes);
+        off += o.bytes;
+    }
+    return PEKF_OK;
+}
+
 #define D(T, p) static_cast<T>(p)
 
 }  // namespace pekf
@@ -324,8 +380,15 @@ int pekf_predict(int64_t n, const double *gyro, const double *dt_ns, const doubl
     if (n == 0) return PEKF_OK;
     PEKF_CHECK_ARG(gyro && dt_ns && X && P && Q && R && z && Pm && K, "null pointer");
     if (int st = require_device()) return st;
-    Staging &s = Staging::get();
     const size_t b = (size_t)n * sizeof(double);
+    if (n == 1) {
+        int32_t st1 = 0;
+        if (int st = call1<kCallPredict>({{gyro, 3 * b}, {dt_ns, b}, {X, 4 * b}, {P, 16 * b}, {Q, 9 * b}, {R, 16 * b}},
+                                         {{z, 4 * b}, {Pm, 16 * b}, {K, 16 * b}}, &st1))
+            return st;
+        return st1 ? set_error(PEKF_ERR_SINGULAR, "Singular matrix") : PEKF_OK;
+    }
+    Staging &s = Staging::get();
     const size_t sb = (size_t)n * sizeof(int32_t);
     std::vector<int32_t> status((size_t)n);
     void *in[6], *out[4];
@@ -350,8 +413,16 @@ int pekf_correct(int64_t n, const double *mag, const double *acc, const double *
     if (n == 0) return PEKF_OK;
     PEKF_CHECK_ARG(mag && acc && z && P && K && acc0 && mag0 && X && P_out, "null pointer");
     if (int st = require_device()) return st;
-    Staging &s = Staging::get();
     const size_t b = (size_t)n * sizeof(double);
+    if (n == 1) {
+        int32_t st1 = 0;
+        if (int st = call1<kCallCorrect>({{mag, 3 * b}, {acc, 3 * b}, {z, 4 * b}, {P, 16 * b}, {K, 16 * b},
+                                          {acc0, 3 * b}, {mag0, 3 * b}},
+                                         {{X, 4 * b}, {P_out, 16 * b}}, &st1))
+            return st;
+        return st1 ? set_error(PEKF_ERR_SVD, "SVD did not converge") : PEKF_OK;
+    }
+    Staging &s = Staging::get();
     const size_t sb = (size_t)n * sizeof(int32_t);
     std::vector<int32_t> status((size_t)n);
     void *in[7], *out[3];
@@ -377,8 +448,16 @@ static int wahba_host(bool quat, int64_t n, const double *acc0, const double *ma
     if (n == 0) return PEKF_OK;
     PEKF_CHECK_ARG(acc0 && mag0 && acc && mag && k_acc && k_mag && res, "null pointer");
     if (int st = require_device()) return st;
-    Staging &s = Staging::get();
     const size_t b = (size_t)n * sizeof(double);
+    if (n == 1 && quat) {
+        int32_t st1 = 0;
+        if (int st = call1<kCallWahbaQuat>({{acc0, 3 * b}, {mag0, 3 * b}, {acc, 3 * b}, {mag, 3 * b}, {k_acc, b},
+                                            {k_mag, b}},
+                                           {{res, 4 * b}}, &st1))
+            return st;
+        return st1 ? set_error(PEKF_ERR_SVD, "SVD did not converge") : PEKF_OK;
+    }
+    Staging &s = Staging::get();
     const size_t ob = (quat ? 4 : 9) * b;
     const size_t sb = (size_t)n * sizeof(int32_t);
     std::vector<int32_t> status((size_t)n);

@@ -4,11 +4,13 @@
 eps), methods and return tuples, so ``main_file.py`` runs unchanged against it.  X, P, z
 and K are caller-owned values: every call returns fresh arrays and never mutates its
 inputs (main_file.py:39-44 keeps the returned X in a list).  The arithmetic runs in the
-per-call gfx950 kernels of libpekf.so (k_predict, k_correct, k_rk4, ...).  For many
+per-call gfx950 kernels of libpekf.so (k_predict, k_correct, k_rk4, ...); the two per-record
+methods go through the CPython binding ``_fastcall`` (same C entry points, less call overhead).  For many
 filters at once use ``poseestimationkf_amd.engine.BatchedEKF`` (the fused kernel).
 """
 import numpy as np
 from _bootstrap import engine as _eng
+from _bootstrap import fastcall as _fc
 from Wahba import Wahba
 
 
@@ -41,10 +43,9 @@ class KalmanFilter:
 
     def Prediction(self, Gyro, T, X_k, P_k):             # :58-68
         dt = T - self.previousT                          # same float64 op as :62
-        z, P, K = _eng.predict(Gyro, dt, X_k, P_k, self.Q, self.R)   # LinAlgError if S singular
+        z, P, K = _fc.predict(Gyro, dt, X_k, P_k, self.Q, self.R)    # LinAlgError if S singular
         self.previousT = T                               # :67, only after a successful step
-        return z[0], P[0], K[0]
+        return z, P, K
 
     def Correction(self, Mag, Acc, z_k, P_k, K_k):       # :70-80
-        X, P = _eng.correct(Mag, Acc, z_k, P_k, K_k, self.wahba.w_initial_acc, self.wahba.w_initial_mag)
-        return X[0], P[0]
+        return _fc.correct(Mag, Acc, z_k, P_k, K_k, self.wahba.w_initial_acc, self.wahba.w_initial_mag)

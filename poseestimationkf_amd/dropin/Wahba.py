@@ -6,6 +6,7 @@ attitude profile matrix is replaced by its closed form (DESIGN.md "Wahba closed 
 the rotation is unique, so results agree with np.linalg.svd to rounding.
 """
 from _bootstrap import engine as _eng
+from _bootstrap import fastcall as _fc
 
 
 class Wahba:
@@ -21,4 +22,4 @@ class Wahba:
         return _eng.rotmat_to_quat(M)[0]
 
     def getQuarternion(self, acc, mag, k_acc, k_mag):   # Wahba.py:49-50
-        return _eng.wahba_quaternion(self.w_initial_acc, self.w_initial_mag, acc, mag, k_acc, k_mag)[0]
+        return _fc.wahba_quaternion(self.w_initial_acc, self.w_initial_mag, acc, mag, k_acc, k_mag)

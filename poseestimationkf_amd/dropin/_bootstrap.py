@@ -12,3 +12,4 @@ if _ROOT not in sys.path:
     sys.path.append(_ROOT)
 
 from poseestimationkf_amd import engine  # noqa: E402,F401
+from poseestimationkf_amd import _fastcall as fastcall  # noqa: E402,F401  (n = 1 calls, CPython binding)

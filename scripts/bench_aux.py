@@ -7,7 +7,9 @@
   wahba_stream  pekf_wahba_stream_dev (§8f-3): 24 B read + 32 B written per filter-record
   predict_dev / correct_dev   per-call operators at n = 1M items (device pointers)
   online_step_aos / _soa   1M filters x 1 record per launch (state through HBM every launch)
-  dropin_call   host-pointer per-call latency at n = 1 (the path main_file.py takes)
+  ctypes_call / dropin_call   host-pointer per-call latency at n = 1 via ctypes / via the CPython
+                binding the drop-in modules use (the path main_file.py takes)
+  c1_loop       config 1: main_file.py's loop over the committed log, drop-ins vs NumPy on the host
 
 Kernel times are HIP events on the launch stream; run under rocprofv3 --kernel-trace --stats
 for the per-kernel summary committed in profiles/.
@@ -46,6 +48,62 @@ def timed(fn, stream, reps=3):
         e1.sync()
         out.append(e0.elapsed_ms(e1))
     return float(np.median(out))
+
+
+def c1_loop():
+    """Config 1: main_file.py:38-46 over the committed 1,550-record log, once through the drop-in
+    modules (GPU per-call kernels) and once through oracle/ekf_numpy.py (the NumPy restatement,
+    bit-identical to the reference) on this host's CPU: microseconds per record."""
+    import gzip
+    import importlib
+    import tempfile
+    from oracle import ekf_numpy as npo
+    golden = os.path.join(ROOT, "tests", "golden")
+    with gzip.open(os.path.join(golden, "c1_log.txt.gz"), "rt") as fh:
+        text = fh.read()
+    with tempfile.NamedTemporaryFile("w", suffix=".txt", delete=False) as fh:
+        fh.write(text)
+    os.environ["PEKF_LOG_PATH"] = fh.name
+    sys.path.insert(0, os.path.join(ROOT, "poseestimationkf_amd", "dropin"))
+    ReadFile = importlib.import_module("ReadFile")
+    EKF = importlib.import_module("ExtendedKalmanFilter")
+    Wahba = importlib.import_module("Wahba")
+    g = ReadFile.getData()
+    os.unlink(fh.name)
+    T = [t[0] for t in g.timestamp]
+    n = len(g.acc_1)
+
+    def dropin():
+        w = Wahba.Wahba(g.acc_0, g.mag_0)
+        k = EKF.KalmanFilter(T[0], g.mag_0, g.acc_0, 0.5)
+        k.setQ(1)
+        k.setR(0.1)
+        X, P = np.asarray([1., 0., 0., 0.]), np.identity(4)
+        for i in range(n):
+            z, P, K = k.Prediction(g.gyro[i], T[i + 1], X, P)
+            w.getQuarternion(g.acc_1[i], g.mag_1[i], 0.5, 0.5)
+            X, P = k.Correction(g.mag_1[i], g.acc_1[i], z, P, K)
+        return X
+
+    def numpy_port():
+        Q, R = np.identity(3), np.identity(4) * 0.1
+        X, P, prev = np.asarray([1., 0., 0., 0.]), np.identity(4), T[0]
+        a0, m0 = np.asarray(g.acc_0, float), np.asarray(g.mag_0, float)
+        for i in range(n):
+            z, P, K = npo.predict(np.asarray(g.gyro[i], float), T[i + 1] - prev, X, P, Q, R)
+            prev = T[i + 1]
+            npo.wahba_quat(a0, m0, np.asarray(g.acc_1[i], float), np.asarray(g.mag_1[i], float), 0.5, 0.5)
+            X, P = npo.correct(np.asarray(g.mag_1[i], float), np.asarray(g.acc_1[i], float), z, P, K, a0, m0)
+        return X
+
+    out = {"records": n}
+    for name, fn in (("dropin_gpu_us_per_record", dropin), ("numpy_port_cpu_us_per_record", numpy_port)):
+        fn()
+        t0 = time.perf_counter()
+        X = fn()
+        out[name] = (time.perf_counter() - t0) / n * 1e6
+        out[name.replace("us_per_record", "final_X")] = X.tolist()
+    return out
 
 
 def main():
@@ -141,20 +199,27 @@ def main():
                           "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM}
     log("per-call predict %.2f ms, correct %.2f ms at n=1M" % (res["predict_dev"]["kernel_ms"], ms))
 
-    # ---- drop-in latency at n = 1 (host pointers, what main_file.py pays per call)
+    # ---- per-call latency at n = 1 (host pointers): the ctypes engine wrappers, and the CPython
+    # binding the drop-in KalmanFilter.Prediction / Correction use (what main_file.py pays per call)
+    from poseestimationkf_amd import _fastcall
     gy, X1, P1, Q1, R1 = [0.1, 0.2, 0.3], np.array([1.0, 0, 0, 0]), np.eye(4), np.eye(3), np.eye(4) * 0.1
-    lat = {"predict": [], "correct": []}
-    for i in range(300):
-        t0 = time.perf_counter()
-        zz, pm, kk = engine.predict(gy, 1e7, X1, P1, Q1, R1)
-        t1 = time.perf_counter()
-        engine.correct([0.5, 0, -0.86], [0, 0.1, 0.99], zz, pm, kk, [0, 0, 1.0], [0.5, 0, -0.86])
-        t2 = time.perf_counter()
-        if i >= 50:
-            lat["predict"].append(t1 - t0)
-            lat["correct"].append(t2 - t1)
-    res["dropin_call_us"] = {k: float(np.median(v) * 1e6) for k, v in lat.items()}
-    log("drop-in latency: %s" % res["dropin_call_us"])
+    mg, ac, a0, m0 = [0.5, 0, -0.86], [0, 0.1, 0.99], [0, 0, 1.0], [0.5, 0, -0.86]
+    for key, pred, corr in (("ctypes_call_us", engine.predict, engine.correct),
+                            ("dropin_call_us", _fastcall.predict, _fastcall.correct)):
+        lat = {"predict": [], "correct": []}
+        for i in range(300):
+            t0 = time.perf_counter()
+            zz, pm, kk = pred(gy, 1e7, X1, P1, Q1, R1)
+            t1 = time.perf_counter()
+            corr(mg, ac, zz, pm, kk, a0, m0)
+            t2 = time.perf_counter()
+            if i >= 50:
+                lat["predict"].append(t1 - t0)
+                lat["correct"].append(t2 - t1)
+        res[key] = {k: float(np.median(v) * 1e6) for k, v in lat.items()}
+        log("%s: %s" % (key, res[key]))
+    res["c1_loop"] = c1_loop()
+    log("config-1 loop: %s" % res["c1_loop"])
     res["device"] = engine.device_name(0)
     print(json.dumps(res))
 

@@ -14,8 +14,9 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path through the C-ABI)")
     # a fresh checkout has no built artefacts (*.so are git-ignored): build them once
     import subprocess
-    lib = os.path.join(ROOT, "poseestimationkf_amd", "libpekf.so")
-    if not os.path.exists(lib) and os.path.exists("/opt/rocm/bin/hipcc"):
+    pkg = os.path.join(ROOT, "poseestimationkf_amd")
+    built = all(os.path.exists(os.path.join(pkg, f)) for f in ("libpekf.so", "_fastcall.so"))
+    if not built and os.path.exists("/opt/rocm/bin/hipcc"):
         subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(ROOT, "poseestimationkf_amd", "csrc")])
     if not os.path.exists(os.path.join(ROOT, "oracle", "build", "libekf_oracle.so")):
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])

@@ -56,9 +56,22 @@ def test_no_cpu_fallback_without_device():
         engine.BatchedEKF(4)
     with pytest.raises(_lib.NoDeviceError):
         engine.FilterHandle(np.zeros((4, 3)), np.zeros((4, 3)))
+    from poseestimationkf_amd import _fastcall
+    with pytest.raises(_lib.NoDeviceError):
+        _fastcall.predict([0.1, 0.2, 0.3], 1e7, np.array([1.0, 0, 0, 0]), np.eye(4), np.eye(3), np.eye(4))
     p = ctypes.c_void_p()
     assert _lib.lib.pekf_malloc(ctypes.byref(p), 64) == _lib.PEKF_ERR_NODEVICE
     assert "no HIP device" in _lib.last_error()
+
+
+def test_fastcall_binding_checks_shapes():
+    from poseestimationkf_amd import _fastcall
+    with pytest.raises(ValueError, match="gyro"):
+        _fastcall.predict([0.1, 0.2], 1e7, np.zeros(4), np.eye(4), np.eye(3), np.eye(4))
+    with pytest.raises(ValueError, match="mag0"):
+        _fastcall.correct(np.zeros(3), np.zeros(3), np.zeros(4), np.eye(4), np.eye(4), np.zeros(3), np.zeros(2))
+    with pytest.raises(TypeError):
+        _fastcall.wahba_quaternion(np.zeros(3))
 
 
 def test_invalid_arguments_are_reported_not_crashed():
