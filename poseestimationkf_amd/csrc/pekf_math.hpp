@@ -311,9 +311,10 @@ PEKF_DEV float recip(float x) {
     return fmaf(r, fmaf(-x, r, 1.0f), r);
 }
 
-// A P A^T + g (|x|^2 I - x x^T), A = Omega(h), h = w/2 (ExtendedKalmanFilter.py:44-47,52-55,61)
+// A P A^T + g (|x|^2 I - x x^T), A = Omega(h), h = w/2 (ExtendedKalmanFilter.py:44-47,52-55,61);
+// n2 = |x|^2 (shared with rk4_closed's normalisation)
 template <typename T>
-PEKF_DEV Sym4T<T> propagate_cov(const Sym4T<T> &P, const T *h, const T *x, T g) {
+PEKF_DEV Sym4T<T> propagate_cov(const Sym4T<T> &P, const T *h, const T *x, T n2, T g) {
     const T w0 = h[0], w1 = h[1], w2 = h[2];
     // T = Omega P (full 4x4), rows of Omega: [0,-w0,-w1,-w2] [w0,0,w2,-w1] [w1,-w2,0,w0] [w2,w1,-w0,0]
     const T p[4][4] = {{P.a00, P.a01, P.a02, P.a03},
@@ -337,7 +338,6 @@ PEKF_DEV Sym4T<T> propagate_cov(const Sym4T<T> &P, const T *h, const T *x, T g) 
             default: return w2 * t[i][0] + w1 * t[i][1] - w0 * t[i][2];
         }
     };
-    const T n2 = x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
     const T gx0 = g * x[0], gx1 = g * x[1], gx2 = g * x[2], gx3 = g * x[3];
     Sym4T<T> o;
     o.a00 = fma(g, n2 - x[0] * x[0], m(0, 0));
@@ -424,24 +424,23 @@ PEKF_DEV Sym4T<T> spd_inverse_schur(const Sym4T<T> &S) {
 }
 
 // Closed form of the classical RK4 step + normalisation (ExtendedKalmanFilter.py:25-41),
-// h_w = w/2 (so Omega(h_w) = 0.5*Omega(w), the reference's W).
-PEKF_DEV void rk4_closed(const double *x, double dt_ns, const double *hw, double *z) {
+// h_w = w/2 (so Omega(h_w) = 0.5*Omega(w), the reference's W).  z = ca x + cb 0.5*Omega(w) x and,
+// since 0.5*Omega(w) is skew with square -|h_w|^2 I, |z|^2 = (ca^2 + cb^2 |h_w|^2) |x|^2 exactly:
+// the normalisation factor is known before z is formed and folds into ca and cb.  n2 = |x|^2.
+PEKF_DEV void rk4_closed(const double *x, double n2, double dt_ns, const double *hw, double *z) {
     const double h = dt_ns * kNsToS;
     const double th2 = hw[0] * hw[0] + hw[1] * hw[1] + hw[2] * hw[2];
     const double xx = (h * h) * th2;
     const double ca = 1.0 - 0.5 * xx + xx * xx * (1.0 / 24.0);
     const double cb = h * (1.0 - xx * (1.0 / 6.0));
-    // 0.5*Omega(w) x
-    const double o0 = -hw[0] * x[1] - hw[1] * x[2] - hw[2] * x[3];
-    const double o1 = hw[0] * x[0] + hw[2] * x[2] - hw[1] * x[3];
-    const double o2 = hw[1] * x[0] - hw[2] * x[1] + hw[0] * x[3];
-    const double o3 = hw[2] * x[0] + hw[1] * x[1] - hw[0] * x[2];
-    z[0] = ca * x[0] + cb * o0;
-    z[1] = ca * x[1] + cb * o1;
-    z[2] = ca * x[2] + cb * o2;
-    z[3] = ca * x[3] + cb * o3;
-    const double in = rsqrt<true>(z[0] * z[0] + z[1] * z[1] + z[2] * z[2] + z[3] * z[3]);
-    z[0] *= in; z[1] *= in; z[2] *= in; z[3] *= in;
+    const double in = rsqrt<true>((ca * ca + (cb * cb) * th2) * n2);
+    const double a = ca * in, c = cb * in;
+    const double w0 = c * hw[0], w1 = c * hw[1], w2 = c * hw[2];
+    // z = a x + Omega(c h_w) x, rows of Omega as in propagate_cov
+    z[0] = a * x[0] - w0 * x[1] - w1 * x[2] - w2 * x[3];
+    z[1] = a * x[1] + w0 * x[0] + w2 * x[2] - w1 * x[3];
+    z[2] = a * x[2] + w1 * x[0] - w2 * x[1] + w0 * x[3];
+    z[3] = a * x[3] + w2 * x[0] + w1 * x[1] - w0 * x[2];
 }
 
 }  // namespace pekf

@@ -77,9 +77,10 @@ __device__ __forceinline__ void ekf_record_step(double *x, Sym4T<PT> &P, const F
     // ---- Prediction (ExtendedKalmanFilter.py:58-68) ----
     const PT hp[3] = {(PT)hw[0], (PT)hw[1], (PT)hw[2]};
     const PT xp[4] = {(PT)x[0], (PT)x[1], (PT)x[2], (PT)x[3]};
-    const Sym4T<PT> Pm = propagate_cov<PT>(P, hp, xp, g);  // Jb from the prior X (:60)
+    const double n2 = x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
+    const Sym4T<PT> Pm = propagate_cov<PT>(P, hp, xp, (PT)n2, g);  // Jb from the prior X (:60)
     double z[4];
-    rk4_closed(x, dt_ns, hw, z);                            // (:62)
+    rk4_closed(x, n2, dt_ns, hw, z);                                // (:62)
 
     if (missing) {
         // Wahba-skip: no Correction for this record (X = z, P = P-)

@@ -47,7 +47,7 @@ __global__ __launch_bounds__(kSideBlock) void k_gyro_chain(int64_t batch, int64_
             const double hw[3] = {0.5 * (double)r.x, 0.5 * (double)r.y, 0.5 * (double)r.z};
             const double dt_ns = (double)(__float_as_uint(r.w) & 0x7FFFFFFFu);
             double z[4];
-            rk4_closed(x, dt_ns, hw, z);
+            rk4_closed(x, x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3], dt_ns, hw, z);
             x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
             if (traj) {
                 double2 *o = reinterpret_cast<double2 *>(traj + t * batch * 4) + 2 * (int64_t)lane;
