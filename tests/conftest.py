@@ -15,7 +15,8 @@ def pytest_configure(config):
     # a fresh checkout has no built artefacts (*.so are git-ignored): build them once
     import subprocess
     pkg = os.path.join(ROOT, "poseestimationkf_amd")
-    built = all(os.path.exists(os.path.join(pkg, f)) for f in ("libpekf.so", "_fastcall.so"))
+    built = all(os.path.exists(os.path.join(pkg, f)) for f in ("libpekf.so", "_fastcall.so")) and \
+        os.path.exists(os.path.join(ROOT, "examples", "build", "libc_client.so"))
     if not built and os.path.exists("/opt/rocm/bin/hipcc"):
         subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(ROOT, "poseestimationkf_amd", "csrc")])
     if not os.path.exists(os.path.join(ROOT, "oracle", "build", "libekf_oracle.so")):
