@@ -354,45 +354,11 @@ PEKF_DEV Sym4T<T> propagate_cov(const Sym4T<T> &P, const T *h, const T *x, T n2,
     return o;
 }
 
-// Inverse of an SPD 4x4 by LDL^T (no pivoting needed: S = P- + rI, r > 0).
-template <typename T, bool FAST = true>
-PEKF_DEV Sym4T<T> spd_inverse(const Sym4T<T> &S) {
-    const T i0 = recip<FAST>(S.a00);
-    const T l10 = S.a01 * i0, l20 = S.a02 * i0, l30 = S.a03 * i0;
-    const T d1 = S.a11 - l10 * S.a01, i1 = recip<FAST>(d1);
-    const T a21 = S.a12 - l20 * S.a01, a31 = S.a13 - l30 * S.a01;
-    const T l21 = a21 * i1, l31 = a31 * i1;
-    const T d2 = S.a22 - l20 * S.a02 - l21 * a21, i2 = recip<FAST>(d2);
-    const T a32 = S.a23 - l30 * S.a02 - l31 * a21;
-    const T l32 = a32 * i2;
-    const T d3 = S.a33 - l30 * S.a03 - l31 * a31 - l32 * a32, i3 = recip<FAST>(d3);
-    // N = L^-1 (unit lower)
-    const T n10 = -l10;
-    const T n21 = -l21, n20 = -(l20 + l21 * n10);
-    const T n32 = -l32, n31 = -(l31 + l32 * n21), n30 = -(l30 + l31 * n10 + l32 * n20);
-    // S^-1 = N^T D^-1 N
-    const T m30 = n30 * i3, m31 = n31 * i3, m32 = n32 * i3;
-    const T m20 = n20 * i2, m21 = n21 * i2;
-    const T m10 = n10 * i1;
-    Sym4T<T> o;
-    o.a33 = i3;
-    o.a23 = m32;
-    o.a22 = i2 + n32 * m32;
-    o.a13 = m31;
-    o.a12 = m21 + n31 * m32;
-    o.a11 = i1 + n21 * m21 + n31 * m31;
-    o.a03 = m30;
-    o.a02 = m20 + n30 * m32;
-    o.a01 = m10 + n20 * m21 + n30 * m31;
-    o.a00 = i0 + n10 * m10 + n20 * m20 + n30 * m30;
-    return o;
-}
-
 // Inverse of an SPD 4x4 by 2x2 blocks, S = [[A, B], [B^T, D]]: A^-1 by its adjugate, the Schur
 // complement C = D - B^T A^-1 B (SPD) likewise, then
 //   S^-1 = [[A^-1 + X C^-1 X^T, -X C^-1], [-C^-1 X^T, C^-1]],  X = A^-1 B.
-// Two reciprocals instead of LDL^T's four (a v_rcp_f64 issues at 3x an FMA on gfx950,
-// scripts/probe_rates.hip): 38 plain operations + 2 Newton-refined reciprocals.
+// Two reciprocals (an LDL^T factorisation needs four, and a v_rcp_f64 issues at 3x an FMA on
+// gfx950, scripts/probe_rates.hip): 38 plain operations + 2 Newton-refined reciprocals.
 template <typename T, bool FAST = true>
 PEKF_DEV Sym4T<T> spd_inverse_schur(const Sym4T<T> &S) {
     const T ia = recip<FAST>(S.a00 * S.a11 - S.a01 * S.a01);
