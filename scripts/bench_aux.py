@@ -155,12 +155,13 @@ def main():
     log("wahba stream: %.1f ms" % ms)
     del win, out
 
-    # ---- online serving: every launch advances 1M filters by ONE new record; the state X, P is
-    # read and written through HBM each launch.  AoS: 40 B record + 32+128 B read (P's cache
-    # lines come whole) + 32+128 B written; SoA (X[4][B], P[10][B]): 40 + 32+80 + 32+80 B.
+    # ---- online serving: every launch advances 1M filters by ONE new record; the state X, P and
+    # the reference vectors are read and the state written through HBM each launch.  AoS: 40 B
+    # record + 48 B refs + 32+128 B state read (P's cache lines come whole) + 32+128 B written;
+    # SoA (X[4][B], P[10][B]): 40 + 48 + 32+80 + 32+80 B.
     B1 = 1 << 20
     win1 = engine.IMUWindow(B1, 8).synthesize(stream=s)
-    for layout, per in (("aos", 40 + 32 + 128 + 32 + 128), ("soa", 40 + 32 + 80 + 32 + 80)):
+    for layout, per in (("aos", 40 + 48 + 32 + 128 + 32 + 128), ("soa", 40 + 48 + 32 + 80 + 32 + 80)):
         f1 = engine.BatchedEKF(B1, layout=layout)
         k = [0]
 
