@@ -1,10 +1,13 @@
 """Restatement of the live server's pre-processing front-end -- TEST INFRASTRUCTURE ONLY.
 
-PARITY UNPINNED: the source is C++ (Kalman Filter Server/PoseEstimator/Parser.cpp,
+PARITY PARTLY PINNED: the source is C++ (Kalman Filter Server/PoseEstimator/Parser.cpp,
 KalmanFilter.cpp) that needs Eigen, conio.h and winsock, so it cannot be
-built here and there are no fixtures for it; this file restates its phase-3 logic by
-reading the code.  Used only by tests/test_frontend.py as the checker of
-pekf_frontend_dev.
+built here and ships no fixtures; this file restates its phase-3 logic by reading the code.
+The low-pass stage (`lpf_step`) is pinned bit for bit by the reference's own Python
+`Test.py:20-35` (the same alpha = 0.1 recurrence from a zero state, run unchanged to produce
+tests/golden/lpf_testpy.npz); the state machine, interpolation and normalisation are
+unpinned.  Used only by tests/test_frontend.py as the checker of pekf_frontend_dev
+(SURVEY.md §8f-2).
 
 Per filter, events (type '0' acc, '1' gyro, '2' mag; 3 values; integer ns time) go through
 Parser::WriteKalmanFilterMeasurement (Parser.cpp:148-219):
@@ -31,6 +34,20 @@ ACC, GYRO, MAG = 0, 1, 2
 def _interp(t1, t2, t3, y1, y2):
     """Parser::LinearInterpolationSensor (Parser.cpp:259-267)."""
     return [(y2[i] - y1[i]) / (float(t2) - float(t1)) * (float(t3) - float(t1)) + y1[i] for i in range(3)]
+
+
+def lpf_step(prev, x, alpha):
+    """alpha * x + (1 - alpha) * prev per component (KalmanFilter.cpp:285,298; Test.py:29-35)."""
+    return [alpha * x[i] + (1 - alpha) * prev[i] for i in range(3)]
+
+
+def lpf(samples, alpha=0.1):
+    """The low-pass over a sample sequence from a zero state: (n, 3) -> (n, 3)."""
+    out, prev = [], [0.0, 0.0, 0.0]
+    for x in np.asarray(samples, np.float64):
+        prev = lpf_step(prev, x, alpha)
+        out.append(prev)
+    return np.array(out)
 
 
 def _normalise(v):
@@ -81,8 +98,8 @@ def run_frontend(types, values, times, init_acc, init_mag, t_init, alpha=0.1):
             gyro_set = acc1_set = mag1_set = False
             a = _normalise(_interp(t_acc0, t_acc1, t_gyro, acc0, acc1))
             m = _normalise(_interp(t_mag0, t_mag1, t_gyro, mag0, mag1))
-            lpf_mag = [alpha * m[i] + (1 - alpha) * lpf_mag[i] for i in range(3)]
-            lpf_acc = [alpha * a[i] + (1 - alpha) * lpf_acc[i] for i in range(3)]
+            lpf_mag = lpf_step(lpf_mag, m, alpha)
+            lpf_acc = lpf_step(lpf_acc, a, alpha)
             out_g.append(gyro)
             out_dt.append(t_gyro - prev_t)
             out_a.append(lpf_acc)

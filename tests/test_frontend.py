@@ -1,8 +1,11 @@
 """Server front-end: raw phone events -> records -> filter.
 
-PARITY UNPINNED: the checker is oracle/frontend_numpy.py, a restatement of the C++ front-end
+PARTLY PINNED: the checker is oracle/frontend_numpy.py, a restatement of the C++ front-end
 (KFS/Parser.cpp, KFS/KalmanFilter.cpp), which cannot be built here (Eigen, Windows headers) and
-ships no fixtures.  The filter that consumes the records is pinned as everywhere else."""
+ships no fixtures.  Its low-pass stage is pinned by the reference's own Test.py
+(tests/golden/lpf_testpy.npz, made by tests/golden/make_lpf_golden.py); the state machine,
+interpolation and normalisation are not.  The filter that consumes the records is pinned as
+everywhere else."""
 import numpy as np
 import pytest
 
@@ -13,6 +16,16 @@ from poseestimationkf_amd import synth
 def _oracle_records(ev, k):
     return fe.run_frontend(ev["types"][:, k], ev["values"][:, k].astype(np.float64), ev["times"][:, k],
                            ev["init_acc"][k], ev["init_mag"][k], ev["t_init"][k])
+
+
+def test_oracle_lpf_matches_reference_test_py():
+    """The alpha = 0.1 low-pass from a zero state, bit for bit against Test.py's own output."""
+    import os
+    from .conftest import GOLDEN
+    d = np.load(os.path.join(GOLDEN, "lpf_testpy.npz"))
+    alpha = float(d["alpha"][0])
+    assert np.array_equal(fe.lpf(d["acc_raw"], alpha), d["acc_lpf"])
+    assert np.array_equal(fe.lpf(d["mag_raw"], alpha), d["mag_lpf"])
 
 
 def test_oracle_state_machine_basics():
