@@ -1,0 +1,10 @@
+#!/usr/bin/env bash
+B="python3 bench.py --cpu-baseline none --parity-samples 0"
+exec scripts/gpu_session.sh r1y \
+ "timeout -k 10 500 python -m pytest tests -m gpu -q -p no:cacheprovider -x" \
+ "timeout -k 10 400 python bench.py --steps 3 --warmup 1 > gpurun_out/r1y/bench_f64.json" \
+ "timeout -k 10 300 python bench.py --steps 3 --warmup 1 --precision mixed --cpu-baseline none > gpurun_out/r1y/bench_mixed.json" \
+ "timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r1y/trace -o run --output-format csv -- $B --steps 3 --warmup 1" \
+ "timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/r1y/pmc_fetch -o run --output-format csv -- $B --steps 1 --warmup 0" \
+ "timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d gpurun_out/r1y/pmc_sq -o run --output-format csv -- $B --steps 1 --warmup 0" \
+ "timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/r1y/auxtrace -o aux --output-format csv -- python3 scripts/bench_aux.py"
