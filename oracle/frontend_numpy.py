@@ -33,7 +33,9 @@ ACC, GYRO, MAG = 0, 1, 2
 
 def _interp(t1, t2, t3, y1, y2):
     """Parser::LinearInterpolationSensor (Parser.cpp:259-267)."""
-    return [(y2[i] - y1[i]) / (float(t2) - float(t1)) * (float(t3) - float(t1)) + y1[i] for i in range(3)]
+    with np.errstate(divide="ignore", invalid="ignore"):  # C++ double: x / 0 is inf / nan, not an error
+        return [np.float64(y2[i] - y1[i]) / np.float64(float(t2) - float(t1)) * (float(t3) - float(t1)) + y1[i]
+                for i in range(3)]
 
 
 def lpf_step(prev, x, alpha):
@@ -52,8 +54,9 @@ def lpf(samples, alpha=0.1):
 
 def _normalise(v):
     """Parser::NormalizeValues (Parser.cpp:221-228)."""
-    d = np.sqrt((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2])
-    return [v[0] / d, v[1] / d, v[2] / d]
+    d = np.sqrt(np.float64((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return [v[0] / d, v[1] / d, v[2] / d]
 
 
 def run_frontend(types, values, times, init_acc, init_mag, t_init, alpha=0.1):

@@ -109,3 +109,57 @@ def test_events_to_filter_end_to_end(eng, oracle_c):
     err = float(np.abs(X[cols] - Xo).max())
     print("events -> front-end -> filter vs oracle chain: max |dq| = %.3e over %d records" % (err, n))
     assert err < 1e-9
+
+
+def _events(K, spec):
+    """Hand-made event streams: spec = list of (type, gap_ns) applied to every filter, values
+    from a fixed pattern.  Returns the generate_events-style dict."""
+    E = len(spec)
+    types = np.array([[t] * K for t, _ in spec], np.uint32).reshape(E, K)
+    gaps = np.array([[g] * K for _, g in spec], np.int64).reshape(E, K)
+    times = synth.T_INIT_NS + np.cumsum(gaps, axis=0)
+    e = np.arange(E)[:, None, None]
+    vals = (np.cos(0.3 * e + np.arange(3)[None, None, :] + 0.01 * np.arange(K)[None, :, None]) +
+            np.where(types[..., None] == synth.EV_ACC, [0, 0, 9.0], [0, 0, 0])).astype(np.float32)
+    return dict(types=types, values=vals, times=times, init_acc=np.tile([0.1, 0.2, 9.8], (K, 1)),
+                init_mag=np.tile([20.0, 1.0, -40.0], (K, 1)), t_init=np.full(K, synth.T_INIT_NS, np.int64))
+
+
+@pytest.mark.gpu
+def test_frontend_streams_without_records(eng):
+    K = 70
+    for spec in ([], [(synth.EV_ACC, 10), (synth.EV_MAG, 10)] * 5,            # nothing, or no gyro at all
+                 [(synth.EV_GYRO, 10), (synth.EV_ACC, 10), (synth.EV_GYRO, 10)] * 3):  # never a mag after a gyro
+        _, counts = eng.run_frontend(_events(K, spec), r_max=8)
+        assert np.all(counts == 0)
+
+
+@pytest.mark.gpu
+def test_frontend_r_max_overflow_is_reported(eng):
+    spec = [(synth.EV_GYRO, 1000), (synth.EV_ACC, 1000), (synth.EV_MAG, 1000)] * 6  # 6 records
+    with pytest.raises(ValueError, match="r_max"):
+        eng.run_frontend(_events(4, spec), r_max=5)
+    _, counts = eng.run_frontend(_events(4, spec), r_max=6)
+    assert np.all(counts == 6)
+
+
+@pytest.mark.gpu
+def test_frontend_zero_time_gaps_follow_ieee_like_the_cpp(eng):
+    """Equal acc (or mag) timestamps make the interpolation divide by zero: the C++ server's double
+    arithmetic gives inf/nan there (no exception), and so do the oracle and the kernel."""
+    K = 8
+    # acc_0 and acc_1 both at t = 500 (zero gaps): the first record's acc is 0/0 -> nan, and the
+    # low-pass carries the nan into the second record; the magnetometer channel stays finite
+    spec = [(synth.EV_ACC, 500), (synth.EV_GYRO, 0), (synth.EV_ACC, 0), (synth.EV_MAG, 500),
+            (synth.EV_GYRO, 500), (synth.EV_ACC, 500), (synth.EV_MAG, 500)]
+    ev = _events(K, spec)
+    win, counts = eng.run_frontend(ev, r_max=4)
+    rec = win.download_filters(np.arange(K))
+    for k in range(K):
+        g, dt, a, m = _oracle_records(ev, k)
+        r = len(dt)
+        assert counts[k] == r == 2
+        assert np.isnan(a).all() and np.isnan(rec.acc[:r, k]).all()
+        fin = np.isfinite(a)
+        assert _f32_ulps(rec.acc[:r, k][fin], a[fin]) <= 1
+        assert _f32_ulps(rec.mag[:r, k], m) <= 1
