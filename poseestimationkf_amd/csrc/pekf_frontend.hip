@@ -25,16 +25,6 @@ struct F3 {
 };
 __device__ __forceinline__ V3 widen(const F3 &f) { return {f.x, f.y, f.z}; }
 
-// Parser::LinearInterpolationSensor (:259-267): (y2 - y1) / (t2 - t1) * (t3 - t1) + y1, with the
-// division by (t2 - t1) taken once as a reciprocal (the emit path runs for the whole wave whenever
-// any lane emits a record, so its cost is paid on almost every event).  Timestamps are integer
-// nanoseconds held in doubles (exact below 2^53 ns), so t3 - t1 is the exact difference that
-// (double)t3 - (double)t1 gives, without int64 <-> double conversions.
-__device__ __forceinline__ V3 lerp_to(double t1, double t2, double t3, const V3 &a, const V3 &b) {
-    const double f = (t3 - t1) * recip<true>(t2 - t1);
-    return {(b.x - a.x) * f + a.x, (b.y - a.y) * f + a.y, (b.z - a.z) * f + a.z};
-}
-
 // Parser::NormalizeValues (:221-228) with one rsqrt instead of a sqrt and three divisions
 __device__ __forceinline__ V3 normalised(const V3 &v) {
     const double in = rsqrt<true>((v.x * v.x + v.y * v.y) + v.z * v.z);
@@ -68,10 +58,51 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
     const double beta = 1.0 - alpha;
     int64_t r = 0;
     int bad = 0;
+
+    // Emission is deferred: when a lane completes a record, only its inputs are copied aside
+    // (pend), and the expensive part -- two interpolations with a reciprocal, two normalisations
+    // with an rsqrt, the low-pass and the f32 packing -- runs for the whole wave once every
+    // kFlush events instead of on every event some lane emits (which, with 64 lanes, is nearly
+    // every event).  A lane needs at least 3 events (gyro, acc, mag) between two records, so
+    // with kFlush = 3 it never has two pending.  Arithmetic is unchanged: the time differences
+    // are formed at emission, exactly as lerp_to would form them.
+    constexpr int kFlush = 3;
+    bool pend = false;
+    F3 p_gyro = {0, 0, 0}, p_acc1 = {0, 0, 0}, p_mag1 = {0, 0, 0};
+    V3 p_acc0 = {0, 0, 0}, p_mag0 = {0, 0, 0};
+    double p_dt = 0, p_an = 0, p_ad = 1, p_mn = 0, p_md = 1;  // dt, acc / mag lerp num and den
+    auto flush = [&]() {
+        if (!pend) return;
+        pend = false;
+        // Parser::LinearInterpolationSensor (:259-267): (y2 - y1) / (t2 - t1) * (t3 - t1) + y1, the
+        // division taken as one reciprocal.  Timestamps are integer ns held in doubles (exact below
+        // 2^53), so t3 - t1 and t2 - t1 are the exact differences (double)t3 - (double)t1 gives.
+        const double fa = p_an * recip<true>(p_ad), fm = p_mn * recip<true>(p_md);
+        const V3 a1 = widen(p_acc1), m1 = widen(p_mag1);
+        const V3 a = normalised({(a1.x - p_acc0.x) * fa + p_acc0.x, (a1.y - p_acc0.y) * fa + p_acc0.y,
+                                 (a1.z - p_acc0.z) * fa + p_acc0.z});
+        const V3 m = normalised({(m1.x - p_mag0.x) * fm + p_mag0.x, (m1.y - p_mag0.y) * fm + p_mag0.y,
+                                 (m1.z - p_mag0.z) * fm + p_mag0.z});
+        lpf_mag = {alpha * m.x + beta * lpf_mag.x, alpha * m.y + beta * lpf_mag.y, alpha * m.z + beta * lpf_mag.z};
+        lpf_acc = {alpha * a.x + beta * lpf_acc.x, alpha * a.y + beta * lpf_acc.y, alpha * a.z + beta * lpf_acc.z};
+        if (!(p_dt >= 0.0 && p_dt < 2147483648.0)) bad |= 1;  // not representable in the 31-bit dt word
+        if (r < r_max) {
+            const int64_t o = r * batch + b;
+            gd[o] = make_float4((float)p_gyro.x, (float)p_gyro.y, (float)p_gyro.z,
+                                __uint_as_float((uint32_t)fmin(fmax(p_dt, 0.0), 2147483647.0)));
+            am[o] = make_float4((float)lpf_acc.x, (float)lpf_acc.y, (float)lpf_acc.z, (float)lpf_mag.x);
+            my[o] = make_float2((float)lpf_mag.y, (float)lpf_mag.z);
+        } else {
+            bad |= 2;  // more records than the output window holds
+        }
+        ++r;
+    };
+
     // the next event is loaded before the current one is processed; latency is covered by
     // occupancy (small register footprint)
     float4 nv4 = n_events > 0 ? ev[b] : make_float4(0.f, 0.f, 0.f, 0.f);
     double t = t_start;
+    int phase = 0;
     for (int64_t e = 0; e < n_events; ++e) {
         const float4 v4 = nv4;
         if (e + 1 < n_events) nv4 = ev[(e + 1) * batch + b];
@@ -93,29 +124,22 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
                 acc1_set = mag1_set = false;
             }
         }
-        if (acc1_set && mag1_set) {
+        if (acc1_set && mag1_set) {  // ExecuteKalmanFilter (Parser.cpp:229-257): record its inputs
             gyro_set = acc1_set = mag1_set = false;
-            const V3 a = normalised(lerp_to(t_acc0, t_acc1, t_gyro, acc0, widen(acc1)));
-            const V3 m = normalised(lerp_to(t_mag0, t_mag1, t_gyro, mag0, widen(mag1)));
-            lpf_mag = {alpha * m.x + beta * lpf_mag.x, alpha * m.y + beta * lpf_mag.y, alpha * m.z + beta * lpf_mag.z};
-            lpf_acc = {alpha * a.x + beta * lpf_acc.x, alpha * a.y + beta * lpf_acc.y, alpha * a.z + beta * lpf_acc.z};
-            const double dt = t_gyro - prev_t;
-            if (!(dt >= 0.0 && dt < 2147483648.0)) bad |= 1;  // not representable in the 31-bit dt word
-            if (r < r_max) {
-                const int64_t o = r * batch + b;
-                gd[o] = make_float4((float)gyro.x, (float)gyro.y, (float)gyro.z,
-                                    __uint_as_float((uint32_t)fmin(fmax(dt, 0.0), 2147483647.0)));
-                am[o] = make_float4((float)lpf_acc.x, (float)lpf_acc.y, (float)lpf_acc.z, (float)lpf_mag.x);
-                my[o] = make_float2((float)lpf_mag.y, (float)lpf_mag.z);
-            } else {
-                bad |= 2;  // more records than the output window holds
-            }
-            ++r;
+            pend = true;
+            p_gyro = gyro; p_dt = t_gyro - prev_t;
+            p_acc0 = acc0; p_acc1 = acc1; p_an = t_gyro - t_acc0; p_ad = t_acc1 - t_acc0;
+            p_mag0 = mag0; p_mag1 = mag1; p_mn = t_gyro - t_mag0; p_md = t_mag1 - t_mag0;
             prev_t = t_gyro;
             acc0 = widen(acc1); t_acc0 = t_acc1;
             mag0 = widen(mag1); t_mag0 = t_mag1;
         }
+        if (++phase == kFlush) {  // uniform
+            phase = 0;
+            flush();
+        }
     }
+    flush();
     counts[b] = (int32_t)(r < r_max ? r : r_max);
     if (bad && err) atomicOr(err, bad);
 }
