@@ -24,6 +24,13 @@ struct F3 {
     float x, y, z;
 };
 __device__ __forceinline__ V3 widen(const F3 &f) { return {f.x, f.y, f.z}; }
+// component-wise c ? a : b (a struct-valued ?: would go through scratch memory)
+__device__ __forceinline__ V3 sel(bool c, const V3 &a, const V3 &b) {
+    return {c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z};
+}
+__device__ __forceinline__ F3 sel(bool c, const F3 &a, const F3 &b) {
+    return {c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z};
+}
 
 // Parser::NormalizeValues (:221-228) with one rsqrt instead of a sqrt and three divisions
 __device__ __forceinline__ V3 normalised(const V3 &v) {
@@ -51,7 +58,8 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
         refs[6 * b + 0] = a.x; refs[6 * b + 1] = a.y; refs[6 * b + 2] = a.z;
         refs[6 * b + 3] = m.x; refs[6 * b + 4] = m.y; refs[6 * b + 5] = m.z;
     }
-    F3 acc1 = {0, 0, 0}, mag1 = {0, 0, 0}, gyro = {0, 0, 0};  // sensor samples: exact in f32
+    V3 acc1 = {0, 0, 0}, mag1 = {0, 0, 0};  // sensor samples (exact f32 values, kept widened)
+    F3 gyro = {0, 0, 0};
     double t_acc1 = 0, t_mag1 = 0, t_gyro = 0;
     bool gyro_set = false, acc1_set = false, mag1_set = false;
     V3 lpf_acc = {0, 0, 0}, lpf_mag = {0, 0, 0};
@@ -68,8 +76,8 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
     // are formed at emission, exactly as lerp_to would form them.
     constexpr int kFlush = 3;
     bool pend = false;
-    F3 p_gyro = {0, 0, 0}, p_acc1 = {0, 0, 0}, p_mag1 = {0, 0, 0};
-    V3 p_acc0 = {0, 0, 0}, p_mag0 = {0, 0, 0};
+    F3 p_gyro = {0, 0, 0};
+    V3 p_acc0 = {0, 0, 0}, p_mag0 = {0, 0, 0}, p_acc1 = {0, 0, 0}, p_mag1 = {0, 0, 0};
     double p_dt = 0, p_an = 0, p_ad = 1, p_mn = 0, p_md = 1;  // dt, acc / mag lerp num and den
     auto flush = [&]() {
         if (!pend) return;
@@ -78,7 +86,7 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
         // division taken as one reciprocal.  Timestamps are integer ns held in doubles (exact below
         // 2^53), so t3 - t1 and t2 - t1 are the exact differences (double)t3 - (double)t1 gives.
         const double fa = p_an * recip<true>(p_ad), fm = p_mn * recip<true>(p_md);
-        const V3 a1 = widen(p_acc1), m1 = widen(p_mag1);
+        const V3 a1 = p_acc1, m1 = p_mag1;
         const V3 a = normalised({(a1.x - p_acc0.x) * fa + p_acc0.x, (a1.y - p_acc0.y) * fa + p_acc0.y,
                                  (a1.z - p_acc0.z) * fa + p_acc0.z});
         const V3 m = normalised({(m1.x - p_mag0.x) * fm + p_mag0.x, (m1.y - p_mag0.y) * fm + p_mag0.y,
@@ -98,48 +106,71 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
         ++r;
     };
 
-    // the next event is loaded before the current one is processed; latency is covered by
-    // occupancy (small register footprint)
-    float4 nv4 = n_events > 0 ? ev[b] : make_float4(0.f, 0.f, 0.f, 0.f);
+    // Events stream through a register ring of kFlush records loaded kFlush events ahead (the
+    // loop is unrolled by kFlush so every ring index is static; the row is clamped to the last
+    // event, so the loads past the end read a valid row and need no predicate).
+    const uint32_t lane = (uint32_t)b;
+    auto load = [&](int64_t e) -> float4 {
+        const int64_t row = e < n_events ? e : n_events - 1;
+        return (ev + row * batch)[lane];
+    };
     double t = t_start;
-    int phase = 0;
-    for (int64_t e = 0; e < n_events; ++e) {
-        const float4 v4 = nv4;
-        if (e + 1 < n_events) nv4 = ev[(e + 1) * batch + b];
+    auto event = [&](const float4 v4) {
         const uint32_t word = __float_as_uint(v4.w);
         const uint32_t ty = word & 3u;
         t += (double)(word >> 2);  // the event word carries the ns gap to the previous event
-        const F3 v = {v4.x, v4.y, v4.z};
-        if (!gyro_set) {
-            if (ty == kEvAcc) { acc0 = widen(v); t_acc0 = t; }
-            else if (ty == kEvMag) { mag0 = widen(v); t_mag0 = t; }
-            else if (ty == kEvGyro) { gyro = v; t_gyro = t; gyro_set = true; }
-        } else {
-            if (ty == kEvAcc) { acc1 = v; t_acc1 = t; acc1_set = true; }
-            else if (ty == kEvMag) { mag1 = v; t_mag1 = t; mag1_set = true; }
-            else if (ty == kEvGyro) {
-                gyro = v; t_gyro = t;
-                if (acc1_set) { acc0 = widen(acc1); t_acc0 = t_acc1; }
-                if (mag1_set) { mag0 = widen(mag1); t_mag0 = t_mag1; }
-                acc1_set = mag1_set = false;
-            }
-        }
-        if (acc1_set && mag1_set) {  // ExecuteKalmanFilter (Parser.cpp:229-257): record its inputs
-            gyro_set = acc1_set = mag1_set = false;
+        // Parser::WriteKalmanFilterMeasurement (Parser.cpp:148-219), branch-free: each state
+        // variable is one select, so nothing is copied between divergent paths.
+        //   before a gyro sample: acc -> acc_0, mag -> mag_0, gyro -> gyro (gyro_is_set);
+        //   after it: acc -> acc_1, mag -> mag_1 (set); a new gyro replaces the gyro and shifts a set
+        //   acc_1 -> acc_0 / mag_1 -> mag_0, clearing both flags.
+        const bool isA = ty == kEvAcc, isM = ty == kEvMag, isG = ty == kEvGyro;
+        const bool gs = gyro_set;
+        const double vx = v4.x, vy = v4.y, vz = v4.z;
+        const bool wA1 = isA && gs, wM1 = isM && gs;
+        acc1 = sel(wA1, V3{vx, vy, vz}, acc1);
+        t_acc1 = wA1 ? t : t_acc1;
+        mag1 = sel(wM1, V3{vx, vy, vz}, mag1);
+        t_mag1 = wM1 ? t : t_mag1;
+        const bool a1s = wA1 || (acc1_set && !(isG && gs)), m1s = wM1 || (mag1_set && !(isG && gs));
+        const bool sA = isG && gs && acc1_set, sM = isG && gs && mag1_set;  // gyro shift
+        // ExecuteKalmanFilter (Parser.cpp:229-257) once acc_1 and mag_1 are both set: record its
+        // inputs (pending until the next flush), then acc_0 <- acc_1, mag_0 <- mag_1, flags cleared
+        const bool emit = a1s && m1s;
+        if (emit) {
             pend = true;
             p_gyro = gyro; p_dt = t_gyro - prev_t;
             p_acc0 = acc0; p_acc1 = acc1; p_an = t_gyro - t_acc0; p_ad = t_acc1 - t_acc0;
             p_mag0 = mag0; p_mag1 = mag1; p_mn = t_gyro - t_mag0; p_md = t_mag1 - t_mag0;
             prev_t = t_gyro;
-            acc0 = widen(acc1); t_acc0 = t_acc1;
-            mag0 = widen(mag1); t_mag0 = t_mag1;
         }
-        if (++phase == kFlush) {  // uniform
-            phase = 0;
+        const bool wA0 = isA && !gs, wM0 = isM && !gs;
+        const bool cA = sA || emit, cM = sM || emit;  // acc_0 <- acc_1 (shift or after a record)
+        acc0 = sel(wA0, V3{vx, vy, vz}, sel(cA, acc1, acc0));
+        t_acc0 = wA0 ? t : (cA ? t_acc1 : t_acc0);
+        mag0 = sel(wM0, V3{vx, vy, vz}, sel(cM, mag1, mag0));
+        t_mag0 = wM0 ? t : (cM ? t_mag1 : t_mag0);
+        gyro = sel(isG, F3{v4.x, v4.y, v4.z}, gyro);
+        t_gyro = isG ? t : t_gyro;
+        gyro_set = (gs || isG) && !emit;
+        acc1_set = a1s && !emit;
+        mag1_set = m1s && !emit;
+    };
+    if (n_events > 0) {
+        float4 ring[kFlush];
+#pragma unroll
+        for (int k = 0; k < kFlush; ++k) ring[k] = load(k);
+        for (int64_t e0 = 0; e0 < n_events; e0 += kFlush) {
+#pragma unroll
+            for (int k = 0; k < kFlush; ++k) {
+                if (e0 + k >= n_events) break;  // uniform
+                const float4 v4 = ring[k];
+                ring[k] = load(e0 + k + kFlush);
+                event(v4);
+            }
             flush();
         }
     }
-    flush();
     counts[b] = (int32_t)(r < r_max ? r : r_max);
     if (bad && err) atomicOr(err, bad);
 }
