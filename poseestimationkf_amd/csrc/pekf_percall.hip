@@ -1,12 +1,15 @@
 // pekf_percall.hip -- per-call operators behind the drop-in Python API (one thread per item).
 //
 // These keep the reference's dense formulation (ExtendedKalmanFilter.py, Wahba.py) so
-// each call matches NumPy to rounding; the fused time-loop kernel is pekf_run.hip.
+// each call matches NumPy to rounding; the fused time-loop kernel is pekf_run.hip.  The batched
+// kernels move their per-item operands through WaveTile (pekf_tile.hpp): coalesced block reads
+// and writes, transposed through LDS; the d_* bodies work on per-lane copies.
 #include <cstring>
 #include <vector>
 
 #include "pekf_internal.hpp"
 #include "pekf_math.hpp"
+#include "pekf_tile.hpp"
 
 namespace pekf {
 
@@ -17,10 +20,23 @@ __device__ __forceinline__ void d_rk4(int64_t i, const double *q0, const double 
     rk4_literal(q0 + 4 * i, dt[i], w + 3 * i, out + 4 * i);
 }
 
+// Pool of LDS for the WaveTiles of a block whose widest operand has W doubles per item.
+#define PEKF_TILE(t, W, n)                                                  \
+    __shared__ double pool_[kBlock / kWave * tile_doubles<W>()];           \
+    const WaveTile t(pool_, tile_doubles<W>(), (n))
+
 __global__ __launch_bounds__(kBlock) void k_rk4(int64_t n, const double *q0, const double *dt,
                                                const double *w, double *out, Done done) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) d_rk4(i, q0, dt, w, out);
+    PEKF_TILE(t, 4, n);
+    double cq[4], cd[1], cw[3], vq[4], vd[1], vw[3], o[4];
+    t.gather(q0, cq);
+    t.gather(dt, cd);
+    t.gather(w, cw);
+    t.to_lanes(cq, vq);
+    t.to_lanes(cd, vd);
+    t.to_lanes(cw, vw);
+    d_rk4(0, vq, vd, vw, o);
+    t.store(out, o);
     done.signal();  // the whole block reaches this point (no early return)
 }
 
@@ -43,8 +59,11 @@ __device__ __forceinline__ void d_jac_a(int64_t i, const double *w, double *A) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_jac_a(int64_t n, const double *w, double *A, Done done) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) d_jac_a(i, w, A);
+    PEKF_TILE(t, 16, n);
+    double vw[3], o[16];
+    t.load(w, vw);
+    d_jac_a(0, vw, o);
+    t.store(A, o);
     done.signal();  // the whole block reaches this point (no early return)
 }
 
@@ -53,8 +72,11 @@ __device__ __forceinline__ void d_jac_b(int64_t i, const double *q, double *J) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_jac_b(int64_t n, const double *q, double *J, Done done) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) d_jac_b(i, q, J);
+    PEKF_TILE(t, 12, n);
+    double vq[4], o[12];
+    t.load(q, vq);
+    d_jac_b(0, vq, o);
+    t.store(J, o);
     done.signal();  // the whole block reaches this point (no early return)
 }
 
@@ -69,41 +91,57 @@ __device__ __forceinline__ void d_comparator(int64_t i, const double *q1,
 
 __global__ __launch_bounds__(kBlock) void k_comparator(int64_t n, const double *q1,
                                                       const double *q2, double *out, Done done) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) d_comparator(i, q1, q2, out);
+    PEKF_TILE(t, 4, n);
+    double c1[4], c2[4], v1[4], v2[4], o[4];
+    t.gather(q1, c1);
+    t.gather(q2, c2);
+    t.to_lanes(c1, v1);
+    t.to_lanes(c2, v2);
+    d_comparator(0, v1, v2, o);
+    t.store(out, o);
     done.signal();  // the whole block reaches this point (no early return)
 }
 
-// KalmanFilter.Prediction (ExtendedKalmanFilter.py:58-68)
-__device__ __forceinline__ void d_predict(int64_t i, const double *gyro,
-                                                   const double *dt, const double *X,
-                                                   const double *P, const double *Q,
-                                                   const double *R, double *z, double *Pm,
-                                                   double *K, int32_t *status) {
-    double A[16], At[16], Jb[12], Jbt[12], t16[16], a16[16], t12[12], b16[16], S[16], Si[16], pm[16];
-    omega_half(gyro + 3 * i, A);
-    xi_half(X + 4 * i, Jb);
+// KalmanFilter.Prediction (ExtendedKalmanFilter.py:58-68), in two phases so that a batched
+// kernel needs R only once P^- is formed.  Phase 1: P^- = A P A^T + Jb Q Jb^T (:59-61).
+__device__ __forceinline__ void d_predict_cov(const double *gyro, const double *X, const double *P,
+                                              const double *Q, double *pm) {
+    double A[16], At[16], Jb[12], Jbt[12], t16[16], a16[16], t12[12], b16[16];
+    omega_half(gyro, A);
+    xi_half(X, Jb);
     transpose<4, 4>(A, At);
     transpose<4, 3>(Jb, Jbt);
-    matmul<4, 4, 4>(A, P + 16 * i, t16);
+    matmul<4, 4, 4>(A, P, t16);
     matmul<4, 4, 4>(t16, At, a16);
-    matmul<4, 3, 3>(Jb, Q + 9 * i, t12);
+    matmul<4, 3, 3>(Jb, Q, t12);
     matmul<4, 3, 4>(t12, Jbt, b16);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        pm[k] = a16[k] + b16[k];
-        S[k] = pm[k] + R[16 * i + k];
-        Pm[16 * i + k] = pm[k];
-    }
-    rk4_literal(X + 4 * i, dt[i], gyro + 3 * i, z + 4 * i);
+    for (int k = 0; k < 16; ++k) pm[k] = a16[k] + b16[k];
+}
+
+// Phase 2: z = RK4 (:62), S = P^- + R, K = P^- inv(S) (:63-66); status 1 = singular S.
+__device__ __forceinline__ void d_predict_gain(const double *gyro, const double *dt, const double *X,
+                                               const double *pm, const double *R, double *z, double *K,
+                                               int32_t *status) {
+    double S[16], Si[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) S[k] = pm[k] + R[k];
+    rk4_literal(X, dt[0], gyro, z);
     const bool ok = inverse4(S, Si);
-    if (status) status[i] = ok ? 0 : 1;
+    *status = ok ? 0 : 1;
     if (!ok) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) K[16 * i + k] = NAN;
+        for (int k = 0; k < 16; ++k) K[k] = NAN;
         return;
     }
-    matmul<4, 4, 4>(pm, Si, K + 16 * i);
+    matmul<4, 4, 4>(pm, Si, K);
+}
+
+__device__ __forceinline__ void d_predict(const double *gyro, const double *dt, const double *X,
+                                          const double *P, const double *Q, const double *R, double *z,
+                                          double *Pm, double *K, int32_t *status) {
+    d_predict_cov(gyro, X, P, Q, Pm);
+    d_predict_gain(gyro, dt, X, Pm, R, z, K, status);
 }
 
 __global__ __launch_bounds__(kBlock) void k_predict(int64_t n, const double *gyro,
@@ -111,39 +149,79 @@ __global__ __launch_bounds__(kBlock) void k_predict(int64_t n, const double *gyr
                                                    const double *P, const double *Q,
                                                    const double *R, double *z, double *Pm,
                                                    double *K, int32_t *status, Done done) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) d_predict(i, gyro, dt, X, P, Q, R, z, Pm, K, status);
+    PEKF_TILE(t, 16, n);
+    // every operand's loads are issued up front (one memory round trip per wave)
+    double cg[3], cd[1], cx[4], cp[16], cq[9], cr[16], vg[3], vd[1], vx[4], vp[16], vq[9], vr[16];
+    t.gather(gyro, cg);
+    t.gather(dt, cd);
+    t.gather(X, cx);
+    t.gather(P, cp);
+    t.gather(Q, cq);
+    t.gather(R, cr);
+    t.to_lanes(cg, vg);
+    t.to_lanes(cd, vd);
+    t.to_lanes(cx, vx);
+    t.to_lanes(cp, vp);
+    t.to_lanes(cq, vq);
+    double opm[16];
+    d_predict_cov(vg, vx, vp, vq, opm);
+    t.store(Pm, opm);
+    t.to_lanes(cr, vr);
+    double oz[4], ok[16];
+    int32_t st = 0;
+    d_predict_gain(vg, vd, vx, opm, vr, oz, ok, &st);
+    t.store(z, oz);
+    t.store(K, ok);
+    if (status && t.active()) status[t.first + t.lane] = st;
     done.signal();  // the whole block reaches this point (no early return)
 }
 
-// KalmanFilter.Correction (ExtendedKalmanFilter.py:70-80)
-__device__ __forceinline__ void d_correct(int64_t i, const double *mag,
-                                                   const double *acc, const double *z,
-                                                   const double *P, const double *K,
-                                                   const double *acc0, const double *mag0,
-                                                   double *X, double *Pout, int32_t *status) {
-    const double *a = acc + 3 * i, *zz = z + 4 * i, *kk = K + 16 * i, *pp = P + 16 * i;
-    const double ka = fabs(a[2]);
-    if (status) status[i] = wahba_b_finite(acc0 + 3 * i, mag0 + 3 * i, a, mag + 3 * i, ka, 1.0 - ka) ? 0 : 1;
-    double R[9], y[4], e[4], ke[4], kp[16], x[4];
-    wahba_rotation_vectors(acc0 + 3 * i, mag0 + 3 * i, a, mag + 3 * i, ka, 1.0 - ka, R);
+// KalmanFilter.Correction (ExtendedKalmanFilter.py:70-80), in parts so that a batched kernel
+// can form P - K P before the Wahba solve and keep only K live across it.  Phase 1: Y = Wahba(Acc, Mag, |Acc_z|,
+// 1 - |Acc_z|) (:71), flipped when Y . z < 0 (:73-75); status 1 = non-finite B (SVD failure).
+__device__ __forceinline__ void d_correct_measure(const double *mag, const double *acc, const double *z,
+                                                  const double *acc0, const double *mag0, double *y,
+                                                  int32_t *status) {
+    const double ka = fabs(acc[2]);
+    *status = wahba_b_finite(acc0, mag0, acc, mag, ka, 1.0 - ka) ? 0 : 1;
+    double R[9];
+    wahba_rotation_vectors(acc0, mag0, acc, mag, ka, 1.0 - ka, R);
     rotm_to_quat(R, y);
-    const double cmp = y[0] * zz[0] + y[1] * zz[1] + y[2] * zz[2] + y[3] * zz[3];
+    const double cmp = y[0] * z[0] + y[1] * z[1] + y[2] * z[2] + y[3] * z[3];
     if (cmp < 0.0) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) y[k] = -y[k];
     }
+}
+
+// Phase 2: X = z + K (Y - z), X /= norm(X) (:76,78-79).
+__device__ __forceinline__ void d_correct_state(const double *y, const double *z, const double *K, double *X) {
+    double e[4], ke[4], x[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) e[k] = y[k] - zz[k];
-    matmul<4, 4, 1>(kk, e, ke);
+    for (int k = 0; k < 4; ++k) e[k] = y[k] - z[k];
+    matmul<4, 4, 1>(K, e, ke);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) x[k] = zz[k] + ke[k];
-    matmul<4, 4, 4>(kk, pp, kp);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) Pout[16 * i + k] = pp[k] - kp[k];
+    for (int k = 0; k < 4; ++k) x[k] = z[k] + ke[k];
     const double nrm = loop_norm4(x);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) X[4 * i + k] = x[k] / nrm;
+    for (int k = 0; k < 4; ++k) X[k] = x[k] / nrm;
+}
+
+// P = P - K P (:77): independent of the measurement.
+__device__ __forceinline__ void d_correct_cov(const double *P, const double *K, double *Pout) {
+    double kp[16];
+    matmul<4, 4, 4>(K, P, kp);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) Pout[k] = P[k] - kp[k];
+}
+
+__device__ __forceinline__ void d_correct(const double *mag, const double *acc, const double *z,
+                                          const double *P, const double *K, const double *acc0,
+                                          const double *mag0, double *X, double *Pout, int32_t *status) {
+    double y[4];
+    d_correct_measure(mag, acc, z, acc0, mag0, y, status);
+    d_correct_state(y, z, K, X);
+    d_correct_cov(P, K, Pout);
 }
 
 __global__ __launch_bounds__(kBlock) void k_correct(int64_t n, const double *mag,
@@ -151,8 +229,33 @@ __global__ __launch_bounds__(kBlock) void k_correct(int64_t n, const double *mag
                                                    const double *P, const double *K,
                                                    const double *acc0, const double *mag0,
                                                    double *X, double *Pout, int32_t *status, Done done) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) d_correct(i, mag, acc, z, P, K, acc0, mag0, X, Pout, status);
+    PEKF_TILE(t, 16, n);
+    // every operand's loads are issued up front (one memory round trip per wave); P - K P does
+    // not depend on the Wahba solve, so it is formed and stored first and only K stays live
+    double cp[16], ck[16], cm[3], ca[3], cz[4], cm0[3], ca0[3];
+    t.gather(P, cp);
+    t.gather(K, ck);
+    t.gather(mag, cm);
+    t.gather(acc, ca);
+    t.gather(z, cz);
+    t.gather(acc0, ca0);
+    t.gather(mag0, cm0);
+    double vp[16], vk[16], op[16];
+    t.to_lanes(cp, vp);
+    t.to_lanes(ck, vk);
+    d_correct_cov(vp, vk, op);
+    t.store(Pout, op);
+    double vm[3], va[3], vz[4], vm0[3], va0[3], y[4], ox[4];
+    t.to_lanes(cm, vm);
+    t.to_lanes(ca, va);
+    t.to_lanes(cz, vz);
+    t.to_lanes(ca0, va0);
+    t.to_lanes(cm0, vm0);
+    int32_t st = 0;
+    d_correct_measure(vm, va, vz, va0, vm0, y, &st);
+    d_correct_state(y, vz, vk, ox);
+    t.store(X, ox);
+    if (status && t.active()) status[t.first + t.lane] = st;
     done.signal();  // the whole block reaches this point (no early return)
 }
 
@@ -178,8 +281,25 @@ __global__ __launch_bounds__(kBlock) void k_wahba(int64_t n, const double *acc0,
                                                  const double *mag0, const double *acc,
                                                  const double *mag, const double *ka,
                                                  const double *km, double *out, int32_t *status, Done done) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) d_wahba<QUAT>(i, acc0, mag0, acc, mag, ka, km, out, status);
+    PEKF_TILE(t, 9, n);
+    double c0[3], c1[3], c2[3], c3[3], c4[1], c5[1], v0[3], v1[3], v2[3], v3[3], v4[1], v5[1];
+    t.gather(acc0, c0);
+    t.gather(mag0, c1);
+    t.gather(acc, c2);
+    t.gather(mag, c3);
+    t.gather(ka, c4);
+    t.gather(km, c5);
+    t.to_lanes(c0, v0);
+    t.to_lanes(c1, v1);
+    t.to_lanes(c2, v2);
+    t.to_lanes(c3, v3);
+    t.to_lanes(c4, v4);
+    t.to_lanes(c5, v5);
+    double o[QUAT ? 4 : 9];
+    int32_t st = 0;
+    d_wahba<QUAT>(0, v0, v1, v2, v3, v4, v5, o, &st);
+    t.store(out, o);
+    if (status && t.active()) status[t.first + t.lane] = st;
     done.signal();  // the whole block reaches this point (no early return)
 }
 
@@ -188,8 +308,11 @@ __device__ __forceinline__ void d_r2q(int64_t i, const double *M, double *q) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_r2q(int64_t n, const double *M, double *q, Done done) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) d_r2q(i, M, q);
+    PEKF_TILE(t, 9, n);
+    double vm[9], o[4];
+    t.load(M, vm);
+    d_r2q(0, vm, o);
+    t.store(q, o);
     done.signal();  // the whole block reaches this point (no early return)
 }
 
@@ -210,9 +333,9 @@ __global__ __launch_bounds__(64) void k_call1(Blob b, double *out, int32_t *stat
 #pragma unroll
         for (int k = 0; k < kBlobDoubles; ++k) v[k] = b.v[k];
         if (OP == kCallPredict)  // gyro 3, dt 1, X 4, P 16, Q 9, R 16 -> z 4, Pm 16, K 16
-            d_predict(0, v, v + 3, v + 4, v + 8, v + 24, v + 33, out, out + 4, out + 20, status);
+            d_predict(v, v + 3, v + 4, v + 8, v + 24, v + 33, out, out + 4, out + 20, status);
         else if (OP == kCallCorrect)  // mag 3, acc 3, z 4, P 16, K 16, acc0 3, mag0 3 -> X 4, P 16
-            d_correct(0, v, v + 3, v + 6, v + 10, v + 26, v + 42, v + 45, out, out + 4, status);
+            d_correct(v, v + 3, v + 6, v + 10, v + 26, v + 42, v + 45, out, out + 4, status);
         else  // acc0 3, mag0 3, acc 3, mag 3, ka 1, km 1 -> q 4
             d_wahba<true>(0, v, v + 3, v + 6, v + 9, v + 12, v + 13, out, status);
     }

@@ -87,6 +87,40 @@ def test_predict_singular_raises(eng):
         eng.predict(np.zeros(3), 1e7, [1.0, 0, 0, 0], np.zeros((4, 4)), np.zeros((3, 3)), np.zeros((4, 4)))
 
 
+def test_predict_singular_item_in_a_batch_raises(eng, kat):
+    args = [kat[k][:100].copy() for k in ("pc_gyro", "pc_dt", "pc_X", "pc_P", "pc_Q", "pc_R")]
+    args[3][77] = 0.0
+    args[4][77] = 0.0
+    args[5][77] = 0.0
+    with pytest.raises(np.linalg.LinAlgError):
+        eng.predict(*args)
+
+
+@pytest.mark.parametrize("start,n", [(0, 1), (0, 2), (0, 63), (0, 64), (0, 65), (3, 130), (7, 249)])
+def test_percall_items_independent_of_tiling(eng, kat, start, n):
+    """The batched per-call kernels move operands in 64-item wave tiles (csrc/pekf_tile.hpp):
+    any slice -- short last tile, unaligned start, n = 1 (the by-value k_call1 launch) -- gives
+    the rows of the full-batch call bit for bit."""
+    sl = slice(start, start + n)
+    pc = [kat[k] for k in ("pc_gyro", "pc_dt", "pc_X", "pc_P", "pc_Q", "pc_R")]
+    full = eng.predict(*pc)
+    part = eng.predict(*[a[sl] for a in pc])
+    for f, p in zip(full, part):
+        assert np.array_equal(f[sl], p)
+    cc = [kat[k] for k in ("pc_mag", "pc_acc", "pc_z", "pc_Pm", "pc_K", "pc_acc0", "pc_mag0")]
+    for f, p in zip(eng.correct(*cc), eng.correct(*[a[sl] for a in cc])):
+        assert np.array_equal(f[sl], p)
+    wa = [kat[k] for k in ("wahba_acc0", "wahba_mag0", "wahba_acc", "wahba_mag", "wahba_ka", "wahba_km")]
+    assert np.array_equal(eng.wahba_quaternion(*wa)[sl], eng.wahba_quaternion(*[a[sl] for a in wa]))
+    assert np.array_equal(eng.wahba_rotation(*wa)[sl], eng.wahba_rotation(*[a[sl] for a in wa]))
+    rk = [kat[k] for k in ("rk4_q0", "rk4_dt", "rk4_w")]
+    assert np.array_equal(eng.rk4(*rk)[sl], eng.rk4(*[a[sl] for a in rk]))
+    assert np.array_equal(eng.rotmat_to_quat(kat["r2q_M"])[sl], eng.rotmat_to_quat(kat["r2q_M"][sl]),
+                          equal_nan=True)
+    jq = np.concatenate([kat["jac_q"]] * 4)
+    assert np.array_equal(eng.jacobian_b(jq)[sl], eng.jacobian_b(jq[sl]))   # W = 12: the general slot path
+
+
 def test_empty_batch_is_noop(eng):
     assert eng.rk4(np.zeros((0, 4)), np.zeros(0), np.zeros((0, 3))).shape == (0, 4)
 
