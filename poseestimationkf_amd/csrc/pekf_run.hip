@@ -13,6 +13,7 @@
 
 #include "pekf_internal.hpp"
 #include "pekf_math.hpp"
+#include "pekf_tile.hpp"
 
 namespace pekf {
 
@@ -64,6 +65,19 @@ __device__ __forceinline__ void store_state(double *X, double *P, int64_t b, int
         po[8] = S.a02; po[9] = S.a12; po[10] = S.a22; po[11] = S.a23;
         po[12] = S.a03; po[13] = S.a13; po[14] = S.a23; po[15] = S.a33;
     }
+}
+
+// AoS P (full 4x4) <-> its upper triangle, for state moved through a WaveTile
+template <typename PT>
+__device__ __forceinline__ Sym4T<PT> sym_from16(const double (&p)[16]) {
+    return {(PT)p[0], (PT)p[1], (PT)p[2], (PT)p[3], (PT)p[5], (PT)p[6], (PT)p[7], (PT)p[10], (PT)p[11], (PT)p[15]};
+}
+template <typename PT>
+__device__ __forceinline__ void sym_to16(const Sym4T<PT> &S, double (&p)[16]) {
+    p[0] = S.a00; p[1] = S.a01; p[2] = S.a02; p[3] = S.a03;
+    p[4] = S.a01; p[5] = S.a11; p[6] = S.a12; p[7] = S.a13;
+    p[8] = S.a02; p[9] = S.a12; p[10] = S.a22; p[11] = S.a23;
+    p[12] = S.a03; p[13] = S.a13; p[14] = S.a23; p[15] = S.a33;
 }
 
 // One record of main_file.py:42-45 -- Prediction(gyro, T) then Correction(mag, acc) -- on the
@@ -135,6 +149,45 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
                                                    double qs, double rs, double *__restrict__ traj,
                                                    const int32_t *__restrict__ counts) {
     using PT = typename std::conditional<MIXED, float, double>::type;
+    if constexpr (ONE && !SOA) {
+        // one-record launch on AoS state: the state is most of the traffic, so it moves in
+        // coalesced wave tiles (pekf_tile.hpp) instead of 128 B-strided per-lane accesses
+        __shared__ double pool[kRunBlock / kWave * tile_doubles<16>()];
+        const WaveTile t(pool, tile_doubles<16>(), batch);
+        double cx[4], cp[16], cr[6];
+        t.gather(Xio, cx);
+        t.gather(Pio, cp);
+        t.gather(refs, cr);
+        const bool act = t.active();
+        const uint32_t lane = act ? (uint32_t)(t.first + t.lane) : 0u;  // idle lanes read a valid row
+        const int64_t base = (step0 % window) * batch;
+        const Rec cur = {(gd + base)[lane], (am + base)[lane], (my + base)[lane]};
+        const bool run = act && (!COUNTS || counts[lane] > 0);
+        double x[4], pv[16], rf[6];
+        t.to_lanes(cx, x);
+        t.to_lanes(cp, pv);
+        t.to_lanes(cr, rf);
+        Frame Wf;
+        make_frame<true>(rf, rf + 3, Wf);
+        Sym4T<PT> P = sym_from16<PT>(pv);
+        if (run) {
+            const double hw[3] = {0.5 * (double)cur.gd.x, 0.5 * (double)cur.gd.y, 0.5 * (double)cur.gd.z};
+            const uint32_t word = __float_as_uint(cur.gd.w);
+            const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
+            const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
+            ekf_record_step<PT>(x, P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), rs, hw,
+                                (double)(word & 0x7FFFFFFFu), (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
+        }
+        if (TRAJ && act) {
+            double2 *o = reinterpret_cast<double2 *>(traj) + 2 * (int64_t)lane;
+            o[0] = make_double2(x[0], x[1]);
+            o[1] = make_double2(x[2], x[3]);
+        }
+        sym_to16(P, pv);
+        t.store(Xio, x);
+        t.store(Pio, pv);
+        return;
+    }
     const int64_t b = (int64_t)blockIdx.x * kRunBlock + threadIdx.x;
     if (b >= batch) return;
     const int64_t my_steps = COUNTS ? (counts[b] < n_steps ? (int64_t)counts[b] : n_steps) : n_steps;
@@ -207,27 +260,40 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
 }
 
 // AoS <-> SoA state conversion (see load_state); P's 10 unique entries are the upper triangle.
-__global__ __launch_bounds__(kRunBlock) void k_state_layout(int64_t batch, const double *Xa, const double *Pa,
+// (the AoS side in coalesced wave tiles: this kernel is pure data movement)
+__global__ __launch_bounds__(kRunBlock) void k_state_layout(int64_t batch, double *Xa, double *Pa,
                                                             double *Xs, double *Ps, int to_soa) {
-    const int64_t b = (int64_t)blockIdx.x * kRunBlock + threadIdx.x;
-    if (b >= batch) return;
-    double x[4];
-    Sym4T<double> S;
-    if (to_soa) {
-        load_state<false>(Xa, Pa, b, batch, x, S);
-        store_state<true>(Xs, Ps, b, batch, x, S);
+    __shared__ double pool[kRunBlock / kWave * tile_doubles<16>()];
+    const WaveTile tl(pool, tile_doubles<16>(), batch);
+    const bool act = tl.active();
+    const int64_t b = tl.first + tl.lane;
+    double x[4], pv[16];
+    if (to_soa) {  // uniform
+        double cx[4], cp[16];
+        tl.gather(Xa, cx);
+        tl.gather(Pa, cp);
+        tl.to_lanes(cx, x);
+        tl.to_lanes(cp, pv);
+        if (act) store_state<true>(Xs, Ps, b, batch, x, sym_from16<double>(pv));
     } else {
-        load_state<true>(Xs, Ps, b, batch, x, S);
-        store_state<false>(const_cast<double *>(Xa), const_cast<double *>(Pa), b, batch, x, S);
+        Sym4T<double> S = {};
+        x[0] = x[1] = x[2] = x[3] = 0.0;
+        if (act) load_state<true>(Xs, Ps, b, batch, x, S);
+        sym_to16(S, pv);
+        tl.store(Xa, x);
+        tl.store(Pa, pv);
     }
 }
 
 __global__ __launch_bounds__(kRunBlock) void k_reset(int64_t batch, double *X, double *P) {
-    const int64_t b = (int64_t)blockIdx.x * kRunBlock + threadIdx.x;
-    if (b >= batch) return;
-    X[4 * b] = 1.0; X[4 * b + 1] = 0.0; X[4 * b + 2] = 0.0; X[4 * b + 3] = 0.0;
+    __shared__ double pool[kRunBlock / kWave * tile_doubles<16>()];
+    const WaveTile tl(pool, tile_doubles<16>(), batch);
+    const double x[4] = {1.0, 0.0, 0.0, 0.0};
+    double pv[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) P[16 * b + k] = (k % 5 == 0) ? 1.0 : 0.0;
+    for (int k = 0; k < 16; ++k) pv[k] = (k % 5 == 0) ? 1.0 : 0.0;
+    tl.store(X, x);
+    tl.store(P, pv);
 }
 
 // One record per filter from FP64 arrays (the filter handle's online update,
@@ -243,31 +309,51 @@ __global__ __launch_bounds__(kRunBlock) void k_update(int64_t batch, const doubl
                                                       double *__restrict__ Xio, double *__restrict__ Pio, double qs,
                                                       double rs, double *__restrict__ x_out) {
     using PT = typename std::conditional<MIXED, float, double>::type;
-    const int64_t b = (int64_t)blockIdx.x * kRunBlock + threadIdx.x;
-    if (b >= batch) return;
-    Frame Wf;
-    {
-        const double a0[3] = {refs[6 * b + 0], refs[6 * b + 1], refs[6 * b + 2]};
-        const double m0[3] = {refs[6 * b + 3], refs[6 * b + 4], refs[6 * b + 5]};
-        make_frame<true>(a0, m0, Wf);
-    }
+    // the [batch][3] / [batch][6] operands (and AoS state) move in coalesced wave tiles
+    constexpr int kW = SOA ? 6 : 16;
+    __shared__ double pool[kRunBlock / kWave * tile_doubles<kW>()];
+    const WaveTile tl(pool, tile_doubles<kW>(), batch);
+    const bool act = tl.active();
+    const int64_t b = act ? tl.first + tl.lane : 0;  // idle lanes compute on filter 0, store nothing
+    double cr[6], cg[3], ca[3], cm[3];
+    tl.gather(refs, cr);
+    tl.gather(gyro, cg);
+    tl.gather(acc, ca);
+    tl.gather(mag, cm);
     double x[4];
     Sym4T<PT> P;
-    load_state<SOA>(Xio, Pio, b, batch, x, P);
+    double pv[16];
+    if constexpr (SOA) {
+        load_state<true>(Xio, Pio, b, batch, x, P);
+    } else {
+        double cx[4], cp[16];
+        tl.gather(Xio, cx);
+        tl.gather(Pio, cp);
+        tl.to_lanes(cx, x);
+        tl.to_lanes(cp, pv);
+        P = sym_from16<PT>(pv);
+    }
     const int64_t t = t_ns[b];
     const double dt_ns = (double)(t - prev_t[b]);
-    prev_t[b] = t;
-    const double hw[3] = {0.5 * gyro[3 * b], 0.5 * gyro[3 * b + 1], 0.5 * gyro[3 * b + 2]};
-    const double a[3] = {acc[3 * b], acc[3 * b + 1], acc[3 * b + 2]};
-    const double m[3] = {mag[3 * b], mag[3 * b + 1], mag[3 * b + 2]};
-    ekf_record_step<PT>(x, P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), rs, hw, dt_ns,
-                        missing && missing[b], a, m);
-    store_state<SOA>(Xio, Pio, b, batch, x, P);
-    if (x_out) {
-        double2 *o = reinterpret_cast<double2 *>(x_out) + 2 * b;
-        o[0] = make_double2(x[0], x[1]);
-        o[1] = make_double2(x[2], x[3]);
+    const bool miss = missing && missing[b];
+    double rf[6], g[3], a[3], m[3];
+    tl.to_lanes(cr, rf);
+    tl.to_lanes(cg, g);
+    tl.to_lanes(ca, a);
+    tl.to_lanes(cm, m);
+    Frame Wf;
+    make_frame<true>(rf, rf + 3, Wf);
+    const double hw[3] = {0.5 * g[0], 0.5 * g[1], 0.5 * g[2]};
+    ekf_record_step<PT>(x, P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), rs, hw, dt_ns, miss, a, m);
+    if (act) prev_t[b] = t;
+    if constexpr (SOA) {
+        if (act) store_state<true>(Xio, Pio, b, batch, x, P);
+    } else {
+        sym_to16(P, pv);
+        tl.store(Xio, x);
+        tl.store(Pio, pv);
     }
+    if (x_out) tl.store(x_out, x);
 }
 
 int launch_update(int64_t batch, const double *gyro, const int64_t *t_ns, const double *acc, const double *mag,

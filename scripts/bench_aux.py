@@ -177,6 +177,28 @@ def main():
         del f1
     del win1
 
+    # ---- filter handle: one FP64 record per filter per pekf_filter_update_dev (device pointers).
+    # Bytes: gyro/acc/mag 72 + t 8 + prev_t 8+8 + refs 48 + state (AoS 32+128 / SoA 32+80) read and
+    # written + X_out 32.
+    rng = np.random.default_rng(3)
+    a0 = rng.normal(size=(B1, 3))
+    m0 = rng.normal(size=(B1, 3))
+    ub = {k: engine.DeviceBuffer(8 * B1 * w).upload(np.ascontiguousarray(rng.normal(size=(B1, w)) if w == 3 else
+                                                                          np.full((B1, 1), 10_000_000, np.int64)))
+          for k, w in (("g", 3), ("a", 3), ("m", 3), ("t", 1))}
+    xo = engine.DeviceBuffer(32 * B1)
+    for layout, st_b in (("aos", 2 * (32 + 128)), ("soa", 2 * (32 + 80))):
+        h = engine.FilterHandle(a0, m0, layout=layout)
+        per = 72 + 8 + 16 + 48 + st_b + 32
+        ms = timed(lambda: check(lib.pekf_filter_update_dev(h.h, ub["g"].ptr, ub["t"].ptr, ub["a"].ptr, ub["m"].ptr,
+                                                            None, xo.ptr, s)), s, reps=20)
+        res["handle_update_" + layout] = {
+            "filters": B1, "kernel_ms": ms, "updates_per_s": B1 / (ms * 1e-3), "bytes_per_filter": per,
+            "gbs": B1 * per / (ms * 1e-3) / 1e9, "hbm_frac": B1 * per / (ms * 1e-3) / 1e9 / HBM}
+        log("handle update %s (1M filters, FP64 records): %.3f ms" % (layout, ms))
+        del h
+    del ub, xo
+
     # ---- per-call operators at n = 1M (device pointers)
     n = 1 << 20
     rng = np.random.default_rng(0)
