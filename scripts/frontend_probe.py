@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""The front-end kernel alone (the bench_aux.py workload: 16K generated event streams tiled x64 ->
+1,048,576 filters x 1,024 events), for rocprofv3 PMC passes that should see only k_frontend.
+
+usage: python3 scripts/frontend_probe.py [reps]
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from poseestimationkf_amd import engine, synth  # noqa: E402
+from poseestimationkf_amd._lib import check, lib  # noqa: E402
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    st = engine.Stream()
+    s = st.handle
+    K0, E, tile = 16384, 1024, 64
+    ev = synth.generate_events(np.arange(K0), E, seed=11)
+    planes = np.ascontiguousarray(np.tile(synth.pack_events(ev), (1, tile, 1)))
+    K = K0 * tile
+    init = np.tile(np.concatenate([ev["init_acc"], ev["init_mag"]], axis=1), (tile, 1))
+    tinit = np.tile(ev["t_init"], tile)
+    evb = engine.DeviceBuffer(planes.nbytes).upload(planes)
+    ib = engine.DeviceBuffer(init.nbytes).upload(init)
+    tb = engine.DeviceBuffer(tinit.nbytes).upload(tinit.astype(np.int64))
+    r_max = E // 3 + 1
+    win = engine.IMUWindow(K, r_max)
+    cnt = engine.DeviceBuffer(4 * K)
+    err = engine.DeviceBuffer(4).upload(np.zeros(1, np.int32))
+    e0, e1 = engine.Event(), engine.Event()
+    times = []
+    for _ in range(reps):
+        e0.record(s)
+        check(lib.pekf_frontend_dev(K, E, evb.ptr, ib.ptr, tb.ptr, 0.1, r_max, win.gd.ptr, win.am.ptr,
+                                    win.my.ptr, cnt.ptr, win.refs.ptr, err.ptr, s))
+        e1.record(s)
+        e1.sync()
+        times.append(e0.elapsed_ms(e1))
+    recs = int(cnt.download((K,), np.int32).sum())
+    print("frontend_probe: %d filters x %d events, %d records, ms %s" % (K, E, recs, ["%.3f" % t for t in times]))
+
+
+if __name__ == "__main__":
+    main()
