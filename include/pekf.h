@@ -78,6 +78,18 @@ int pekf_event_elapsed_ms(float *ms, void *start, void *stop);
  * One GPU thread per item.  These are the drop-in replacements for the reference's
  * per-timestep methods; at n = 1 they serve main_file.py through the Python shims. */
 
+/* How n = 1 calls of pekf_predict / pekf_correct / pekf_wahba_quaternion (one record of
+ * main_file.py:38-45 at a time) reach the GPU:
+ *   PEKF_PERCALL_SERVICE (default): a resident one-wave kernel answers requests posted in
+ *     coherent pinned host memory (~4 us round trip instead of a launch); it ends by itself
+ *     after 5 ms without requests and before pekf_device_sync, and is restarted on demand.
+ *   PEKF_PERCALL_LAUNCH: one kernel launch per call (also selected by PEKF_PERCALL=launch).
+ * Both run the same device code, so results are identical. */
+#define PEKF_PERCALL_SERVICE 0
+#define PEKF_PERCALL_LAUNCH 1
+int pekf_set_percall_mode(int mode);
+int pekf_get_percall_mode(int *mode);
+
 /* KalmanFilter.RungeKutta4(q_0, T, w), ExtendedKalmanFilter.py:25-41.
  * q0[n*4], dt_ns[n] (nanoseconds; dt = dt_ns * 1e-9 as at :32), w[n*3] -> q_out[n*4]. */
 int pekf_rk4(int64_t n, const double *q0, const double *dt_ns, const double *w, double *q_out);

@@ -56,6 +56,8 @@ SIGNATURES = {
     "pekf_stream_destroy": [_vp],
     "pekf_stream_sync": [_vp],
     "pekf_device_sync": [],
+    "pekf_set_percall_mode": [_int],
+    "pekf_get_percall_mode": [ctypes.POINTER(_int)],
     "pekf_event_create": [ctypes.POINTER(_vp)],
     "pekf_event_destroy": [_vp],
     "pekf_event_record": [_vp, _vp],

@@ -239,6 +239,7 @@ int pekf_stream_sync(void *stream) {
 }
 
 int pekf_device_sync(void) {
+    service_quiesce_all();
     PEKF_HIP(hipDeviceSynchronize());
     return PEKF_OK;
 }

@@ -91,6 +91,10 @@ class Staging {
     int device_ = -1;
 };
 
+// Stops the resident per-call service kernel (pekf_percall.hip) of every device, e.g. before a
+// device-wide synchronisation, which would otherwise wait for its idle limit.
+void service_quiesce_all();
+
 // Filter-handle update kernel launcher (pekf_run.hip): one FP64 record per filter.
 int launch_update(int64_t batch, const double *gyro, const int64_t *t_ns, const double *acc, const double *mag,
                   const uint8_t *missing, const double *refs, int64_t *prev_t, double *X, double *P, double q,

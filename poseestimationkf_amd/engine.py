@@ -101,6 +101,20 @@ def device_name(dev=0):
     return buf.value.decode()
 
 
+PERCALL_SERVICE, PERCALL_LAUNCH = 0, 1
+
+
+def percall_mode(mode=None):
+    """How n = 1 per-call operators reach the GPU (include/pekf.h): PERCALL_SERVICE (a resident
+    kernel answering requests in pinned host memory, the default) or PERCALL_LAUNCH (one launch
+    per call).  Sets the mode when given; returns the mode in effect."""
+    if mode is not None:
+        check(lib.pekf_set_percall_mode(int(mode)))
+    m = ctypes.c_int()
+    check(lib.pekf_get_percall_mode(ctypes.byref(m)))
+    return m.value
+
+
 # ------------------------------------------------------------------ recorded traces (host ingest)
 
 def read_log_records(path):

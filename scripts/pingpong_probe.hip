@@ -1,0 +1,89 @@
+// pingpong_probe.hip -- diagnostic: host <-> resident-kernel round trip through coherent mapped
+// pinned memory (the host posts a request word, one resident lane polls it, answers with a
+// response word), against the launch-per-call round trip of sync_probe.hip.
+// The resident kernel always ends: it exits after `n` requests or after an idle period measured
+// on the constant-rate wall clock.
+// build: hipcc --offload-arch=gfx950 -O2 scripts/pingpong_probe.hip -o build/pingpong_probe
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <vector>
+
+#define CK(x)                                                                   \
+    do {                                                                        \
+        hipError_t e_ = (x);                                                    \
+        if (e_ != hipSuccess) {                                                 \
+            std::printf("%s failed: %s\n", #x, hipGetErrorString(e_));          \
+            return 1;                                                           \
+        }                                                                       \
+    } while (0)
+
+__global__ void k_resident(unsigned *req, unsigned *resp, const double *in, double *out, unsigned n,
+                           unsigned long long idle_ticks, int sleep) {
+    if (threadIdx.x != 0) return;
+    unsigned last = 0;
+    unsigned long long t0 = wall_clock64();
+    while (last < n) {
+        const unsigned r = __hip_atomic_load(req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (r != last) {
+            double v[4];
+            for (int k = 0; k < 4; ++k) v[k] = __hip_atomic_load(in + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            for (int k = 0; k < 4; ++k) __hip_atomic_store(out + k, v[k] * 2.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(resp, r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            last = r;
+            t0 = wall_clock64();
+        } else {
+            if (wall_clock64() - t0 > idle_ticks) break;
+            if (sleep) __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
+int main() {
+    int rate_khz = 0;
+    CK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0));
+    std::printf("wall clock rate: %d kHz\n", rate_khz);
+    char *host, *hdev;
+    CK(hipHostMalloc(&host, 8192, hipHostMallocMapped | hipHostMallocCoherent));
+    CK(hipHostGetDevicePointer(reinterpret_cast<void **>(&hdev), host, 0));
+    volatile unsigned *hreq = reinterpret_cast<volatile unsigned *>(host);
+    volatile unsigned *hresp = reinterpret_cast<volatile unsigned *>(host + 4096);
+    unsigned *dreq = reinterpret_cast<unsigned *>(hdev), *dresp = reinterpret_cast<unsigned *>(hdev + 4096);
+    double *din = reinterpret_cast<double *>(hdev + 256), *dout = reinterpret_cast<double *>(hdev + 4096 + 256);
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const unsigned long long idle = (unsigned long long)rate_khz * 200;  // 200 ms
+    for (int sleep = 0; sleep < 2; ++sleep) {
+        const unsigned N = 3000;
+        *hreq = 0;
+        *hresp = 0;
+        hipLaunchKernelGGL(k_resident, dim3(1), dim3(64), 0, s, dreq, dresp, din, dout, N, idle, sleep);
+        CK(hipGetLastError());
+        std::vector<double> us;
+        bool lost = false;
+        for (unsigned i = 1; i <= N && !lost; ++i) {
+            auto t0 = std::chrono::steady_clock::now();
+            __atomic_store_n(hreq, i, __ATOMIC_RELEASE);
+            while (__atomic_load_n(hresp, __ATOMIC_ACQUIRE) != i) {
+                if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 0.1) {
+                    lost = true;
+                    break;
+                }
+            }
+            us.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+        }
+        CK(hipStreamSynchronize(s));
+        if (lost) {
+            std::printf("sleep=%d: no response within 100 ms\n", sleep);
+            continue;
+        }
+        std::vector<double> tail(us.begin() + 500, us.end());
+        std::sort(tail.begin(), tail.end());
+        std::printf("resident round trip (s_sleep %d): median %.2f us  p10 %.2f  p90 %.2f  p99 %.2f\n", sleep,
+                    tail[tail.size() / 2], tail[tail.size() / 10], tail[tail.size() * 9 / 10],
+                    tail[tail.size() * 99 / 100]);
+    }
+    return 0;
+}

@@ -1,0 +1,116 @@
+"""n = 1 per-call operators through the resident service kernel vs one launch per call.
+
+The drop-in modules make one call per record (main_file.py:38-45).  By default those calls are
+answered by a resident one-wave kernel polling pinned host memory (csrc/pekf_percall.hip,
+`Service`); PEKF_PERCALL_LAUNCH launches k_call1 per call.  Both run the same device functions,
+so results must agree bit for bit with each other and with the batched kernels' rows.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from poseestimationkf_amd._lib import PEKF_ERR_INVALID, lib
+
+
+def test_mode_api_rejects_unknown_modes():
+    assert lib.pekf_set_percall_mode(7) == PEKF_ERR_INVALID
+    m = ctypes.c_int(-1)
+    assert lib.pekf_get_percall_mode(ctypes.byref(m)) == 0 and m.value in (0, 1)
+
+
+@pytest.fixture()
+def eng():
+    from poseestimationkf_amd import engine
+    from poseestimationkf_amd._lib import device_count
+    assert device_count() > 0, "GPU tests need a HIP device"
+    prev = engine.percall_mode()
+    yield engine
+    engine.percall_mode(prev)
+
+
+def _pc(kat, i):
+    p = [kat[k][i] for k in ("pc_gyro", "pc_dt", "pc_X", "pc_P", "pc_Q", "pc_R")]
+    c = [kat[k][i] for k in ("pc_mag", "pc_acc", "pc_z", "pc_Pm", "pc_K", "pc_acc0", "pc_mag0")]
+    w = [kat[k][i] for k in ("wahba_acc0", "wahba_mag0", "wahba_acc", "wahba_mag", "wahba_ka", "wahba_km")]
+    return p, c, w
+
+
+def _one_each(eng, kat, idx):
+    out = []
+    for i in idx:
+        p, c, w = _pc(kat, i)
+        out.append((eng.predict(*p), eng.correct(*c), eng.wahba_quaternion(*w)))
+    return out
+
+
+def _same(a, b):
+    for (p1, c1, w1), (p2, c2, w2) in zip(a, b):
+        for x, y in zip(p1 + c1 + (w1,), p2 + c2 + (w2,)):
+            assert np.array_equal(x, y, equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_service_and_launch_identical_and_match_batched_rows(eng, kat):
+    idx = range(0, 256, 7)
+    eng.percall_mode(eng.PERCALL_SERVICE)
+    svc = _one_each(eng, kat, idx)
+    eng.percall_mode(eng.PERCALL_LAUNCH)
+    lau = _one_each(eng, kat, idx)
+    _same(svc, lau)
+    full_p = eng.predict(*[kat[k] for k in ("pc_gyro", "pc_dt", "pc_X", "pc_P", "pc_Q", "pc_R")])
+    for j, i in enumerate(idx):
+        for f, x in zip(full_p, svc[j][0]):
+            assert np.array_equal(f[i], x.reshape(f[i].shape))
+
+
+@pytest.mark.gpu
+def test_service_survives_idle_exit_and_device_sync(eng, kat):
+    eng.percall_mode(eng.PERCALL_SERVICE)
+    ref = _one_each(eng, kat, [3])
+    time.sleep(0.03)               # past the service's 5 ms idle limit: the kernel has left
+    _same(ref, _one_each(eng, kat, [3]))
+    time.sleep(0.003)              # between half and the whole idle limit: restarted deliberately
+    _same(ref, _one_each(eng, kat, [3]))
+    assert lib.pekf_device_sync() == 0   # stops the resident kernel first, so this returns at once
+    _same(ref, _one_each(eng, kat, [3]))
+
+
+@pytest.mark.gpu
+def test_service_errors_like_the_reference(eng):
+    eng.percall_mode(eng.PERCALL_SERVICE)
+    with pytest.raises(np.linalg.LinAlgError):
+        eng.predict(np.zeros(3), 1e7, [1.0, 0, 0, 0], np.zeros((4, 4)), np.zeros((3, 3)), np.zeros((4, 4)))
+    with pytest.raises(np.linalg.LinAlgError):
+        eng.correct([np.nan, 0, 1], [0, 0, 1.0], [1.0, 0, 0, 0], np.eye(4), np.eye(4) * 0.5, [0, 0, 1.0], [1.0, 0, 0])
+    # and the service still answers afterwards
+    z, _, _ = eng.predict(np.zeros(3), 1e7, [1.0, 0, 0, 0], np.eye(4), np.eye(3), np.eye(4) * 0.1)
+    assert np.array_equal(z[0], np.array([1.0, 0, 0, 0]))
+
+
+@pytest.mark.gpu
+def test_service_from_several_threads(eng, kat):
+    eng.percall_mode(eng.PERCALL_SERVICE)
+    idx = list(range(64))
+    ref = _one_each(eng, kat, idx)
+    results, errors = {}, []
+
+    def worker(t):
+        try:
+            for _ in range(5):
+                results[t] = _one_each(eng, kat, idx[t::4])
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    assert not errors, errors
+    for t in range(4):
+        _same(ref[t::4], results[t])
