@@ -328,7 +328,39 @@ constexpr int kBlobDoubles = 64;
 struct Blob {
     double v[kBlobDoubles];
 };
-enum : int { kCallPredict = 0, kCallCorrect = 1, kCallWahbaQuat = 2 };
+enum : int {
+    kCallPredict = 0,    // gyro 3, dt 1, X 4, P 16, Q 9, R 16 -> z 4, Pm 16, K 16
+    kCallCorrect = 1,    // mag 3, acc 3, z 4, P 16, K 16, acc0 3, mag0 3 -> X 4, P 16
+    kCallWahbaQuat = 2,  // acc0 3, mag0 3, acc 3, mag 3, ka 1, km 1 -> q 4
+    kCallWahbaRot = 3,   // as above -> R 9
+    kCallRk4 = 4,        // q0 4, dt 1, w 3 -> q 4
+    kCallJacA = 5,       // w 3 -> A 16
+    kCallJacB = 6,       // q 4 -> Jb 12
+    kCallComparator = 7, // q1 4, q2 4 -> 4
+    kCallR2q = 8,        // M 9 -> q 4
+};
+constexpr int kCallMaxOut = 36;
+
+__host__ __device__ constexpr int call1_outputs(int op) {
+    return op == kCallPredict ? 36 : op == kCallCorrect ? 20 : op == kCallWahbaRot ? 9 : op == kCallJacA ? 16
+           : op == kCallJacB ? 12 : 4;
+}
+
+// One n = 1 call on lane-private operands (the operand order above); status stays 0 for the
+// operators that cannot fail.
+__device__ __forceinline__ void dispatch1(int op, const double *v, double *o, int32_t *st) {
+    switch (op) {
+        case kCallPredict: d_predict(v, v + 3, v + 4, v + 8, v + 24, v + 33, o, o + 4, o + 20, st); break;
+        case kCallCorrect: d_correct(v, v + 3, v + 6, v + 10, v + 26, v + 42, v + 45, o, o + 4, st); break;
+        case kCallWahbaQuat: d_wahba<true>(0, v, v + 3, v + 6, v + 9, v + 12, v + 13, o, st); break;
+        case kCallWahbaRot: d_wahba<false>(0, v, v + 3, v + 6, v + 9, v + 12, v + 13, o, st); break;
+        case kCallRk4: d_rk4(0, v, v + 4, v + 5, o); break;
+        case kCallJacA: d_jac_a(0, v, o); break;
+        case kCallJacB: d_jac_b(0, v, o); break;
+        case kCallComparator: d_comparator(0, v, v + 4, o); break;
+        default: d_r2q(0, v, o); break;
+    }
+}
 
 template <int OP>
 __global__ __launch_bounds__(64) void k_call1(Blob b, double *out, int32_t *status, Done done) {
@@ -336,12 +368,8 @@ __global__ __launch_bounds__(64) void k_call1(Blob b, double *out, int32_t *stat
         double v[kBlobDoubles];
 #pragma unroll
         for (int k = 0; k < kBlobDoubles; ++k) v[k] = b.v[k];
-        if (OP == kCallPredict)  // gyro 3, dt 1, X 4, P 16, Q 9, R 16 -> z 4, Pm 16, K 16
-            d_predict(v, v + 3, v + 4, v + 8, v + 24, v + 33, out, out + 4, out + 20, status);
-        else if (OP == kCallCorrect)  // mag 3, acc 3, z 4, P 16, K 16, acc0 3, mag0 3 -> X 4, P 16
-            d_correct(v, v + 3, v + 6, v + 10, v + 26, v + 42, v + 45, out, out + 4, status);
-        else  // acc0 3, mag0 3, acc 3, mag 3, ka 1, km 1 -> q 4
-            d_wahba<true>(0, v, v + 3, v + 6, v + 9, v + 12, v + 13, out, status);
+        *status = 0;
+        dispatch1(OP, v, out, status);
     }
     done.signal();
 }
@@ -393,10 +421,7 @@ __global__ __launch_bounds__(64) void k_service(char *box, unsigned long long id
         }
         sh[lane] = __longlong_as_double((long long)w);
         __syncthreads();
-        int n_out = 0;
-        if (op == kCallPredict) n_out = 36;
-        else if (op == kCallCorrect) n_out = 20;
-        else n_out = 4;
+        const int n_out = call1_outputs((int)op);
         if (lane == 0) {
             // the payload as the Blob of k_call1 (same operand order, same device functions)
             double v[kSvcPayload];
@@ -404,16 +429,11 @@ __global__ __launch_bounds__(64) void k_service(char *box, unsigned long long id
             for (int k = 0; k < 8; ++k)
 #pragma unroll
                 for (int j = 0; j < kSvcLinePayload; ++j) v[k * kSvcLinePayload + j] = sh[k * 8 + j];
-            double o[36] = {};
+            double o[kCallMaxOut] = {};
             int32_t st = 0;
-            if (op == kCallPredict)
-                d_predict(v, v + 3, v + 4, v + 8, v + 24, v + 33, o, o + 4, o + 20, &st);
-            else if (op == kCallCorrect)
-                d_correct(v, v + 3, v + 6, v + 10, v + 26, v + 42, v + 45, o, o + 4, &st);
-            else
-                d_wahba<true>(0, v, v + 3, v + 6, v + 9, v + 12, v + 13, o, &st);
+            dispatch1((int)op, v, o, &st);
 #pragma unroll
-            for (int k = 0; k < 36; ++k) sh[k] = o[k];  // static indices: o stays in registers
+            for (int k = 0; k < kCallMaxOut; ++k) sh[k] = o[k];  // static indices: o stays in registers
             sh_status = st;
         }
         __syncthreads();
@@ -692,6 +712,10 @@ int pekf_rk4(int64_t n, const double *q0, const double *dt_ns, const double *w, 
     if (n == 0) return PEKF_OK;
     PEKF_CHECK_ARG(q0 && dt_ns && w && q_out, "null pointer");
     if (int st = require_device()) return st;
+    if (n == 1) {
+        int32_t st1 = 0;
+        return call1<kCallRk4>({{q0, 32}, {dt_ns, 8}, {w, 24}}, {{q_out, 32}}, &st1);
+    }
     Staging &s = Staging::get();
     const size_t b = (size_t)n * sizeof(double);
     void *in[3], *out[1];
@@ -722,6 +746,10 @@ int pekf_jacobian_a(int64_t n, const double *w, double *A) {
     if (n == 0) return PEKF_OK;
     PEKF_CHECK_ARG(w && A, "null pointer");
     if (int st = require_device()) return st;
+    if (n == 1) {
+        int32_t st1 = 0;
+        return call1<kCallJacA>({{w, 24}}, {{A, 128}}, &st1);
+    }
     Staging &s = Staging::get();
     const size_t b = (size_t)n * sizeof(double);
     void *in[1], *out[1];
@@ -737,6 +765,10 @@ int pekf_jacobian_b(int64_t n, const double *q, double *Jb) {
     if (n == 0) return PEKF_OK;
     PEKF_CHECK_ARG(q && Jb, "null pointer");
     if (int st = require_device()) return st;
+    if (n == 1) {
+        int32_t st1 = 0;
+        return call1<kCallJacB>({{q, 32}}, {{Jb, 96}}, &st1);
+    }
     Staging &s = Staging::get();
     const size_t b = (size_t)n * sizeof(double);
     void *in[1], *out[1];
@@ -752,6 +784,10 @@ int pekf_comparator(int64_t n, const double *q1, const double *q2, double *res) 
     if (n == 0) return PEKF_OK;
     PEKF_CHECK_ARG(q1 && q2 && res, "null pointer");
     if (int st = require_device()) return st;
+    if (n == 1) {
+        int32_t st1 = 0;
+        return call1<kCallComparator>({{q1, 32}, {q2, 32}}, {{res, 32}}, &st1);
+    }
     Staging &s = Staging::get();
     const size_t b = (size_t)n * sizeof(double);
     void *in[2], *out[1];
@@ -838,12 +874,13 @@ static int wahba_host(bool quat, int64_t n, const double *acc0, const double *ma
     PEKF_CHECK_ARG(acc0 && mag0 && acc && mag && k_acc && k_mag && res, "null pointer");
     if (int st = require_device()) return st;
     const size_t b = (size_t)n * sizeof(double);
-    if (n == 1 && quat) {
+    if (n == 1) {
         int32_t st1 = 0;
-        if (int st = call1<kCallWahbaQuat>({{acc0, 3 * b}, {mag0, 3 * b}, {acc, 3 * b}, {mag, 3 * b}, {k_acc, b},
-                                            {k_mag, b}},
-                                           {{res, 4 * b}}, &st1))
-            return st;
+        const std::initializer_list<HostArg> ins = {{acc0, 3 * b}, {mag0, 3 * b}, {acc, 3 * b}, {mag, 3 * b},
+                                                    {k_acc, b}, {k_mag, b}};
+        const int st = quat ? call1<kCallWahbaQuat>(ins, {{res, 4 * b}}, &st1)
+                            : call1<kCallWahbaRot>(ins, {{res, 9 * b}}, &st1);
+        if (st) return st;
         return st1 ? set_error(PEKF_ERR_SVD, "SVD did not converge") : PEKF_OK;
     }
     Staging &s = Staging::get();
@@ -886,6 +923,10 @@ int pekf_rotmat_to_quat(int64_t n, const double *M, double *q) {
     if (n == 0) return PEKF_OK;
     PEKF_CHECK_ARG(M && q, "null pointer");
     if (int st = require_device()) return st;
+    if (n == 1) {
+        int32_t st1 = 0;
+        return call1<kCallR2q>({{M, 72}}, {{q, 32}}, &st1);
+    }
     Staging &s = Staging::get();
     const size_t b = (size_t)n * sizeof(double);
     void *in[1], *out[1];

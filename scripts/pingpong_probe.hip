@@ -85,5 +85,47 @@ int main() {
                     tail[tail.size() / 2], tail[tail.size() / 10], tail[tail.size() * 9 / 10],
                     tail[tail.size() * 99 / 100]);
     }
+    // Variant: the request word in fine-grained device memory written by the CPU through the
+    // BAR mapping (if the platform maps it), the response in pinned host memory.
+    unsigned *vreq = nullptr;
+    if (hipExtMallocWithFlags(reinterpret_cast<void **>(&vreq), 4096, hipDeviceMallocFinegrained) != hipSuccess) {
+        std::printf("fine-grained device memory: allocation failed\n");
+        return 0;
+    }
+    hipPointerAttribute_t attr;
+    CK(hipPointerGetAttributes(&attr, vreq));
+    std::printf("fine-grained device memory: device ptr %p host ptr %p\n", attr.devicePointer, attr.hostPointer);
+    if (!attr.hostPointer) return 0;
+    volatile unsigned *hv = reinterpret_cast<volatile unsigned *>(attr.hostPointer);
+    for (int sleep = 0; sleep < 2; ++sleep) {
+        const unsigned N = 3000;
+        *hv = 0;
+        *hresp = 0;
+        hipLaunchKernelGGL(k_resident, dim3(1), dim3(64), 0, s, vreq, dresp, din, dout, N, idle, sleep);
+        CK(hipGetLastError());
+        std::vector<double> us;
+        bool lost = false;
+        for (unsigned i = 1; i <= N && !lost; ++i) {
+            auto t0 = std::chrono::steady_clock::now();
+            __atomic_store_n(hv, i, __ATOMIC_RELEASE);
+            while (__atomic_load_n(hresp, __ATOMIC_ACQUIRE) != i) {
+                if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 0.1) {
+                    lost = true;
+                    break;
+                }
+            }
+            us.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+        }
+        CK(hipStreamSynchronize(s));
+        if (lost) {
+            std::printf("VRAM request, sleep=%d: no response within 100 ms\n", sleep);
+            continue;
+        }
+        std::vector<double> tail(us.begin() + 500, us.end());
+        std::sort(tail.begin(), tail.end());
+        std::printf("VRAM request round trip (s_sleep %d): median %.2f us  p10 %.2f  p90 %.2f  p99 %.2f\n", sleep,
+                    tail[tail.size() / 2], tail[tail.size() / 10], tail[tail.size() * 9 / 10],
+                    tail[tail.size() * 99 / 100]);
+    }
     return 0;
 }

@@ -40,17 +40,24 @@ def _pc(kat, i):
     return p, c, w
 
 
-def _one_each(eng, kat, idx):
+def _one_each(eng, kat, idx, every_op=False):
     out = []
     for i in idx:
         p, c, w = _pc(kat, i)
-        out.append((eng.predict(*p), eng.correct(*c), eng.wahba_quaternion(*w)))
+        r = eng.predict(*p) + eng.correct(*c) + (eng.wahba_quaternion(*w),)
+        if every_op:  # the other n = 1 entry points go the same way
+            j = i % 64
+            r += (eng.wahba_rotation(*w), eng.rk4(kat["rk4_q0"][i], kat["rk4_dt"][i], kat["rk4_w"][i]),
+                  eng.jacobian_a(kat["jac_w"][j]), eng.jacobian_b(kat["jac_q"][j]),
+                  eng.comparator(kat["cmp_q1"][j], kat["cmp_q2"][j]), eng.rotmat_to_quat(kat["r2q_M"][i]))
+        out.append(r)
     return out
 
 
 def _same(a, b):
-    for (p1, c1, w1), (p2, c2, w2) in zip(a, b):
-        for x, y in zip(p1 + c1 + (w1,), p2 + c2 + (w2,)):
+    for r1, r2 in zip(a, b):
+        assert len(r1) == len(r2)
+        for x, y in zip(r1, r2):
             assert np.array_equal(x, y, equal_nan=True)
 
 
@@ -58,13 +65,13 @@ def _same(a, b):
 def test_service_and_launch_identical_and_match_batched_rows(eng, kat):
     idx = range(0, 256, 7)
     eng.percall_mode(eng.PERCALL_SERVICE)
-    svc = _one_each(eng, kat, idx)
+    svc = _one_each(eng, kat, idx, every_op=True)
     eng.percall_mode(eng.PERCALL_LAUNCH)
-    lau = _one_each(eng, kat, idx)
+    lau = _one_each(eng, kat, idx, every_op=True)
     _same(svc, lau)
     full_p = eng.predict(*[kat[k] for k in ("pc_gyro", "pc_dt", "pc_X", "pc_P", "pc_Q", "pc_R")])
     for j, i in enumerate(idx):
-        for f, x in zip(full_p, svc[j][0]):
+        for f, x in zip(full_p, svc[j][:3]):
             assert np.array_equal(f[i], x.reshape(f[i].shape))
 
 
