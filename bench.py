@@ -215,7 +215,8 @@ def main():
         achieved = B * N * REC_BYTES / k_s / 1e9
         flop = ISA_COUNTS[args.precision]["flop"]
         valu = ISA_COUNTS[args.precision]["valu_instr"]
-        traffic, tsrc = measured_traffic(B, N) if args.precision == "f64" else (None, None)
+        # the committed PMC pass is of the FP64 command without missing records
+        traffic, tsrc = measured_traffic(B, N) if args.precision == "f64" and not args.missing else (None, None)
         clk = tsrc[1].get("effective_clock_ghz") if tsrc else None
         issue_frac = (4.0 * (B / 64.0) * N * valu / (1024 * clk * 1e9 * k_s)) if clk else None
         out = {
@@ -232,8 +233,7 @@ def main():
             "dtype": "f64" if args.precision == "f64" else "f64 quaternion path + f32 covariance (P, S^-1)",
             "data": "synthetic (on-device Philox IMU generator, bit-identical host mirror; 40 B records, "
                     "%d-record resident window replayed cyclically)" % W,
-            "config": {"workload": "config 5: batch=1,048,576/GPU, 30% missing-mag" if args.missing else
-                       "config 3: batch=1,048,576 filters/GPU x 10,000 records",
+            "config": {"workload": workload_name(B, N, args.missing),
                        "filters_per_gpu": B, "global_filters": B * world, "records_per_step": N,
                        "window_records": W, "parallelism": "dp%d (filter-batch shards, 1 RCCL gather)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -270,6 +270,16 @@ ISA_COUNTS = {"f64": {"flop": 551, "fp64_instr": 376, "valu_instr": 405},
               "mixed": {"flop": 272, "fp64_instr": 221, "valu_instr": 420}}  # mixed: + ~200 f32 instructions
 FLOP_PER_STEP = ISA_COUNTS["f64"]["flop"]
 FP64_INSTR_PER_STEP = ISA_COUNTS["f64"]["fp64_instr"]
+
+
+def workload_name(batch, records, missing):
+    """BASELINE.json's configuration this run is (configs 2, 3 and 5 are 10,000 records)."""
+    if records == 10000 and batch == 1 << 20:
+        return ("config 5: batch=1,048,576/GPU, 30% missing-mag" if missing else
+                "config 3: batch=1,048,576 filters/GPU x 10,000 records")
+    if records == 10000 and batch == 65536 and not missing:
+        return "config 2: batch=65,536 filters/GPU x 10,000 records"
+    return "custom: batch=%d filters/GPU x %d records%s" % (batch, records, ", 30% missing-mag" if missing else "")
 
 
 def measured_traffic(batch, records):
