@@ -584,7 +584,8 @@ class Service {
     char *box_ = nullptr, *box_dev_ = nullptr;
     unsigned long long idle_ticks_ = 0;
     uint32_t seq_ = 0;
-    bool running_ = false, broken_ = false;
+    std::atomic<bool> running_{false};  // read without the lock by quiesce_all
+    bool broken_ = false;
     std::chrono::steady_clock::time_point last_;
 };
 
@@ -593,7 +594,7 @@ void Service::quiesce_all() {
     Service *all = instances();
     int cur = -1;
     for (int d = 0; d < kMaxDevices; ++d) {
-        if (!__atomic_load_n(&all[d].running_, __ATOMIC_ACQUIRE)) continue;
+        if (!all[d].running_.load()) continue;
         if (cur < 0 && hipGetDevice(&cur) != hipSuccess) return;
         if (hipSetDevice(d) != hipSuccess) continue;
         all[d].quiesce();
