@@ -67,6 +67,11 @@ __device__ __forceinline__ void store_state(double *X, double *P, int64_t b, int
     }
 }
 
+// Buffer resource of one plane row (raw, byte-addressed; gfx9 DWORD3 0x00020000)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void *row, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(row), 0, (int)(uint32_t)bytes, 0x00020000);
+}
+
 // AoS P (full 4x4) <-> its upper triangle, for state moved through a WaveTile
 template <typename PT>
 __device__ __forceinline__ Sym4T<PT> sym_from16(const double (&p)[16]) {
@@ -205,15 +210,20 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     Sym4T<PT> P;
     load_state<SOA>(Xio, Pio, b, batch, x, P);
 
-    // Record of stream row r: the row base (r * batch) is wave-uniform (scalar registers); the
-    // lane adds only its 32-bit filter index (batch < 2^28 is checked on the host).
+    // Record of stream row r: raw buffer loads whose resource (the row's base address, scalar
+    // registers) is rebuilt per row and whose 32-bit lane offset is fixed, so no per-step vector
+    // address arithmetic (batch < 2^28 is checked on the host, so the offsets fit).
     const uint32_t lane = (uint32_t)b;
+    const uint32_t off16 = lane * 16u, off8 = lane * 8u;
     auto load_row = [&](int64_t r) -> Rec {
         const int64_t base = r * batch;
         Rec v;
-        v.gd = (gd + base)[lane];
-        v.am = (am + base)[lane];
-        v.my = (my + base)[lane];
+        const auto g4 = __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(gd + base, batch * 16), off16, 0, 0);
+        const auto a4 = __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(am + base, batch * 16), off16, 0, 0);
+        const auto m2 = __builtin_amdgcn_raw_buffer_load_b64(row_rsrc(my + base, batch * 8), off8, 0, 0);
+        v.gd = __builtin_bit_cast(float4, g4);
+        v.am = __builtin_bit_cast(float4, a4);
+        v.my = __builtin_bit_cast(float2, m2);
         return v;
     };
 
