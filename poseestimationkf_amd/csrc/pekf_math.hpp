@@ -288,6 +288,45 @@ PEKF_DEV void rotm_to_quat_fast(const double *M, double *q) {
     q[0] = v[0] * inv_s; q[1] = v[1] * inv_s; q[2] = v[2] * inv_s; q[3] = v[3] * inv_s;
 }
 
+// Y = RotationMatrix2Quart(M) flipped into z's hemisphere (Wahba.py:19-47, then
+// ExtendedKalmanFilter.py:73-75), for the fused kernel.  The four candidate numerators of
+// RotationMatrix2Quart are the columns of Q4 = 4 q q^T (diagonal 1 +- M00 +- M11 +- M22,
+// off-diagonal the sums / differences of M's off-diagonal pairs), so v = Q4 z = 4 q (q.z) is q
+// already carrying the sign of q.z: Y = v / |v|, no branch selects and no separate hemisphere
+// test.  |v| = 4 |q.z| |z|, so where q is nearly orthogonal to z (|q.z| < 1/4: the measured
+// attitude more than 150 degrees from the prediction) and where the reference's own branch
+// formula is ill-conditioned (a rotation within ~1e-5 rad of the identity, where it divides by
+// ~0 and, at the exact identity, returns NaN) the lane takes the reference's branch formula and
+// strict '<' flip instead.  Neither occurs on a tracked stream, so the fallback costs a wave
+// nothing unless one of its lanes needs it.
+PEKF_DEV void rotm_to_quat_toward(const double *M, const double *z, double *y) {
+    const double a = 1.0 + M[8], b = 1.0 - M[8], s = M[0] + M[4], d = M[0] - M[4];
+    const double t0 = a + s, t1 = b + d, t2 = b - d, t3 = a - s;
+    const double dw1 = M[7] - M[5], dw2 = M[2] - M[6], dw3 = M[3] - M[1];
+    const double sxy = M[1] + M[3], sxz = M[2] + M[6], syz = M[5] + M[7];
+    double v[4];
+    v[0] = fma(t0, z[0], fma(dw1, z[1], fma(dw2, z[2], dw3 * z[3])));
+    v[1] = fma(dw1, z[0], fma(t1, z[1], fma(sxy, z[2], sxz * z[3])));
+    v[2] = fma(dw2, z[0], fma(sxy, z[1], fma(t2, z[2], syz * z[3])));
+    v[3] = fma(dw3, z[0], fma(sxz, z[1], fma(syz, z[2], t3 * z[3])));
+    const double nv = fma(v[0], v[0], fma(v[1], v[1], fma(v[2], v[2], v[3] * v[3])));
+    double sc;
+#ifndef PEKF_ISA_COMMON_PATH  // (defined only by scripts/isa_count.py runs: the path a tracked lane takes)
+    if (nv < 1.0 || t0 > 4.0 - 1e-10) {
+#else
+    if (false) {
+#endif
+        // the reference's branch formula and hemisphere test (NaN operands never get here)
+        double inv_s;
+        rotm_to_quat_scaled(M, v, inv_s);
+        const double cmp = v[0] * z[0] + v[1] * z[1] + v[2] * z[2] + v[3] * z[3];
+        sc = cmp < 0.0 ? -inv_s : inv_s;
+    } else {
+        sc = rsqrt<true>(nv);
+    }
+    y[0] = v[0] * sc; y[1] = v[1] * sc; y[2] = v[2] * sc; y[3] = v[3] * sc;
+}
+
 // ------------------------------- fused-step forms --------------------------------------------
 // With R = rI the reference recursion (ExtendedKalmanFilter.py:61-66,76-78) is, exactly in
 // real arithmetic,
@@ -311,46 +350,49 @@ PEKF_DEV float recip(float x) {
     return fmaf(r, fmaf(-x, r, 1.0f), r);
 }
 
-// A P A^T + g (|x|^2 I - x x^T), A = Omega(h), h = w/2 (ExtendedKalmanFilter.py:44-47,52-55,61);
-// n2 = |x|^2 (shared with rk4_closed's normalisation)
+// Innovation covariance S = A P A^T + g (|x|^2 I - x x^T) + rI, A = Omega(h), h = w/2
+// (ExtendedKalmanFilter.py:44-47,52-55,61,63); n2 = |x|^2 (shared with rk4_closed's
+// normalisation), w = the raw gyro (= 2h), hq = h/2.
+//
+// Omega(h) is the matrix of right multiplication by the pure quaternion h, v -> v (x) h.  In the
+// basis {I, L(e_a) R(e_b)} (a, b = 1..3) of symmetric 4x4 matrices, P = c0 I + sum C_ab L(e_a) R(e_b)
+// with C_ab = tr(L(e_a) R(e_b) P) / 4, conjugation by R(h) maps e_b -> h e_b h^* = 2(h.e_b) h - |h|^2 e_b,
+// so C -> 2 (C h) h^T - |h|^2 C and
+//   A P A^T = 2 L(u) R(h) - |h|^2 P + 2 |h|^2 c0 I,   u = C h,
+//   L(u) R(h) = [[-u.h, (u x h)^T], [u x h, (u.h) I - u h^T - h u^T]].
+// u needs only the trace butterflies of P's diagonal and the sums / differences of its off-diagonal
+// pairs: 74 FP64 operations for S against 96 for the direct Omega P Omega^T + Jb Q Jb^T + rI.
 template <typename T>
-PEKF_DEV Sym4T<T> propagate_cov(const Sym4T<T> &P, const T *h, const T *x, T n2, T g) {
-    const T w0 = h[0], w1 = h[1], w2 = h[2];
-    // T = Omega P (full 4x4), rows of Omega: [0,-w0,-w1,-w2] [w0,0,w2,-w1] [w1,-w2,0,w0] [w2,w1,-w0,0]
-    const T p[4][4] = {{P.a00, P.a01, P.a02, P.a03},
-                            {P.a01, P.a11, P.a12, P.a13},
-                            {P.a02, P.a12, P.a22, P.a23},
-                            {P.a03, P.a13, P.a23, P.a33}};
-    T t[4][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        t[0][j] = -w0 * p[1][j] - w1 * p[2][j] - w2 * p[3][j];
-        t[1][j] = w0 * p[0][j] + w2 * p[2][j] - w1 * p[3][j];
-        t[2][j] = w1 * p[0][j] - w2 * p[1][j] + w0 * p[3][j];
-        t[3][j] = w2 * p[0][j] + w1 * p[1][j] - w0 * p[2][j];
-    }
-    // M = T Omega^T: M_ij = T_i . Omega_j
-    auto m = [&](int i, int j) -> T {
-        switch (j) {
-            case 0: return -w0 * t[i][1] - w1 * t[i][2] - w2 * t[i][3];
-            case 1: return w0 * t[i][0] + w2 * t[i][2] - w1 * t[i][3];
-            case 2: return w1 * t[i][0] - w2 * t[i][1] + w0 * t[i][3];
-            default: return w2 * t[i][0] + w1 * t[i][1] - w0 * t[i][2];
-        }
-    };
+PEKF_DEV Sym4T<T> innovation_cov(const Sym4T<T> &P, const T *h, const T *w, const T *hq, T th2, const T *x,
+                                 T n2, T g, T r) {
+    // 2u, with u_a = (D_aa h_a + sum_{b != a} D_ab h_b) / 4, D_ab = tr(L(e_a) R(e_b) P):
+    //   D_11 = -P00 - P11 + P22 + P33, D_22 = -P00 + P11 - P22 + P33, D_33 = -P00 + P11 + P22 - P33,
+    //   D_12 = 2(P03 - P12), D_21 = -2(P03 + P12), D_13 = -2(P02 + P13), D_31 = 2(P02 - P13),
+    //   D_23 = 2(P01 - P23), D_32 = -2(P01 + P23)
+    const T sp = P.a00 + P.a11, dp = P.a11 - P.a00, sq = P.a22 + P.a33, dq = P.a22 - P.a33;
+    const T tr = sp + sq, d11 = sq - sp, d22 = dp - dq, d33 = dp + dq;
+    const T u0 = fma(d11, hq[0], fma(P.a03 - P.a12, h[1], -(P.a02 + P.a13) * h[2]));
+    const T u1 = fma(d22, hq[1], fma(P.a01 - P.a23, h[2], -(P.a03 + P.a12) * h[0]));
+    const T u2 = fma(d33, hq[2], fma(P.a02 - P.a13, h[0], -(P.a01 + P.a23) * h[1]));
+    const T uh = fma(u0, h[0], fma(u1, h[1], u2 * h[2]));                   // 2u . h
+    const T c0 = fma(u1, h[2], -u2 * h[1]), c1 = fma(u2, h[0], -u0 * h[2]);  // 2u x h
+    const T c2 = fma(u0, h[1], -u1 * h[0]);
+    const T nt = -th2;  // th2 = |h|^2
+    // diagonal constant: 2|h|^2 tr(P)/4 + g |x|^2 + r, -/+ 2u.h
+    const T base = fma(T(0.5) * th2, tr, fma(g, n2, r));
+    const T b0 = base - uh, bk = base + uh;
     const T gx0 = g * x[0], gx1 = g * x[1], gx2 = g * x[2], gx3 = g * x[3];
     Sym4T<T> o;
-    o.a00 = fma(g, n2 - x[0] * x[0], m(0, 0));
-    o.a01 = m(0, 1) - gx0 * x[1];
-    o.a02 = m(0, 2) - gx0 * x[2];
-    o.a03 = m(0, 3) - gx0 * x[3];
-    o.a11 = fma(g, n2 - x[1] * x[1], m(1, 1));
-    o.a12 = m(1, 2) - gx1 * x[2];
-    o.a13 = m(1, 3) - gx1 * x[3];
-    o.a22 = fma(g, n2 - x[2] * x[2], m(2, 2));
-    o.a23 = m(2, 3) - gx2 * x[3];
-    o.a33 = fma(g, n2 - x[3] * x[3], m(3, 3));
-    (void)gx3;
+    o.a00 = fma(nt, P.a00, fma(-gx0, x[0], b0));
+    o.a01 = fma(nt, P.a01, fma(-gx0, x[1], c0));
+    o.a02 = fma(nt, P.a02, fma(-gx0, x[2], c1));
+    o.a03 = fma(nt, P.a03, fma(-gx0, x[3], c2));
+    o.a11 = fma(nt, P.a11, fma(-gx1, x[1], fma(-u0, w[0], bk)));
+    o.a22 = fma(nt, P.a22, fma(-gx2, x[2], fma(-u1, w[1], bk)));
+    o.a33 = fma(nt, P.a33, fma(-gx3, x[3], fma(-u2, w[2], bk)));
+    o.a12 = fma(nt, P.a12, fma(-gx1, x[2], -fma(u0, h[1], u1 * h[0])));
+    o.a13 = fma(nt, P.a13, fma(-gx1, x[3], -fma(u0, h[2], u2 * h[0])));
+    o.a23 = fma(nt, P.a23, fma(-gx2, x[3], -fma(u1, h[2], u2 * h[1])));
     return o;
 }
 
@@ -393,9 +435,8 @@ PEKF_DEV Sym4T<T> spd_inverse_schur(const Sym4T<T> &S) {
 // h_w = w/2 (so Omega(h_w) = 0.5*Omega(w), the reference's W).  z = ca x + cb 0.5*Omega(w) x and,
 // since 0.5*Omega(w) is skew with square -|h_w|^2 I, |z|^2 = (ca^2 + cb^2 |h_w|^2) |x|^2 exactly:
 // the normalisation factor is known before z is formed and folds into ca and cb.  n2 = |x|^2.
-PEKF_DEV void rk4_closed(const double *x, double n2, double dt_ns, const double *hw, double *z) {
+PEKF_DEV void rk4_closed(const double *x, double n2, double dt_ns, const double *hw, double th2, double *z) {
     const double h = dt_ns * kNsToS;
-    const double th2 = hw[0] * hw[0] + hw[1] * hw[1] + hw[2] * hw[2];
     const double xx = (h * h) * th2;
     const double ca = 1.0 - 0.5 * xx + xx * xx * (1.0 / 24.0);
     const double cb = h * (1.0 - xx * (1.0 / 6.0));
@@ -407,6 +448,10 @@ PEKF_DEV void rk4_closed(const double *x, double n2, double dt_ns, const double 
     z[1] = a * x[1] + w0 * x[0] + w2 * x[2] - w1 * x[3];
     z[2] = a * x[2] + w1 * x[0] - w2 * x[1] + w0 * x[3];
     z[3] = a * x[3] + w2 * x[0] + w1 * x[1] - w0 * x[2];
+}
+
+PEKF_DEV void rk4_closed(const double *x, double n2, double dt_ns, const double *hw, double *z) {
+    rk4_closed(x, n2, dt_ns, hw, hw[0] * hw[0] + hw[1] * hw[1] + hw[2] * hw[2], z);
 }
 
 }  // namespace pekf

@@ -86,42 +86,41 @@ __device__ __forceinline__ void sym_to16(const Sym4T<PT> &S, double (&p)[16]) {
 }
 
 // One record of main_file.py:42-45 -- Prediction(gyro, T) then Correction(mag, acc) -- on the
-// lane's state (x, P) in registers.  hw = gyro / 2, dt_ns = T - previousT, missing: the record
-// has no magnetometer sample (Wahba-skip, X = z, P = P-).  Shared by the fused stream kernel and
-// the handle's per-record update, so both give bit-identical results for the same inputs.
+// lane's state (x, P) in registers.  gy = the gyro sample, dt_ns = T - previousT, missing: the
+// record has no magnetometer sample (Wahba-skip, X = z, P = P-).  Shared by the fused stream
+// kernel and the handle's per-record update, so both give bit-identical results for the same inputs.
 template <typename PT>
 __device__ __forceinline__ void ekf_record_step(double *x, Sym4T<PT> &P, const Frame &Wf, PT g, PT rp, PT r2,
-                                                double rs, const double *hw, double dt_ns, bool missing,
+                                                double rs, const double *gy, double dt_ns, bool missing,
                                                 const double *acc, const double *mag) {
     // ---- Prediction (ExtendedKalmanFilter.py:58-68) ----
+    const double hw[3] = {0.5 * gy[0], 0.5 * gy[1], 0.5 * gy[2]};  // 0.5*Omega(w) = Omega(w/2)
+    const double th2 = hw[0] * hw[0] + hw[1] * hw[1] + hw[2] * hw[2];
     const PT hp[3] = {(PT)hw[0], (PT)hw[1], (PT)hw[2]};
+    const PT wp[3] = {(PT)gy[0], (PT)gy[1], (PT)gy[2]};
+    const PT hq[3] = {(PT)(0.25 * gy[0]), (PT)(0.25 * gy[1]), (PT)(0.25 * gy[2])};
     const PT xp[4] = {(PT)x[0], (PT)x[1], (PT)x[2], (PT)x[3]};
     const double n2 = x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
-    const Sym4T<PT> Pm = propagate_cov<PT>(P, hp, xp, (PT)n2, g);  // Jb from the prior X (:60)
+    // S = P- + rI with P- = A P A^T + Jb Q Jb^T, Jb from the prior X (:60-61, :63)
+    const Sym4T<PT> S = innovation_cov<PT>(P, hp, wp, hq, (PT)th2, xp, (PT)n2, g, rp);
     double z[4];
-    rk4_closed(x, n2, dt_ns, hw, z);                                // (:62)
+    rk4_closed(x, n2, dt_ns, hw, th2, z);                           // (:62)
 
     if (missing) {
         // Wahba-skip: no Correction for this record (X = z, P = P-)
         x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
-        P = Pm;
+        P = {S.a00 - rp, S.a01, S.a02, S.a03, S.a11 - rp, S.a12, S.a13, S.a22 - rp, S.a23, S.a33 - rp};
     } else {
-        // S = P- + rI; K = P- S^-1 = I - r S^-1  (:63-66)
-        const Sym4T<PT> S = {Pm.a00 + rp, Pm.a01, Pm.a02, Pm.a03, Pm.a11 + rp,
-                             Pm.a12, Pm.a13, Pm.a22 + rp, Pm.a23, Pm.a33 + rp};
+        // K = P- S^-1 = I - r S^-1  (:64-66)
         const Sym4T<PT> Si = spd_inverse_schur<PT, true>(S);
 
         // ---- Correction (ExtendedKalmanFilter.py:70-80) ----
         const double ka = fabs(acc[2]);              // (:71)
         Frame Vf;
         make_frame<true>(acc, mag, Vf, wahba_sign(ka, 1.0 - ka));
-        double R[9], y[4], inv_s;
+        double R[9], y[4];
         wahba_rotation<true>(Wf, Vf, ka, 1.0 - ka, R);  // Wahba.py:8-17
-        rotm_to_quat_scaled(R, y, inv_s);             // Wahba.py:19-47, Y = y * inv_s, inv_s > 0
-        // hemisphere flip (:73-75): sign(Y.z) = sign(y.z), so the flip goes into the scale
-        const double cmp = y[0] * z[0] + y[1] * z[1] + y[2] * z[2] + y[3] * z[3];
-        const double sc = cmp < 0.0 ? -inv_s : inv_s;
-        y[0] *= sc; y[1] *= sc; y[2] *= sc; y[3] *= sc;
+        rotm_to_quat_toward(R, z, y);                  // Wahba.py:19-47 + the flip of :73-75
         const PT e0 = (PT)(y[0] - z[0]), e1 = (PT)(y[1] - z[1]);
         const PT e2 = (PT)(y[2] - z[2]), e3 = (PT)(y[3] - z[3]);
         // X = z + K e = Y - r S^-1 e (:77), normalised (:79)
@@ -176,11 +175,11 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
         make_frame<true>(rf, rf + 3, Wf);
         Sym4T<PT> P = sym_from16<PT>(pv);
         if (run) {
-            const double hw[3] = {0.5 * (double)cur.gd.x, 0.5 * (double)cur.gd.y, 0.5 * (double)cur.gd.z};
+            const double gy[3] = {cur.gd.x, cur.gd.y, cur.gd.z};
             const uint32_t word = __float_as_uint(cur.gd.w);
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
-            ekf_record_step<PT>(x, P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), rs, hw,
+            ekf_record_step<PT>(x, P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), rs, gy,
                                 (double)(word & 0x7FFFFFFFu), (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
         }
         if (TRAJ && act) {
@@ -230,11 +229,11 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     // One record: Prediction + Correction (main_file.py:42-45) on (x, P) in registers.
     auto step = [&](const Rec &cur, int64_t t) {
         if (!COUNTS || t < my_steps) {
-            const double hw[3] = {0.5 * (double)cur.gd.x, 0.5 * (double)cur.gd.y, 0.5 * (double)cur.gd.z};
+            const double gy[3] = {cur.gd.x, cur.gd.y, cur.gd.z};
             const uint32_t word = __float_as_uint(cur.gd.w);
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
-            ekf_record_step<PT>(x, P, Wf, g, rp, r2, rs, hw, (double)(word & 0x7FFFFFFFu),
+            ekf_record_step<PT>(x, P, Wf, g, rp, r2, rs, gy, (double)(word & 0x7FFFFFFFu),
                                 (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
         }
         if (TRAJ) {
@@ -353,8 +352,7 @@ __global__ __launch_bounds__(kRunBlock) void k_update(int64_t batch, const doubl
     tl.to_lanes(cm, m);
     Frame Wf;
     make_frame<true>(rf, rf + 3, Wf);
-    const double hw[3] = {0.5 * g[0], 0.5 * g[1], 0.5 * g[2]};
-    ekf_record_step<PT>(x, P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), rs, hw, dt_ns, miss, a, m);
+    ekf_record_step<PT>(x, P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), rs, g, dt_ns, miss, a, m);
     if (act) prev_t[b] = t;
     if constexpr (SOA) {
         if (act) store_state<true>(Xio, Pio, b, batch, x, P);
