@@ -186,6 +186,7 @@ PEKF_DEV double rsqrt(double x) {
 // Orthonormal frame of a vector pair (a, m): e1 = a/|a|, e2 = GramSchmidt(m), u3 = e1 x e2,
 // with the coordinates of a and m in it: a = alpha e1, m = beta1 e1 + beta2 e2.
 // sg = -1 gives the frame [e1, -e2, -u3] (beta2 -> -beta2), still proper: see wahba_rotation.
+// Only the sign bit of sg is used (any value whose sign is wahba_sign's will do).
 struct Frame {
     double e1[3], e2[3], u3[3];
     double alpha, beta1, beta2;
@@ -199,14 +200,14 @@ PEKF_DEV void make_frame(const double *a, const double *m, Frame &F, double sg =
     const double b1 = F.e1[0] * m[0] + F.e1[1] * m[1] + F.e1[2] * m[2];
     const double t0 = m[0] - b1 * F.e1[0], t1 = m[1] - b1 * F.e1[1], t2 = m[2] - b1 * F.e1[2];
     const double sb = t0 * t0 + t1 * t1 + t2 * t2;
-    const double ib = sg * rsqrt<FAST>(sb);
+    const double ib = copysign(rsqrt<FAST>(sb), sg);
     F.e2[0] = t0 * ib; F.e2[1] = t1 * ib; F.e2[2] = t2 * ib;
     F.u3[0] = F.e1[1] * F.e2[2] - F.e1[2] * F.e2[1];
     F.u3[1] = F.e1[2] * F.e2[0] - F.e1[0] * F.e2[2];
     F.u3[2] = F.e1[0] * F.e2[1] - F.e1[1] * F.e2[0];
     F.alpha = FAST ? sa * ia : sqrt(sa);
     F.beta1 = b1;
-    F.beta2 = FAST ? sb * ib : sg * sqrt(sb);
+    F.beta2 = FAST ? sb * ib : copysign(sqrt(sb), sg);
 }
 
 // sign(det C) of the Wahba core below for weights (ka, km): +1 rotation, -1 reflection case.
@@ -234,7 +235,14 @@ PEKF_DEV void wahba_rotation(const Frame &W, const Frame &V, double ka, double k
         const double g0 = W.e1[i] * p + W.e2[i] * s;     // Fw P2, column 0
         const double g1 = W.e2[i] * p - W.e1[i] * s;     // Fw P2, column 1
 #pragma unroll
-        for (int j = 0; j < 3; ++j) R[i * 3 + j] = g0 * V.e1[j] + g1 * V.e2[j] + W.u3[i] * V.u3[j];
+        for (int j = 0; j < (FAST ? 2 : 3); ++j) R[i * 3 + j] = g0 * V.e1[j] + g1 * V.e2[j] + W.u3[i] * V.u3[j];
+    }
+    if (FAST) {
+        // R is proper orthogonal: its third column is the cross product of the first two
+        // (6 operations instead of 9, and V.u3[2] is never needed)
+        R[2] = R[3] * R[7] - R[6] * R[4];
+        R[5] = R[6] * R[1] - R[0] * R[7];
+        R[8] = R[0] * R[4] - R[3] * R[1];
     }
 }
 
@@ -289,7 +297,7 @@ PEKF_DEV void rotm_to_quat_fast(const double *M, double *q) {
 }
 
 // Y = RotationMatrix2Quart(M) flipped into z's hemisphere (Wahba.py:19-47, then
-// ExtendedKalmanFilter.py:73-75), for the fused kernel.  The four candidate numerators of
+// ExtendedKalmanFilter.py:73-75), for the fused kernel, returned as Y = v * sc.  The four candidate numerators of
 // RotationMatrix2Quart are the columns of Q4 = 4 q q^T (diagonal 1 +- M00 +- M11 +- M22,
 // off-diagonal the sums / differences of M's off-diagonal pairs), so v = Q4 z = 4 q (q.z) is q
 // already carrying the sign of q.z: Y = v / |v|, no branch selects and no separate hemisphere
@@ -299,18 +307,16 @@ PEKF_DEV void rotm_to_quat_fast(const double *M, double *q) {
 // ~0 and, at the exact identity, returns NaN) the lane takes the reference's branch formula and
 // strict '<' flip instead.  Neither occurs on a tracked stream, so the fallback costs a wave
 // nothing unless one of its lanes needs it.
-PEKF_DEV void rotm_to_quat_toward(const double *M, const double *z, double *y) {
+PEKF_DEV void rotm_to_quat_toward(const double *M, const double *z, double *v, double &sc) {
     const double a = 1.0 + M[8], b = 1.0 - M[8], s = M[0] + M[4], d = M[0] - M[4];
     const double t0 = a + s, t1 = b + d, t2 = b - d, t3 = a - s;
     const double dw1 = M[7] - M[5], dw2 = M[2] - M[6], dw3 = M[3] - M[1];
     const double sxy = M[1] + M[3], sxz = M[2] + M[6], syz = M[5] + M[7];
-    double v[4];
     v[0] = fma(t0, z[0], fma(dw1, z[1], fma(dw2, z[2], dw3 * z[3])));
     v[1] = fma(dw1, z[0], fma(t1, z[1], fma(sxy, z[2], sxz * z[3])));
     v[2] = fma(dw2, z[0], fma(sxy, z[1], fma(t2, z[2], syz * z[3])));
     v[3] = fma(dw3, z[0], fma(sxz, z[1], fma(syz, z[2], t3 * z[3])));
     const double nv = fma(v[0], v[0], fma(v[1], v[1], fma(v[2], v[2], v[3] * v[3])));
-    double sc;
 #ifndef PEKF_ISA_COMMON_PATH  // (defined only by scripts/isa_count.py runs: the path a tracked lane takes)
     if (nv < 1.0 || t0 > 4.0 - 1e-10) {
 #else
@@ -324,7 +330,6 @@ PEKF_DEV void rotm_to_quat_toward(const double *M, const double *z, double *y) {
     } else {
         sc = rsqrt<true>(nv);
     }
-    y[0] = v[0] * sc; y[1] = v[1] * sc; y[2] = v[2] * sc; y[3] = v[3] * sc;
 }
 
 // ------------------------------- fused-step forms --------------------------------------------

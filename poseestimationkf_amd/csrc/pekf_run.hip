@@ -91,7 +91,7 @@ __device__ __forceinline__ void sym_to16(const Sym4T<PT> &S, double (&p)[16]) {
 // kernel and the handle's per-record update, so both give bit-identical results for the same inputs.
 template <typename PT>
 __device__ __forceinline__ void ekf_record_step(double *x, Sym4T<PT> &P, const Frame &Wf, PT g, PT rp, PT r2,
-                                                double rs, const double *gy, double dt_ns, bool missing,
+                                                double irs, const double *gy, double dt_ns, bool missing,
                                                 const double *acc, const double *mag) {
     // ---- Prediction (ExtendedKalmanFilter.py:58-68) ----
     const double hw[3] = {0.5 * gy[0], 0.5 * gy[1], 0.5 * gy[2]};  // 0.5*Omega(w) = Omega(w/2)
@@ -117,19 +117,21 @@ __device__ __forceinline__ void ekf_record_step(double *x, Sym4T<PT> &P, const F
         // ---- Correction (ExtendedKalmanFilter.py:70-80) ----
         const double ka = fabs(acc[2]);              // (:71)
         Frame Vf;
-        make_frame<true>(acc, mag, Vf, wahba_sign(ka, 1.0 - ka));
-        double R[9], y[4];
+        // ka = |acc_z| >= 0, so wahba_sign(ka, km) is the sign of km = 1 - ka (never -0)
+        make_frame<true>(acc, mag, Vf, 1.0 - ka);
+        double R[9], v[4], sc;
         wahba_rotation<true>(Wf, Vf, ka, 1.0 - ka, R);  // Wahba.py:8-17
-        rotm_to_quat_toward(R, z, y);                  // Wahba.py:19-47 + the flip of :73-75
-        const PT e0 = (PT)(y[0] - z[0]), e1 = (PT)(y[1] - z[1]);
-        const PT e2 = (PT)(y[2] - z[2]), e3 = (PT)(y[3] - z[3]);
-        // X = z + K e = Y - r S^-1 e (:77), normalised (:79)
+        rotm_to_quat_toward(R, z, v, sc);              // Wahba.py:19-47 + the flip of :73-75: Y = v sc
+        const PT e0 = (PT)fma(v[0], sc, -z[0]), e1 = (PT)fma(v[1], sc, -z[1]);  // e = Y - z
+        const PT e2 = (PT)fma(v[2], sc, -z[2]), e3 = (PT)fma(v[3], sc, -z[3]);
+        // X = z + K e = Y - r S^-1 e (:77), normalised (:79): X ~ Y / r - S^-1 e
         const double u0 = Si.a00 * e0 + Si.a01 * e1 + Si.a02 * e2 + Si.a03 * e3;
         const double u1 = Si.a01 * e0 + Si.a11 * e1 + Si.a12 * e2 + Si.a13 * e3;
         const double u2 = Si.a02 * e0 + Si.a12 * e1 + Si.a22 * e2 + Si.a23 * e3;
         const double u3 = Si.a03 * e0 + Si.a13 * e1 + Si.a23 * e2 + Si.a33 * e3;
-        const double x0 = y[0] - rs * u0, x1 = y[1] - rs * u1;
-        const double x2 = y[2] - rs * u2, x3 = y[3] - rs * u3;
+        const double sr = sc * irs;
+        const double x0 = fma(v[0], sr, -u0), x1 = fma(v[1], sr, -u1);
+        const double x2 = fma(v[2], sr, -u2), x3 = fma(v[3], sr, -u3);
         const double in = rsqrt<true>(x0 * x0 + x1 * x1 + x2 * x2 + x3 * x3);
         x[0] = x0 * in; x[1] = x1 * in; x[2] = x2 * in; x[3] = x3 * in;
         // P = P- - K P- = r K = r I - r^2 S^-1 (:78)
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
             const uint32_t word = __float_as_uint(cur.gd.w);
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
-            ekf_record_step<PT>(x, P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), rs, gy,
+            ekf_record_step<PT>(x, P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), 1.0 / rs, gy,
                                 (double)(word & 0x7FFFFFFFu), (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
         }
         if (TRAJ && act) {
@@ -205,6 +207,7 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     }
     const PT g = (PT)(0.25 * qs);     // Jb Q Jb^T = (q/4)(|X|^2 I - X X^T)
     const PT rp = (PT)rs, r2 = (PT)(rs * rs);
+    const double irs = 1.0 / rs;
     double x[4];
     Sym4T<PT> P;
     load_state<SOA>(Xio, Pio, b, batch, x, P);
@@ -233,7 +236,7 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
             const uint32_t word = __float_as_uint(cur.gd.w);
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
-            ekf_record_step<PT>(x, P, Wf, g, rp, r2, rs, gy, (double)(word & 0x7FFFFFFFu),
+            ekf_record_step<PT>(x, P, Wf, g, rp, r2, irs, gy, (double)(word & 0x7FFFFFFFu),
                                 (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
         }
         if (TRAJ) {
@@ -352,7 +355,7 @@ __global__ __launch_bounds__(kRunBlock) void k_update(int64_t batch, const doubl
     tl.to_lanes(cm, m);
     Frame Wf;
     make_frame<true>(rf, rf + 3, Wf);
-    ekf_record_step<PT>(x, P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), rs, g, dt_ns, miss, a, m);
+    ekf_record_step<PT>(x, P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), 1.0 / rs, g, dt_ns, miss, a, m);
     if (act) prev_t[b] = t;
     if constexpr (SOA) {
         if (act) store_state<true>(Xio, Pio, b, batch, x, P);

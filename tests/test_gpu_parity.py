@@ -324,3 +324,29 @@ def test_dropin_returns_fresh_arrays_and_keeps_inputs(eng, monkeypatch):
     want = npo.correct([0.5, 0.01, -0.86], [0.01, 0.1, 0.99], z, Pm, K, [0.0, 0.1, 0.99], [0.5, 0.0, -0.86])
     assert _maxerr(X1, want[0]) < 1e-13 and _maxerr(P1, want[1]) < 1e-13
     assert X1 is not z and P1 is not Pm
+
+
+@pytest.mark.gpu
+def test_fused_measurement_far_from_prediction(eng):
+    """Filters started at random attitudes, so early Wahba measurements Y lie anywhere relative to
+    the prediction z, including |Y.z| < 1/4 where the fused kernel leaves Y = normalise(4qq^T z) for
+    the reference's branch formula and strict '<' flip (ExtendedKalmanFilter.py:73-75)."""
+    K, W = 256, 30
+    rec = synth.generate(np.arange(K), W, seed=11)
+    rng = np.random.default_rng(3)
+    X0 = rng.normal(size=(K, 4))
+    X0 /= np.linalg.norm(X0, axis=1, keepdims=True)
+    P0 = np.broadcast_to(np.identity(4), (K, 4, 4)).copy()
+    f = eng.BatchedEKF(K)
+    f.set_state(X0, P0)
+    tr = f.run(eng.IMUWindow.from_records(rec), want_traj=True)
+    Q, R = np.identity(3), np.identity(4) * 0.1
+    far = 0
+    for k in range(K):
+        g, d, a, m = rec.filter(k)
+        z, _, _ = npo.predict(g[0], d[0], X0[k], P0[k], Q, R)
+        y = npo.wahba_quat(rec.acc0[k], rec.mag0[k], a[0], m[0], abs(a[0][2]), 1 - abs(a[0][2]))
+        far += abs(float(np.dot(y, z))) < 0.25
+        _, _, want = npo.run_filter(g, d, a, m, rec.acc0[k], rec.mag0[k], X0=X0[k], P0=P0[k])
+        assert _maxerr(tr[:, k], want) < PREC_GUARD, k
+    assert far >= 20  # the fallback lanes really ran
