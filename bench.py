@@ -265,9 +265,10 @@ def main():
 # FP64 work per filter-step of the fused kernel, counted from its gfx950 ISA hot loop by
 # scripts/isa_count.py (DESIGN.md "FP64 budget"): FP64 VALU instructions, and the FLOP of
 # the arithmetic ones with an FMA counted as 2.
-# per filter-step, from scripts/isa_count.py on the hot loop of k_run (make -C .../csrc asm)
-ISA_COUNTS = {"f64": {"flop": 546, "fp64_instr": 373, "valu_instr": 402},
-              "mixed": {"flop": 274, "fp64_instr": 223, "valu_instr": 418}}  # mixed: + ~200 f32 instructions
+# per filter-step, from scripts/isa_count.py on the hot loop of k_run (make -C .../csrc asm-common:
+# the path a tracked lane runs, without the rarely taken R->q fallback branch)
+ISA_COUNTS = {"f64": {"flop": 517, "fp64_instr": 354, "valu_instr": 360},
+              "mixed": {"flop": 292, "fp64_instr": 224, "valu_instr": 377}}  # mixed: + ~150 f32 instructions
 FLOP_PER_STEP = ISA_COUNTS["f64"]["flop"]
 FP64_INSTR_PER_STEP = ISA_COUNTS["f64"]["fp64_instr"]
 
