@@ -21,6 +21,15 @@
 
 #define PEKF_DEV __device__ __forceinline__
 
+// Rarely taken fallback branches of the fused step: PEKF_TAKEN(cond, c) is cond, except in the
+// instruction-count build (make asm-common, -DPEKF_ISA_COMMON_PATH), where it is the constant c of
+// the path a tracked lane takes, so scripts/isa_count.py counts what actually executes.
+#ifdef PEKF_ISA_COMMON_PATH
+#define PEKF_TAKEN(cond, common) (common)
+#else
+#define PEKF_TAKEN(cond, common) (cond)
+#endif
+
 namespace pekf {
 
 constexpr double kNsToS = 1e-09;  // ExtendedKalmanFilter.py:32 (10**-9)
@@ -317,11 +326,7 @@ PEKF_DEV void rotm_to_quat_toward(const double *M, const double *z, double *v, d
     v[2] = fma(dw2, z[0], fma(sxy, z[1], fma(t2, z[2], syz * z[3])));
     v[3] = fma(dw3, z[0], fma(sxz, z[1], fma(syz, z[2], t3 * z[3])));
     const double nv = fma(v[0], v[0], fma(v[1], v[1], fma(v[2], v[2], v[3] * v[3])));
-#ifndef PEKF_ISA_COMMON_PATH  // (defined only by scripts/isa_count.py runs: the path a tracked lane takes)
-    if (nv < 1.0 || t0 > 4.0 - 1e-10) {
-#else
-    if (false) {
-#endif
+    if (PEKF_TAKEN(nv < 1.0 || t0 > 4.0 - 1e-10, false)) {
         // the reference's branch formula and hemisphere test (NaN operands never get here)
         double inv_s;
         rotm_to_quat_scaled(M, v, inv_s);
