@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     }
     const int64_t b = (int64_t)blockIdx.x * kRunBlock + threadIdx.x;
     if (b >= batch) return;
-    const int64_t my_steps = COUNTS ? (counts[b] < n_steps ? (int64_t)counts[b] : n_steps) : n_steps;
+    const int32_t my_steps = COUNTS ? (counts[b] < n_steps ? counts[b] : (int32_t)n_steps) : (int32_t)n_steps;
 
     // per-filter constants: the Wahba reference frame of (acc0, mag0) (Wahba.py:4-6)
     Frame Wf;
@@ -214,23 +214,29 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
 
     // Record of stream row r: raw buffer loads whose resource (the row's base address, scalar
     // registers) is rebuilt per row and whose 32-bit lane offset is fixed, so no per-step vector
-    // address arithmetic (batch < 2^28 is checked on the host, so the offsets fit).
+    // address arithmetic (batch < 2^28 is checked on the host, so the offsets fit).  The row is
+    // tracked as one wave-uniform byte offset (row * batch * 8, advanced by an add and wrapped by a
+    // compare per step; the 16 B planes sit at twice it) instead of a 64-bit row * batch multiply.
     const uint32_t lane = (uint32_t)b;
     const uint32_t off16 = lane * 16u, off8 = lane * 8u;
-    auto load_row = [&](int64_t r) -> Rec {
-        const int64_t base = r * batch;
+    const uint64_t row8 = (uint64_t)batch * 8u, wrap8 = (uint64_t)window * row8;
+    auto load_row = [&](uint64_t o8) -> Rec {
         Rec v;
-        const auto g4 = __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(gd + base, batch * 16), off16, 0, 0);
-        const auto a4 = __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(am + base, batch * 16), off16, 0, 0);
-        const auto m2 = __builtin_amdgcn_raw_buffer_load_b64(row_rsrc(my + base, batch * 8), off8, 0, 0);
+        const char *g = reinterpret_cast<const char *>(gd) + 2 * o8;
+        const char *a = reinterpret_cast<const char *>(am) + 2 * o8;
+        const char *m = reinterpret_cast<const char *>(my) + o8;
+        const auto g4 = __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(g, batch * 16), off16, 0, 0);
+        const auto a4 = __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(a, batch * 16), off16, 0, 0);
+        const auto m2 = __builtin_amdgcn_raw_buffer_load_b64(row_rsrc(m, batch * 8), off8, 0, 0);
         v.gd = __builtin_bit_cast(float4, g4);
         v.am = __builtin_bit_cast(float4, a4);
         v.my = __builtin_bit_cast(float2, m2);
         return v;
     };
+    auto next = [&](uint64_t o8) -> uint64_t { o8 += row8; return o8 == wrap8 ? 0 : o8; };
 
     // One record: Prediction + Correction (main_file.py:42-45) on (x, P) in registers.
-    auto step = [&](const Rec &cur, int64_t t) {
+    auto step = [&](const Rec &cur, int32_t t) {
         if (!COUNTS || t < my_steps) {
             const double gy[3] = {cur.gd.x, cur.gd.y, cur.gd.z};
             const uint32_t word = __float_as_uint(cur.gd.w);
@@ -240,7 +246,7 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
                                 (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
         }
         if (TRAJ) {
-            double2 *o = reinterpret_cast<double2 *>(traj + t * batch * 4) + 2 * (int64_t)lane;
+            double2 *o = reinterpret_cast<double2 *>(traj + (int64_t)t * batch * 4) + 2 * (int64_t)lane;
             o[0] = make_double2(x[0], x[1]);
             o[1] = make_double2(x[2], x[3]);
         }
@@ -251,22 +257,24 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     // The prefetch is unconditional (the row wraps inside the resident window, so it is always
     // a valid address); n_steps >= 1 here.  One-record launches (online serving) use the ONE
     // instantiation, which has no prefetch: there its 40 B would be an eighth of the traffic.
-    int64_t row = step0 % window;
-    Rec ra = load_row(row), rb;
+    uint64_t o8 = (uint64_t)(step0 % window) * row8;
+    Rec ra = load_row(o8), rb;
     if constexpr (ONE) {
         step(ra, 0);
         store_state<SOA>(Xio, Pio, b, batch, x, P);
         return;
     }
-    for (int64_t t = 0;;) {
-        row = row + 1 == window ? 0 : row + 1;
-        rb = load_row(row);
+    // 32-bit step counter (n_steps < 2^31 is checked on the host)
+    const int32_t n32 = (int32_t)n_steps;
+    for (int32_t t = 0;;) {
+        o8 = next(o8);
+        rb = load_row(o8);
         step(ra, t);
-        if (++t == n_steps) break;
-        row = row + 1 == window ? 0 : row + 1;
-        ra = load_row(row);
+        if (++t == n32) break;
+        o8 = next(o8);
+        ra = load_row(o8);
         step(rb, t);
-        if (++t == n_steps) break;
+        if (++t == n32) break;
     }
     store_state<SOA>(Xio, Pio, b, batch, x, P);
 }
@@ -401,6 +409,7 @@ int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
     if (batch == 0 || n_steps == 0) return PEKF_OK;
     PEKF_CHECK_ARG(window > 0 && step0 >= 0, "window must be > 0 and step0 >= 0");
     PEKF_CHECK_ARG(batch < ((int64_t)1 << 28), "batch must be < 2^28 filters per launch");
+    PEKF_CHECK_ARG(n_steps < ((int64_t)1 << 31), "n_steps must be < 2^31 records per launch");
     PEKF_CHECK_ARG(plane_gd && plane_am && plane_my && refs && X && P, "null pointer");
     PEKF_CHECK_ARG(((uintptr_t)plane_gd % 16 == 0) && ((uintptr_t)plane_am % 16 == 0) &&
                        ((uintptr_t)plane_my % 8 == 0) && ((uintptr_t)traj % 16 == 0),
