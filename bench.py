@@ -248,8 +248,11 @@ def main():
                           "frac": B * N * flop / k_s / 1e12 / FP64_PEAK_TFLOPS,
                           "valu_busy_pmc": tsrc[1].get("valu_busy") if tsrc else None,
                           "issue_frac": issue_frac,
-                          "note": "the kernel is VALU-issue-bound: issue_frac = 4 cycles x wave-instructions / "
-                                  "(1024 SIMDs x PMC effective clock x kernel time); HBM frac is capped by it"},
+                          "clock_ghz_pmc": clk,
+                          "note": "the kernel is VALU-issue-bound at a power-limited clock: issue_frac = 4 cycles x "
+                                  "wave-instructions / (1024 SIMDs x PMC effective clock x kernel time); the same "
+                                  "launch with cache-resident records runs at 2.11 GHz instead of 1.80 "
+                                  "(profiles/r1/power_probe); HBM frac is capped by it"},
             "cpu_baseline": cpu,
             "parity": parity,
         }

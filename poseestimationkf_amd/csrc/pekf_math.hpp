@@ -453,7 +453,7 @@ PEKF_DEV void rk4_closed(const double *x, double n2, double dt_ns, const double 
     const double in = rsqrt<true>((ca * ca + (cb * cb) * th2) * n2);
     const double a = ca * in, c = cb * in;
     const double w0 = c * hw[0], w1 = c * hw[1], w2 = c * hw[2];
-    // z = a x + Omega(c h_w) x, rows of Omega as in propagate_cov
+    // z = a x + Omega(c h_w) x, rows of Omega: [0,-w0,-w1,-w2] [w0,0,w2,-w1] [w1,-w2,0,w0] [w2,w1,-w0,0]
     z[0] = a * x[0] - w0 * x[1] - w1 * x[2] - w2 * x[3];
     z[1] = a * x[1] + w0 * x[0] + w2 * x[2] - w1 * x[3];
     z[2] = a * x[2] + w1 * x[0] - w2 * x[1] + w0 * x[3];
