@@ -85,13 +85,25 @@ __device__ __forceinline__ void sym_to16(const Sym4T<PT> &S, double (&p)[16]) {
     p[12] = S.a03; p[13] = S.a13; p[14] = S.a23; p[15] = S.a33;
 }
 
+// |X|^2 of the state entering a launch.  After any record the state is unit (X /= |X|,
+// ExtendedKalmanFilter.py:79, or X = z from the normalised RK4 step) to within ~40 ulp of the
+// one-Newton-step rsqrt, and that is snapped to exactly 1: the stream kernel carries n2 = 1 as a
+// constant after a launch's first record, and every launch shape (n records at once, one record
+// per launch, the handle's per-record update) rounds identically.  A state that is not unit (a
+// user's set_state) keeps its |X|^2, which the reference's Jb and RK4 use (:60-62).
+__device__ __forceinline__ double state_norm2(const double *x) {
+    const double n2 = x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
+    return fabs(n2 - 1.0) < 1e-13 ? 1.0 : n2;
+}
+
 // One record of main_file.py:42-45 -- Prediction(gyro, T) then Correction(mag, acc) -- on the
-// lane's state (x, P) in registers.  gy = the gyro sample, dt_ns = T - previousT, missing: the
-// record has no magnetometer sample (Wahba-skip, X = z, P = P-).  Shared by the fused stream
-// kernel and the handle's per-record update, so both give bit-identical results for the same inputs.
+// lane's state (x, P) in registers; n2 = state_norm2 of x (1 for every record after a launch's
+// first).  gy = the gyro sample, dt_ns = T - previousT, missing: the record has no magnetometer
+// sample (Wahba-skip, X = z, P = P-).  Shared by the fused stream kernel and the handle's
+// per-record update, so both give bit-identical results for the same inputs.
 template <typename PT>
-__device__ __forceinline__ void ekf_record_step(double *x, Sym4T<PT> &P, const Frame &Wf, PT g, PT rp, PT r2,
-                                                double irs, const double *gy, double dt_ns, bool missing,
+__device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> &P, const Frame &Wf, PT g, PT rp,
+                                                PT r2, double irs, const double *gy, double dt_ns, bool missing,
                                                 const double *acc, const double *mag) {
     // ---- Prediction (ExtendedKalmanFilter.py:58-68) ----
     const double hw[3] = {0.5 * gy[0], 0.5 * gy[1], 0.5 * gy[2]};  // 0.5*Omega(w) = Omega(w/2)
@@ -100,7 +112,6 @@ __device__ __forceinline__ void ekf_record_step(double *x, Sym4T<PT> &P, const F
     const PT wp[3] = {(PT)gy[0], (PT)gy[1], (PT)gy[2]};
     const PT hq[3] = {(PT)(0.25 * gy[0]), (PT)(0.25 * gy[1]), (PT)(0.25 * gy[2])};
     const PT xp[4] = {(PT)x[0], (PT)x[1], (PT)x[2], (PT)x[3]};
-    const double n2 = x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
     // S = P- + rI with P- = A P A^T + Jb Q Jb^T, Jb from the prior X (:60-61, :63)
     const Sym4T<PT> S = innovation_cov<PT>(P, hp, wp, hq, (PT)th2, xp, (PT)n2, g, rp);
     double z[4];
@@ -181,7 +192,7 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
             const uint32_t word = __float_as_uint(cur.gd.w);
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
-            ekf_record_step<PT>(x, P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), 1.0 / rs, gy,
+            ekf_record_step<PT>(x, state_norm2(x), P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), 1.0 / rs, gy,
                                 (double)(word & 0x7FFFFFFFu), (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
         }
         if (TRAJ && act) {
@@ -236,13 +247,13 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     auto next = [&](uint64_t o8) -> uint64_t { o8 += row8; return o8 == wrap8 ? 0 : o8; };
 
     // One record: Prediction + Correction (main_file.py:42-45) on (x, P) in registers.
-    auto step = [&](const Rec &cur, int32_t t) {
+    auto step = [&](const Rec &cur, int32_t t, double n2) {
         if (!COUNTS || t < my_steps) {
             const double gy[3] = {cur.gd.x, cur.gd.y, cur.gd.z};
             const uint32_t word = __float_as_uint(cur.gd.w);
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
-            ekf_record_step<PT>(x, P, Wf, g, rp, r2, irs, gy, (double)(word & 0x7FFFFFFFu),
+            ekf_record_step<PT>(x, n2, P, Wf, g, rp, r2, irs, gy, (double)(word & 0x7FFFFFFFu),
                                 (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
         }
         if (TRAJ) {
@@ -260,21 +271,26 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     uint64_t o8 = (uint64_t)(step0 % window) * row8;
     Rec ra = load_row(o8), rb;
     if constexpr (ONE) {
-        step(ra, 0);
+        step(ra, 0, state_norm2(x));
         store_state<SOA>(Xio, Pio, b, batch, x, P);
         return;
     }
-    // 32-bit step counter (n_steps < 2^31 is checked on the host)
+    // The launch's first record takes |X|^2 from the loaded state; from then on the state is
+    // unit and n2 = 1 is a compile-time constant (see state_norm2).  32-bit step counter
+    // (n_steps < 2^31 is checked on the host).
     const int32_t n32 = (int32_t)n_steps;
-    for (int32_t t = 0;;) {
-        o8 = next(o8);
-        rb = load_row(o8);
-        step(ra, t);
-        if (++t == n32) break;
+    o8 = next(o8);
+    rb = load_row(o8);
+    step(ra, 0, state_norm2(x));
+    for (int32_t t = 1; t < n32;) {
         o8 = next(o8);
         ra = load_row(o8);
-        step(rb, t);
+        step(rb, t, 1.0);
         if (++t == n32) break;
+        o8 = next(o8);
+        rb = load_row(o8);
+        step(ra, t, 1.0);
+        ++t;
     }
     store_state<SOA>(Xio, Pio, b, batch, x, P);
 }
@@ -363,7 +379,8 @@ __global__ __launch_bounds__(kRunBlock) void k_update(int64_t batch, const doubl
     tl.to_lanes(cm, m);
     Frame Wf;
     make_frame<true>(rf, rf + 3, Wf);
-    ekf_record_step<PT>(x, P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), 1.0 / rs, g, dt_ns, miss, a, m);
+    ekf_record_step<PT>(x, state_norm2(x), P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), 1.0 / rs, g, dt_ns, miss,
+                        a, m);
     if (act) prev_t[b] = t;
     if constexpr (SOA) {
         if (act) store_state<true>(Xio, Pio, b, batch, x, P);
