@@ -350,3 +350,25 @@ def test_fused_measurement_far_from_prediction(eng):
         _, _, want = npo.run_filter(g, d, a, m, rec.acc0[k], rec.mag0[k], X0=X0[k], P0=P0[k])
         assert _maxerr(tr[:, k], want) < PREC_GUARD, k
     assert far >= 20  # the fallback lanes really ran
+
+
+@pytest.mark.gpu
+def test_fused_non_unit_initial_state(eng):
+    """A state set to a non-unit X (set_state) keeps its |X|^2 in the first record's Jb term and RK4
+    normalisation (ExtendedKalmanFilter.py:60-62), as the reference; unit states snap |X|^2 to 1."""
+    K, W = 64, 20
+    rec = synth.generate(np.arange(K), W, seed=13)
+    rng = np.random.default_rng(5)
+    X0 = rng.normal(size=(K, 4))
+    X0 *= (rng.uniform(0.3, 3.0, size=K) / np.linalg.norm(X0, axis=1))[:, None]
+    X0[::4] /= np.linalg.norm(X0[::4], axis=1, keepdims=True)          # some exactly-normalised rows
+    P0 = np.broadcast_to(np.identity(4) * 0.3, (K, 4, 4)).copy()
+    f = eng.BatchedEKF(K)
+    f.set_state(X0, P0)
+    tr = f.run(eng.IMUWindow.from_records(rec), want_traj=True)
+    _, Pf = f.get_state()
+    for k in range(K):
+        g, d, a, m = rec.filter(k)
+        _, Pk, want = npo.run_filter(g, d, a, m, rec.acc0[k], rec.mag0[k], X0=X0[k], P0=P0[k])
+        assert _maxerr(tr[:, k], want) < PREC_GUARD, k
+        assert _maxerr(Pf[k], Pk) < PREC_GUARD, k
