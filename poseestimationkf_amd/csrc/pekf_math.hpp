@@ -316,25 +316,139 @@ PEKF_DEV void rotm_to_quat_fast(const double *M, double *q) {
 // ~0 and, at the exact identity, returns NaN) the lane takes the reference's branch formula and
 // strict '<' flip instead.  Neither occurs on a tracked stream, so the fallback costs a wave
 // nothing unless one of its lanes needs it.
-PEKF_DEV void rotm_to_quat_toward(const double *M, const double *z, double *v, double &sc) {
+// v = Q4(M) z with Q4 = 4 q q^T of the rotation M (see rotm_to_quat_toward); nv = |v|^2,
+// t0 = 1 + tr M = 4 qw^2
+PEKF_DEV void q4_times(const double *M, const double *z, double *v, double &nv, double &t0) {
     const double a = 1.0 + M[8], b = 1.0 - M[8], s = M[0] + M[4], d = M[0] - M[4];
-    const double t0 = a + s, t1 = b + d, t2 = b - d, t3 = a - s;
+    t0 = a + s;
+    const double t1 = b + d, t2 = b - d, t3 = a - s;
     const double dw1 = M[7] - M[5], dw2 = M[2] - M[6], dw3 = M[3] - M[1];
     const double sxy = M[1] + M[3], sxz = M[2] + M[6], syz = M[5] + M[7];
     v[0] = fma(t0, z[0], fma(dw1, z[1], fma(dw2, z[2], dw3 * z[3])));
     v[1] = fma(dw1, z[0], fma(t1, z[1], fma(sxy, z[2], sxz * z[3])));
     v[2] = fma(dw2, z[0], fma(sxy, z[1], fma(t2, z[2], syz * z[3])));
     v[3] = fma(dw3, z[0], fma(sxz, z[1], fma(syz, z[2], t3 * z[3])));
-    const double nv = fma(v[0], v[0], fma(v[1], v[1], fma(v[2], v[2], v[3] * v[3])));
-    if (PEKF_TAKEN(nv < 1.0 || t0 > 4.0 - 1e-10, false)) {
-        // the reference's branch formula and hemisphere test (NaN operands never get here)
-        double inv_s;
-        rotm_to_quat_scaled(M, v, inv_s);
-        const double cmp = v[0] * z[0] + v[1] * z[1] + v[2] * z[2] + v[3] * z[3];
-        sc = cmp < 0.0 ? -inv_s : inv_s;
+    nv = fma(v[0], v[0], fma(v[1], v[1], fma(v[2], v[2], v[3] * v[3])));
+}
+
+// the reference's branch formula and strict '<' hemisphere test (Wahba.py:19-47,
+// ExtendedKalmanFilter.py:73-75): Y = v * sc
+PEKF_DEV void rotm_to_quat_flip_reference(const double *M, const double *z, double *v, double &sc) {
+    double inv_s;
+    rotm_to_quat_scaled(M, v, inv_s);
+    const double cmp = v[0] * z[0] + v[1] * z[1] + v[2] * z[2] + v[3] * z[3];
+    sc = cmp < 0.0 ? -inv_s : inv_s;
+}
+
+PEKF_DEV void rotm_to_quat_toward(const double *M, const double *z, double *v, double &sc) {
+    double nv, t0;
+    q4_times(M, z, v, nv, t0);
+    sc = rsqrt<true>(nv);  // (the common path carries no data merge with the rare branch)
+    if (PEKF_TAKEN(nv < 1.0 || t0 > 4.0 - 1e-10, false))
+        rotm_to_quat_flip_reference(M, z, v, sc);  // (NaN operands never get here)
+}
+
+// ------------------------------- reference-frame basis ---------------------------------------
+// The multi-record stream kernel runs each filter in the basis of its own Wahba reference frame:
+// X' = q_W^* (x) X and P' = L(q_W^*) P L(q_W^*)^T, q_W the quaternion of Fw = [e1 e2 u3] of
+// (acc0, mag0).  The filter is equivariant under this change of basis: Omega(w) = R(w) is right
+// multiplication and commutes with the left multiplication L(q_W^*) (RK4 and A P A^T,
+// ExtendedKalmanFilter.py:25-48,61), Xi(q) Xi(q)^T = |q|^2 I - q q^T, R = rI and the hemisphere
+// test are invariant under the orthogonal L (:51-56,63-79), and Wahba's rotation becomes
+// R' = Fw^T R = diag(P2, 1) Fv^T, whose quaternion is q_W^* (x) Y (Wahba.py:8-47, the quaternion
+// of a product being the product of the quaternions).  R' is the current frame's rows rotated by
+// P2: p e1 - s e2, s e1 + p e2, u3 -- 12 operations instead of the 36 of Fw diag(P2, 1) Fv^T.
+struct RefW {
+    double aW, b1W, b2W;  // the reference pair in its own frame: acc0 = (aW, 0, 0), mag0 = (b1W, b2W, 0)
+    double q[4];          // q_W
+};
+
+// quaternion of the proper frame [e1 e2 u3] (columns): Shepperd's largest diagonal of 4 q q^T,
+// IEEE arithmetic; once per filter and launch.
+PEKF_DEV void frame_quat(const Frame &F, double *q) {
+    const double m00 = F.e1[0], m10 = F.e1[1], m20 = F.e1[2];
+    const double m01 = F.e2[0], m11 = F.e2[1], m21 = F.e2[2];
+    const double m02 = F.u3[0], m12 = F.u3[1], m22 = F.u3[2];
+    const double t0 = 1.0 + m00 + m11 + m22, t1 = 1.0 + m00 - m11 - m22;
+    const double t2 = 1.0 - m00 + m11 - m22, t3 = 1.0 - m00 - m11 + m22;
+    const double w1 = m21 - m12, w2 = m02 - m20, w3 = m10 - m01;
+    const double sxy = m01 + m10, sxz = m02 + m20, syz = m12 + m21;
+    double v0, v1, v2, v3;
+    if (t0 >= t1 && t0 >= t2 && t0 >= t3) {
+        v0 = t0; v1 = w1; v2 = w2; v3 = w3;
+    } else if (t1 >= t2 && t1 >= t3) {
+        v0 = w1; v1 = t1; v2 = sxy; v3 = sxz;
+    } else if (t2 >= t3) {
+        v0 = w2; v1 = sxy; v2 = t2; v3 = syz;
     } else {
-        sc = rsqrt<true>(nv);
+        v0 = w3; v1 = sxz; v2 = syz; v3 = t3;
     }
+    const double in = 1.0 / sqrt(v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3);
+    q[0] = v0 * in; q[1] = v1 * in; q[2] = v2 * in; q[3] = v3 * in;
+}
+
+// y = q (x) x (CONJ = false) or q^* (x) x (CONJ = true), i.e. L(q) x or L(q)^T x
+template <bool CONJ>
+PEKF_DEV void qmul_left(const double *q, const double *x, double *y) {
+    const double q0 = q[0], q1 = CONJ ? -q[1] : q[1], q2 = CONJ ? -q[2] : q[2], q3 = CONJ ? -q[3] : q[3];
+    y[0] = q0 * x[0] - q1 * x[1] - q2 * x[2] - q3 * x[3];
+    y[1] = q0 * x[1] + q1 * x[0] + q2 * x[3] - q3 * x[2];
+    y[2] = q0 * x[2] - q1 * x[3] + q2 * x[0] + q3 * x[1];
+    y[3] = q0 * x[3] + q1 * x[2] - q2 * x[1] + q3 * x[0];
+}
+
+// rotation matrix of the unit quaternion q (q v q^* = M v)
+PEKF_DEV void quat_to_rotm(const double *q, double *M) {
+    const double w = q[0], x = q[1], y = q[2], z = q[3];
+    M[0] = 1.0 - 2.0 * (y * y + z * z); M[1] = 2.0 * (x * y - w * z);       M[2] = 2.0 * (x * z + w * y);
+    M[3] = 2.0 * (x * y + w * z);       M[4] = 1.0 - 2.0 * (x * x + z * z); M[5] = 2.0 * (y * z - w * x);
+    M[6] = 2.0 * (x * z - w * y);       M[7] = 2.0 * (y * z + w * x);       M[8] = 1.0 - 2.0 * (x * x + y * y);
+}
+
+// Y' = q_W^* (x) Y for the flipped Wahba quaternion Y of the weights (ka, km), in the reference
+// frame's basis (z' the prediction in that basis): Y' = v * sc.  As rotm_to_quat_toward, with its
+// fallback taken in the world basis (R = Fw R', z = q_W (x) z') so that it is the reference's own
+// branch formula; the near-identity test of the world rotation is 4 (q_W (x) Y')_0^2 > 4 - 1e-10.
+PEKF_DEV void wahba_quat_toward(const RefW &W, const Frame &V, double ka, double km, const double *z, double *v,
+                                double &sc) {
+    const double kw = km * W.b2W, kb = km * W.b1W;
+    double p = ka * W.aW * V.alpha + kb * V.beta1 + kw * V.beta2;
+    double s = kw * V.beta1 - kb * V.beta2;
+    const double ih = rsqrt<true>(p * p + s * s);
+    p *= ih;
+    s *= ih;
+    double R[9];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        R[j] = p * V.e1[j] - s * V.e2[j];
+        R[3 + j] = s * V.e1[j] + p * V.e2[j];
+        R[6 + j] = V.u3[j];
+    }
+    double nv, t0;
+    q4_times(R, z, v, nv, t0);
+    sc = rsqrt<true>(nv);
+    const double yw = W.q[0] * v[0] - W.q[1] * v[1] - W.q[2] * v[2] - W.q[3] * v[3];
+    if (PEKF_TAKEN(nv < 1.0 || yw * yw > (1.0 - 2.5e-11) * nv, false)) {
+        double Fw[9], Rw[9], zw[4], vw[4];
+        quat_to_rotm(W.q, Fw);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) Rw[3 * i + j] = Fw[3 * i] * R[j] + Fw[3 * i + 1] * R[3 + j] + Fw[3 * i + 2] * R[6 + j];
+        qmul_left<false>(W.q, z, zw);
+        rotm_to_quat_flip_reference(Rw, zw, vw, sc);
+        qmul_left<true>(W.q, vw, v);
+    }
+    (void)t0;
+    (void)yw;
+}
+
+// Y = v * sc in the world basis (the per-record kernels)
+PEKF_DEV void wahba_quat_toward(const Frame &W, const Frame &V, double ka, double km, const double *z, double *v,
+                                double &sc) {
+    double R[9];
+    wahba_rotation<true>(W, V, ka, km, R);
+    rotm_to_quat_toward(R, z, v, sc);
 }
 
 // ------------------------------- fused-step forms --------------------------------------------
@@ -350,6 +464,25 @@ struct Sym4T {
     T a00, a01, a02, a03, a11, a12, a13, a22, a23, a33;
 };
 using Sym4 = Sym4T<double>;
+
+// M P M^T for M = L(q) (CONJ = false) or L(q)^T (CONJ = true): the covariance in the other basis
+template <bool CONJ, typename T>
+PEKF_DEV Sym4T<T> sym_rotate(const double *q, const Sym4T<T> &S) {
+    const double p[4][4] = {{S.a00, S.a01, S.a02, S.a03}, {S.a01, S.a11, S.a12, S.a13},
+                            {S.a02, S.a12, S.a22, S.a23}, {S.a03, S.a13, S.a23, S.a33}};
+    double t[4][4], o[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // columns of M P (P symmetric: row j = column j)
+        double c[4];
+        qmul_left<CONJ>(q, p[j], c);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t[i][j] = c[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) qmul_left<CONJ>(q, t[i], o[i]);  // (M P) M^T: row i = M (row i of M P)
+    return {(T)o[0][0], (T)o[0][1], (T)o[0][2], (T)o[0][3], (T)o[1][1],
+            (T)o[1][2], (T)o[1][3], (T)o[2][2], (T)o[2][3], (T)o[3][3]};
+}
 
 // single-precision reciprocal for the opt-in mixed-precision covariance path: v_rcp_f32
 // (1 ulp) + one Newton step

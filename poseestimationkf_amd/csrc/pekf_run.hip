@@ -97,12 +97,13 @@ __device__ __forceinline__ double state_norm2(const double *x) {
 }
 
 // One record of main_file.py:42-45 -- Prediction(gyro, T) then Correction(mag, acc) -- on the
-// lane's state (x, P) in registers; n2 = state_norm2 of x (1 for every record after a launch's
+// lane's state (x, P) in registers, in the world basis (Wf: the reference pair's Frame) or in the
+// reference frame's own basis (Wf: a RefW, see pekf_math.hpp); n2 = state_norm2 of x (1 for every record after a launch's
 // first).  gy = the gyro sample, dt_ns = T - previousT, missing: the record has no magnetometer
 // sample (Wahba-skip, X = z, P = P-).  Shared by the fused stream kernel and the handle's
 // per-record update, so both give bit-identical results for the same inputs.
-template <typename PT>
-__device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> &P, const Frame &Wf, PT g, PT rp,
+template <typename PT, typename Ref>
+__device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> &P, const Ref &Wf, PT g, PT rp,
                                                 PT r2, double irs, const double *gy, double dt_ns, bool missing,
                                                 const double *acc, const double *mag) {
     // ---- Prediction (ExtendedKalmanFilter.py:58-68) ----
@@ -130,9 +131,8 @@ __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> 
         Frame Vf;
         // ka = |acc_z| >= 0, so wahba_sign(ka, km) is the sign of km = 1 - ka (never -0)
         make_frame<true>(acc, mag, Vf, 1.0 - ka);
-        double R[9], v[4], sc;
-        wahba_rotation<true>(Wf, Vf, ka, 1.0 - ka, R);  // Wahba.py:8-17
-        rotm_to_quat_toward(R, z, v, sc);              // Wahba.py:19-47 + the flip of :73-75: Y = v sc
+        double v[4], sc;
+        wahba_quat_toward(Wf, Vf, ka, 1.0 - ka, z, v, sc);  // Wahba.py:8-47 + the flip of :73-75: Y = v sc
         const PT e0 = (PT)fma(v[0], sc, -z[0]), e1 = (PT)fma(v[1], sc, -z[1]);  // e = Y - z
         const PT e2 = (PT)fma(v[2], sc, -z[2]), e3 = (PT)fma(v[3], sc, -z[3]);
         // X = z + K e = Y - r S^-1 e (:77), normalised (:79): X ~ Y / r - S^-1 e
@@ -247,19 +247,21 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     auto next = [&](uint64_t o8) -> uint64_t { o8 += row8; return o8 == wrap8 ? 0 : o8; };
 
     // One record: Prediction + Correction (main_file.py:42-45) on (x, P) in registers.
-    auto step = [&](const Rec &cur, int32_t t, double n2) {
+    auto step = [&](const Rec &cur, int32_t t, double n2, const auto &ref) {
         if (!COUNTS || t < my_steps) {
             const double gy[3] = {cur.gd.x, cur.gd.y, cur.gd.z};
             const uint32_t word = __float_as_uint(cur.gd.w);
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
-            ekf_record_step<PT>(x, n2, P, Wf, g, rp, r2, irs, gy, (double)(word & 0x7FFFFFFFu),
+            ekf_record_step<PT>(x, n2, P, ref, g, rp, r2, irs, gy, (double)(word & 0x7FFFFFFFu),
                                 (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
         }
         if (TRAJ) {
+            double xo[4] = {x[0], x[1], x[2], x[3]};
+            if constexpr (std::is_same<std::decay_t<decltype(ref)>, RefW>::value) qmul_left<false>(ref.q, x, xo);
             double2 *o = reinterpret_cast<double2 *>(traj + (int64_t)t * batch * 4) + 2 * (int64_t)lane;
-            o[0] = make_double2(x[0], x[1]);
-            o[1] = make_double2(x[2], x[3]);
+            o[0] = make_double2(xo[0], xo[1]);
+            o[1] = make_double2(xo[2], xo[3]);
         }
     };
 
@@ -271,9 +273,23 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     uint64_t o8 = (uint64_t)(step0 % window) * row8;
     Rec ra = load_row(o8), rb;
     if constexpr (ONE) {
-        step(ra, 0, state_norm2(x));
+        step(ra, 0, state_norm2(x), Wf);
         store_state<SOA>(Xio, Pio, b, batch, x, P);
         return;
+    }
+    // A multi-record launch runs the filter in its reference frame's own basis (RefW in
+    // pekf_math.hpp: the same filter, with Wahba's rotation 24 operations cheaper per record);
+    // the state is rotated in once and out once per launch.  A filter with no records in this
+    // launch (COUNTS) rotates by the identity, which is exact, so it is left untouched.
+    RefW Wr;
+    Wr.aW = Wf.alpha; Wr.b1W = Wf.beta1; Wr.b2W = Wf.beta2;
+    frame_quat(Wf, Wr.q);
+    if (COUNTS && my_steps == 0) { Wr.q[0] = 1.0; Wr.q[1] = Wr.q[2] = Wr.q[3] = 0.0; }
+    {
+        double xw[4];
+        qmul_left<true>(Wr.q, x, xw);
+        x[0] = xw[0]; x[1] = xw[1]; x[2] = xw[2]; x[3] = xw[3];
+        P = sym_rotate<true>(Wr.q, P);
     }
     // The launch's first record takes |X|^2 from the loaded state; from then on the state is
     // unit and n2 = 1 is a compile-time constant (see state_norm2).  32-bit step counter
@@ -281,16 +297,22 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     const int32_t n32 = (int32_t)n_steps;
     o8 = next(o8);
     rb = load_row(o8);
-    step(ra, 0, state_norm2(x));
+    step(ra, 0, state_norm2(x), Wr);
     for (int32_t t = 1; t < n32;) {
         o8 = next(o8);
         ra = load_row(o8);
-        step(rb, t, 1.0);
+        step(rb, t, 1.0, Wr);
         if (++t == n32) break;
         o8 = next(o8);
         rb = load_row(o8);
-        step(ra, t, 1.0);
+        step(ra, t, 1.0, Wr);
         ++t;
+    }
+    {
+        double xo[4];
+        qmul_left<false>(Wr.q, x, xo);
+        x[0] = xo[0]; x[1] = xo[1]; x[2] = xo[2]; x[3] = xo[3];
+        P = sym_rotate<false>(Wr.q, P);
     }
     store_state<SOA>(Xio, Pio, b, batch, x, P);
 }

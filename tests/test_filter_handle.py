@@ -1,8 +1,9 @@
 """Filter handle (pekf_filter_*): B KalmanFilter objects with device-resident state.
 
 update() is main_file.py:42-45 per filter from FP64 host arrays; it shares ekf_record_step with
-the stream kernel, so on f32-representable records it is bit-identical to pekf_run_dev, and on
-general FP64 records it is checked against the NumPy restatement of the reference.
+the stream kernel (the stream kernel in the reference frame's basis, update() in the world basis),
+so on f32-representable records it agrees with pekf_run_dev to rounding, and on general FP64
+records it is checked against the NumPy restatement of the reference.
 """
 from __future__ import annotations
 
@@ -27,8 +28,15 @@ def _same(a, b):
     return np.array_equal(np.asarray(a).view(np.uint64), np.asarray(b).view(np.uint64))
 
 
+ROUNDING = 1e-13  # per-record (world basis) vs multi-record (reference-frame basis) launches
+
+
+def _close(a, b):
+    return float(np.abs(np.asarray(a) - np.asarray(b)).max()) < ROUNDING
+
+
 @pytest.mark.parametrize("layout", ["aos", "soa"])
-def test_update_loop_bit_identical_to_stream_run(eng, layout):
+def test_update_loop_matches_stream_run(eng, layout):
     K, N = 300, 40
     rec = synth.generate(np.arange(K), N, seed=31, missing=True)
     ref = eng.BatchedEKF(K)
@@ -40,10 +48,10 @@ def test_update_loop_bit_identical_to_stream_run(eng, layout):
         t += (rec.dtw[i] & 0x7FFFFFFF).astype(np.int64)
         X = h.update(rec.gyro[i].astype(np.float64), t, rec.acc[i].astype(np.float64), rec.mag[i].astype(np.float64),
                      missing=(rec.dtw[i] >> 31).astype(np.uint8))
-        assert _same(X, tr[i]), i
+        assert _close(X, tr[i]), i
     Xr, Pr = ref.get_state()
     Xh, Ph = h.get_state()
-    assert _same(Xh, Xr) and _same(Ph, Pr)
+    assert _close(Xh, Xr) and _close(Ph, Pr)
 
 
 def test_update_fp64_records_against_numpy_restatement(eng):

@@ -1,8 +1,10 @@
 """SoA state layout (PEKF_RUN_STATE_SOA) and per-filter record counts of pekf_run_dev.
 
-Both are launch-shape options, not numerics: every result here must be BIT-IDENTICAL to the
-default AoS, uniform-length launch on the same records (which test_gpu_parity.py pins to the
-oracle).  Ragged logs end-to-end are checked against the reference's own C1 trajectory.
+Both are launch-shape options, not numerics: every multi-record result here must be BIT-IDENTICAL
+to the default AoS, uniform-length launch on the same records (which test_gpu_parity.py pins to
+the oracle).  One-record launches run the same step in the world basis instead of the reference
+frame's basis (pekf_run.hip), so they agree with multi-record launches to rounding.  Ragged logs
+end-to-end are checked against the reference's own C1 trajectory.
 """
 from __future__ import annotations
 
@@ -31,6 +33,13 @@ def _same(a, b):
     return np.array_equal(np.asarray(a).view(np.uint64), np.asarray(b).view(np.uint64))
 
 
+ROUNDING = 1e-13  # one-record (world basis) vs multi-record (reference-frame basis) launches
+
+
+def _close(a, b):
+    return float(np.abs(np.asarray(a) - np.asarray(b)).max(initial=0.0)) < ROUNDING
+
+
 @pytest.mark.parametrize("precision", ["f64", "mixed"])
 def test_soa_layout_bit_identical_to_aos(eng, precision):
     K, W = 300, 48
@@ -50,7 +59,7 @@ def test_soa_layout_bit_identical_to_aos(eng, precision):
 
 
 def test_soa_online_single_record_launches(eng):
-    """Online serving: one launch per new record equals one launch over all records."""
+    """Online serving: one launch per new record agrees with one launch over all records."""
     K, W, N = 513, 8, 21
     rec = synth.generate(np.arange(K), W, seed=4)
     win = eng.IMUWindow.from_records(rec)
@@ -61,7 +70,7 @@ def test_soa_online_single_record_launches(eng):
         s.run_async(win, 1, t)
     Xr, Pr = ref.get_state()
     Xs, Ps = s.get_state()
-    assert _same(Xr, Xs) and _same(Pr, Ps)
+    assert _close(Xr, Xs) and _close(Pr, Ps)
 
 
 def test_state_layout_roundtrip(eng):
@@ -94,10 +103,11 @@ def test_per_filter_counts_equal_truncated_launches(eng, layout):
         g = eng.BatchedEKF(K)
         tg = g.run(win, n_steps=int(c), want_traj=True) if c else None
         Xg, Pg = g.get_state()
-        assert _same(X[sel], Xg[sel]) and _same(P[sel], Pg[sel]), c
+        eq = _close if c == 1 else _same  # n_steps = 1 is a one-record launch (world basis)
+        assert eq(X[sel], Xg[sel]) and eq(P[sel], Pg[sel]), c
         if c:
-            assert _same(tr[:c, sel], tg[:, sel])
-        assert _same(tr[c:, sel], np.broadcast_to(Xg[sel], (N - c,) + Xg[sel].shape))
+            assert eq(tr[:c, sel], tg[:, sel])
+        assert eq(tr[c:, sel], np.broadcast_to(Xg[sel], (N - c,) + Xg[sel].shape))
 
 
 def test_ragged_logs_share_one_launch(eng, tmp_path):
