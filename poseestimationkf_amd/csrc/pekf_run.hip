@@ -19,6 +19,13 @@ namespace pekf {
 
 constexpr int kRunBlock = 256;
 
+// Cache policy of the record loads: nt (aux = 2), as each record is read once per launch.
+// Same box, config 3: 136.8 / 137.7 ms against 137.8 / 138.8 with the default policy
+// (profiles/r1/ab_nt_loads/); sc0 nt 137.0 / 137.9.
+#ifndef PEKF_REC_AUX
+#define PEKF_REC_AUX 2
+#endif
+
 struct Rec {
     float4 gd;  // gx, gy, gz, bits(dt word)
     float4 am;  // ax, ay, az, mx
@@ -236,9 +243,9 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
         const char *g = reinterpret_cast<const char *>(gd) + 2 * o8;
         const char *a = reinterpret_cast<const char *>(am) + 2 * o8;
         const char *m = reinterpret_cast<const char *>(my) + o8;
-        const auto g4 = __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(g, batch * 16), off16, 0, 0);
-        const auto a4 = __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(a, batch * 16), off16, 0, 0);
-        const auto m2 = __builtin_amdgcn_raw_buffer_load_b64(row_rsrc(m, batch * 8), off8, 0, 0);
+        const auto g4 = __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(g, batch * 16), off16, 0, PEKF_REC_AUX);
+        const auto a4 = __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(a, batch * 16), off16, 0, PEKF_REC_AUX);
+        const auto m2 = __builtin_amdgcn_raw_buffer_load_b64(row_rsrc(m, batch * 8), off8, 0, PEKF_REC_AUX);
         v.gd = __builtin_bit_cast(float4, g4);
         v.am = __builtin_bit_cast(float4, a4);
         v.my = __builtin_bit_cast(float2, m2);
