@@ -36,6 +36,23 @@ def log(msg):
     print("[bench] " + msg, file=sys.stderr, flush=True)
 
 
+class StdoutForTheResult:
+    """Native libraries print on the process's stdout (RCCL writes a version banner there when a
+    communicator is created, on every rank): point file descriptor 1 at stderr for the whole run
+    and restore it only to print the result line, so stdout carries exactly one JSON line."""
+
+    def __init__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def emit(self, line):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        print(line, flush=True)
+        os.dup2(2, 1)
+
+
 # ----------------------------------------------------------------------------------- CPU baseline
 def _cpu_worker(args):
     """Runs in a forked child (before any GPU initialisation): NumPy restatement of main_file.py's loop."""
@@ -105,6 +122,7 @@ def main():
     ap.add_argument("--dist", action="store_true",
                     help="use torch.distributed/RCCL even at world size 1 (exercises the gather path)")
     args = ap.parse_args()
+    out_fd = StdoutForTheResult()
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -256,7 +274,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
         }
-        print(json.dumps(out), flush=True)
+        out_fd.emit(json.dumps(out))
     if use_dist:
         if rank == 0 and gathered is not None:  # the gathered quaternions are the filters' final X
             Xr, _ = filt.get_state()

@@ -305,17 +305,6 @@ PEKF_DEV void rotm_to_quat_fast(const double *M, double *q) {
     q[0] = v[0] * inv_s; q[1] = v[1] * inv_s; q[2] = v[2] * inv_s; q[3] = v[3] * inv_s;
 }
 
-// Y = RotationMatrix2Quart(M) flipped into z's hemisphere (Wahba.py:19-47, then
-// ExtendedKalmanFilter.py:73-75), for the fused kernel, returned as Y = v * sc.  The four candidate numerators of
-// RotationMatrix2Quart are the columns of Q4 = 4 q q^T (diagonal 1 +- M00 +- M11 +- M22,
-// off-diagonal the sums / differences of M's off-diagonal pairs), so v = Q4 z = 4 q (q.z) is q
-// already carrying the sign of q.z: Y = v / |v|, no branch selects and no separate hemisphere
-// test.  |v| = 4 |q.z| |z|, so where q is nearly orthogonal to z (|q.z| < 1/4: the measured
-// attitude more than 150 degrees from the prediction) and where the reference's own branch
-// formula is ill-conditioned (a rotation within ~1e-5 rad of the identity, where it divides by
-// ~0 and, at the exact identity, returns NaN) the lane takes the reference's branch formula and
-// strict '<' flip instead.  Neither occurs on a tracked stream, so the fallback costs a wave
-// nothing unless one of its lanes needs it.
 // v = Q4(M) z with Q4 = 4 q q^T of the rotation M (see rotm_to_quat_toward); nv = |v|^2,
 // t0 = 1 + tr M = 4 qw^2
 PEKF_DEV void q4_times(const double *M, const double *z, double *v, double &nv, double &t0) {
@@ -340,6 +329,17 @@ PEKF_DEV void rotm_to_quat_flip_reference(const double *M, const double *z, doub
     sc = cmp < 0.0 ? -inv_s : inv_s;
 }
 
+// Y = RotationMatrix2Quart(M) flipped into z's hemisphere (Wahba.py:19-47, then
+// ExtendedKalmanFilter.py:73-75), for the fused kernel, returned as Y = v * sc.  The four candidate numerators of
+// RotationMatrix2Quart are the columns of Q4 = 4 q q^T (diagonal 1 +- M00 +- M11 +- M22,
+// off-diagonal the sums / differences of M's off-diagonal pairs), so v = Q4 z = 4 q (q.z) is q
+// already carrying the sign of q.z: Y = v / |v|, no branch selects and no separate hemisphere
+// test.  |v| = 4 |q.z| |z|, so where q is nearly orthogonal to z (|q.z| < 1/4: the measured
+// attitude more than 150 degrees from the prediction) and where the reference's own branch
+// formula is ill-conditioned (a rotation within ~1e-5 rad of the identity, where it divides by
+// ~0 and, at the exact identity, returns NaN) the lane takes the reference's branch formula and
+// strict '<' flip instead.  Neither occurs on a tracked stream, so the fallback costs a wave
+// nothing unless one of its lanes needs it.
 PEKF_DEV void rotm_to_quat_toward(const double *M, const double *z, double *v, double &sc) {
     double nv, t0;
     q4_times(M, z, v, nv, t0);
