@@ -109,6 +109,15 @@ __device__ __forceinline__ double state_norm2(const double *x) {
 // first).  gy = the gyro sample, dt_ns = T - previousT, missing: the record has no magnetometer
 // sample (Wahba-skip, X = z, P = P-).  Shared by the fused stream kernel and the handle's
 // per-record update, so both give bit-identical results for the same inputs.
+// a * b - c as one three-address v_fma_f64 with a negated operand.  Left to itself the compiler
+// picks the accumulating v_fmac_f64 for e = v sc - z and sets -z up in the accumulator registers
+// ahead of the rare Wahba fallback branch (a negation and two register copies per component).
+__device__ __forceinline__ double fma_sub(double a, double b, double c) {
+    double d;
+    asm("v_fma_f64 %0, %1, %2, -%3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
 template <typename PT, typename Ref>
 __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> &P, const Ref &Wf, PT g, PT rp,
                                                 PT r2, double irs, const double *gy, double dt_ns, bool missing,
@@ -140,8 +149,8 @@ __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> 
         make_frame<true>(acc, mag, Vf, 1.0 - ka);
         double v[4], sc;
         wahba_quat_toward(Wf, Vf, ka, 1.0 - ka, z, v, sc);  // Wahba.py:8-47 + the flip of :73-75: Y = v sc
-        const PT e0 = (PT)fma(v[0], sc, -z[0]), e1 = (PT)fma(v[1], sc, -z[1]);  // e = Y - z
-        const PT e2 = (PT)fma(v[2], sc, -z[2]), e3 = (PT)fma(v[3], sc, -z[3]);
+        const PT e0 = (PT)fma_sub(v[0], sc, z[0]), e1 = (PT)fma_sub(v[1], sc, z[1]);  // e = Y - z
+        const PT e2 = (PT)fma_sub(v[2], sc, z[2]), e3 = (PT)fma_sub(v[3], sc, z[3]);
         // X = z + K e = Y - r S^-1 e (:77), normalised (:79): X ~ Y / r - S^-1 e
         const double u0 = Si.a00 * e0 + Si.a01 * e1 + Si.a02 * e2 + Si.a03 * e3;
         const double u1 = Si.a01 * e0 + Si.a11 * e1 + Si.a12 * e2 + Si.a13 * e3;
