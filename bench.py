@@ -286,11 +286,12 @@ def main():
 # FP64 work per filter-step of the fused kernel, counted from its gfx950 ISA hot loop by
 # scripts/isa_count.py (DESIGN.md "FP64 budget"): FP64 VALU instructions, and the FLOP of
 # the arithmetic ones with an FMA counted as 2.
-# per filter-step, from scripts/isa_count.py on the hot loop of k_run (make -C .../csrc asm-common:
-# the path a tracked lane runs, without the bodies of the rarely taken R->q fallback branches;
-# their tests, ~8 VALU, are added back -- the PMC pass in profiles/ counts the executed total)
-ISA_COUNTS = {"f64": {"flop": 478, "fp64_instr": 332, "valu_instr": 340},
-              "mixed": {"flop": 255, "fp64_instr": 202, "valu_instr": 356}}  # mixed: + ~150 f32 instructions
+# per filter-step: the VALU instructions of the basic blocks a tracked lane executes in k_run's hot
+# loop (scripts/loop_blocks.py on the hipcc -S listing: the fallback bodies sit behind
+# s_cbranch_execz); FP64 instructions and FLOP from scripts/isa_count.py on the same blocks.  The
+# PMC pass in profiles/ counts the executed total (SQ_INSTS_VALU per wave-step).
+ISA_COUNTS = {"f64": {"flop": 473, "fp64_instr": 334, "valu_instr": 340},
+              "mixed": {"flop": 252, "fp64_instr": 200, "valu_instr": 356}}  # mixed: + ~150 f32 instructions
 FLOP_PER_STEP = ISA_COUNTS["f64"]["flop"]
 FP64_INSTR_PER_STEP = ISA_COUNTS["f64"]["fp64_instr"]
 
