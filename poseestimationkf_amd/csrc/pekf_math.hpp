@@ -407,8 +407,13 @@ PEKF_DEV void quat_to_rotm(const double *q, double *M) {
 
 // Y' = q_W^* (x) Y for the flipped Wahba quaternion Y of the weights (ka, km), in the reference
 // frame's basis (z' the prediction in that basis): Y' = v * sc.  As rotm_to_quat_toward, with its
-// fallback taken in the world basis (R = Fw R', z = q_W (x) z') so that it is the reference's own
-// branch formula; the near-identity test of the world rotation is 4 (q_W (x) Y')_0^2 > 4 - 1e-10.
+// |q.z| < 1/4 fallback taken in the world basis (R = Fw R', z = q_W (x) z') so that it is the
+// reference's own branch formula and flip.  There is no near-identity fallback here: within
+// ~1e-5 rad of the identity the reference's formula divides rounding noise by ~theta, so its
+// result differs from ANY other evaluation of the same rotation by ~1e-16/theta (ours included,
+// whatever formula we use: R' and numpy's SVD rotation differ in the last bits), and an exactly
+// identity world rotation -- the one input where it is deterministic (NaN) -- does not arise from
+// Fw R'.  The well-conditioned Q4 z value is returned instead.
 PEKF_DEV void wahba_quat_toward(const RefW &W, const Frame &V, double ka, double km, const double *z, double *v,
                                 double &sc) {
     const double kw = km * W.b2W, kb = km * W.b1W;
@@ -427,8 +432,7 @@ PEKF_DEV void wahba_quat_toward(const RefW &W, const Frame &V, double ka, double
     double nv, t0;
     q4_times(R, z, v, nv, t0);
     sc = rsqrt<true>(nv);
-    const double yw = W.q[0] * v[0] - W.q[1] * v[1] - W.q[2] * v[2] - W.q[3] * v[3];
-    if (PEKF_TAKEN(nv < 1.0 || yw * yw > (1.0 - 2.5e-11) * nv, false)) {
+    if (PEKF_TAKEN(nv < 1.0, false)) {
         double Fw[9], Rw[9], zw[4], vw[4];
         quat_to_rotm(W.q, Fw);
 #pragma unroll
@@ -440,7 +444,6 @@ PEKF_DEV void wahba_quat_toward(const RefW &W, const Frame &V, double ka, double
         qmul_left<true>(W.q, vw, v);
     }
     (void)t0;
-    (void)yw;
 }
 
 // Y = v * sc in the world basis (the per-record kernels)

@@ -22,5 +22,7 @@ for l in body[hdr+1:end+1]:
         cnt[blk]+=1
     elif s.startswith('s_cbranch') or s.startswith('s_branch'):
         order.append('   '+s)
+        # the fall-through after a conditional branch is a block of its own (it may be the rare side)
+        blk = (blk.split('+')[0] + '+%d' % (len(order))); order.append(blk)
 for o in order:
     print(o, cnt.get(o,'') if not o.startswith(' ') else '')
