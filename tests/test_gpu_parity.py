@@ -372,3 +372,22 @@ def test_fused_non_unit_initial_state(eng):
         _, Pk, want = npo.run_filter(g, d, a, m, rec.acc0[k], rec.mag0[k], X0=X0[k], P0=P0[k])
         assert _maxerr(tr[:, k], want) < PREC_GUARD, k
         assert _maxerr(Pf[k], Pk) < PREC_GUARD, k
+
+
+@pytest.mark.gpu
+def test_fused_arbitrary_reference_frames(eng):
+    """Reference pairs (acc0, mag0) in arbitrary directions: every filter's Wahba reference frame,
+    and with it the basis the multi-record kernel runs the filter in (its quaternion q_W, all four
+    of Shepperd's branches), differs; records stay in the body frame, so the filters start far from
+    the attitude they converge to."""
+    from scipy.spatial.transform import Rotation
+    K, W = 256, 40
+    rec = synth.generate(np.arange(K), W, seed=23)
+    Rk = Rotation.random(K, random_state=7).as_matrix()
+    rec.acc0[:] = np.einsum("kij,kj->ki", Rk, rec.acc0)
+    rec.mag0[:] = np.einsum("kij,kj->ki", Rk, rec.mag0)
+    tr = eng.BatchedEKF(K).run(eng.IMUWindow.from_records(rec), want_traj=True)
+    for k in range(K):
+        g, d, a, m = rec.filter(k)
+        _, _, want = npo.run_filter(g, d, a, m, rec.acc0[k], rec.mag0[k])
+        assert _maxerr(tr[:, k], want) < PREC_GUARD, k
