@@ -497,8 +497,11 @@ PEKF_DEV float recip(float x) {
 }
 
 // Innovation covariance S = A P A^T + g (|x|^2 I - x x^T) + rI, A = Omega(h), h = w/2
-// (ExtendedKalmanFilter.py:44-47,52-55,61,63); n2 = |x|^2 (shared with rk4_closed's
-// normalisation), w = the raw gyro (= 2h), hq = h/2.
+// (ExtendedKalmanFilter.py:44-47,52-55,61,63), returned DOUBLED: 2S, every entry exactly twice
+// S's (a power-of-two factor commutes with rounding), so that the gyro enters only as w (the raw
+// sample) and h -- S itself would need w/4 as well.  g2 = 2g, r2 = 2r; n2 = |x|^2 (shared with
+// rk4_closed's normalisation); th2 = |h|^2.  The caller folds the factor into its constants:
+// (2S)^-1 = S^-1 / 2 exactly, and the update (X normalised, P = rI - r^2 S^-1) is unchanged.
 //
 // Omega(h) is the matrix of right multiplication by the pure quaternion h, v -> v (x) h.  In the
 // basis {I, L(e_a) R(e_b)} (a, b = 1..3) of symmetric 4x4 matrices, P = c0 I + sum C_ab L(e_a) R(e_b)
@@ -507,27 +510,26 @@ PEKF_DEV float recip(float x) {
 //   A P A^T = 2 L(u) R(h) - |h|^2 P + 2 |h|^2 c0 I,   u = C h,
 //   L(u) R(h) = [[-u.h, (u x h)^T], [u x h, (u.h) I - u h^T - h u^T]].
 // u needs only the trace butterflies of P's diagonal and the sums / differences of its off-diagonal
-// pairs: 74 FP64 operations for S against 96 for the direct Omega P Omega^T + Jb Q Jb^T + rI.
+// pairs: 71 FP64 operations for 2S against 96 for the direct Omega P Omega^T + Jb Q Jb^T + rI.
 template <typename T>
-PEKF_DEV Sym4T<T> innovation_cov(const Sym4T<T> &P, const T *h, const T *w, const T *hq, T th2, const T *x,
-                                 T n2, T g, T r) {
-    // 2u, with u_a = (D_aa h_a + sum_{b != a} D_ab h_b) / 4, D_ab = tr(L(e_a) R(e_b) P):
+PEKF_DEV Sym4T<T> innovation_cov2(const Sym4T<T> &P, const T *h, const T *w, T th2, const T *x, T n2, T g2, T r2) {
+    // U = 4u, U_a = D_aa h_a + sum_{b != a} D_ab h_b with D_ab = tr(L(e_a) R(e_b) P):
     //   D_11 = -P00 - P11 + P22 + P33, D_22 = -P00 + P11 - P22 + P33, D_33 = -P00 + P11 + P22 - P33,
     //   D_12 = 2(P03 - P12), D_21 = -2(P03 + P12), D_13 = -2(P02 + P13), D_31 = 2(P02 - P13),
     //   D_23 = 2(P01 - P23), D_32 = -2(P01 + P23)
     const T sp = P.a00 + P.a11, dp = P.a11 - P.a00, sq = P.a22 + P.a33, dq = P.a22 - P.a33;
     const T tr = sp + sq, d11 = sq - sp, d22 = dp - dq, d33 = dp + dq;
-    const T u0 = fma(d11, hq[0], fma(P.a03 - P.a12, h[1], -(P.a02 + P.a13) * h[2]));
-    const T u1 = fma(d22, hq[1], fma(P.a01 - P.a23, h[2], -(P.a03 + P.a12) * h[0]));
-    const T u2 = fma(d33, hq[2], fma(P.a02 - P.a13, h[0], -(P.a01 + P.a23) * h[1]));
-    const T uh = fma(u0, h[0], fma(u1, h[1], u2 * h[2]));                   // 2u . h
-    const T c0 = fma(u1, h[2], -u2 * h[1]), c1 = fma(u2, h[0], -u0 * h[2]);  // 2u x h
+    const T u0 = fma(d11, h[0], fma(P.a03 - P.a12, w[1], -(P.a02 + P.a13) * w[2]));
+    const T u1 = fma(d22, h[1], fma(P.a01 - P.a23, w[2], -(P.a03 + P.a12) * w[0]));
+    const T u2 = fma(d33, h[2], fma(P.a02 - P.a13, w[0], -(P.a01 + P.a23) * w[1]));
+    const T uh = fma(u0, h[0], fma(u1, h[1], u2 * h[2]));                   // 4u . h
+    const T c0 = fma(u1, h[2], -u2 * h[1]), c1 = fma(u2, h[0], -u0 * h[2]);  // 4u x h
     const T c2 = fma(u0, h[1], -u1 * h[0]);
-    const T nt = -th2;  // th2 = |h|^2
-    // diagonal constant: 2|h|^2 tr(P)/4 + g |x|^2 + r, -/+ 2u.h
-    const T base = fma(T(0.5) * th2, tr, fma(g, n2, r));
+    const T nt = T(-2) * th2;
+    // diagonal constant: 2 (2|h|^2 tr(P)/4 + g |x|^2 + r), -/+ 4u.h
+    const T base = fma(th2, tr, fma(g2, n2, r2));
     const T b0 = base - uh, bk = base + uh;
-    const T gx0 = g * x[0], gx1 = g * x[1], gx2 = g * x[2], gx3 = g * x[3];
+    const T gx0 = g2 * x[0], gx1 = g2 * x[1], gx2 = g2 * x[2], gx3 = g2 * x[3];
     Sym4T<T> o;
     o.a00 = fma(nt, P.a00, fma(-gx0, x[0], b0));
     o.a01 = fma(nt, P.a01, fma(-gx0, x[1], c0));

@@ -127,20 +127,23 @@ __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> 
     const double th2 = hw[0] * hw[0] + hw[1] * hw[1] + hw[2] * hw[2];
     const PT hp[3] = {(PT)hw[0], (PT)hw[1], (PT)hw[2]};
     const PT wp[3] = {(PT)gy[0], (PT)gy[1], (PT)gy[2]};
-    const PT hq[3] = {(PT)(0.25 * gy[0]), (PT)(0.25 * gy[1]), (PT)(0.25 * gy[2])};
     const PT xp[4] = {(PT)x[0], (PT)x[1], (PT)x[2], (PT)x[3]};
-    // S = P- + rI with P- = A P A^T + Jb Q Jb^T, Jb from the prior X (:60-61, :63)
-    const Sym4T<PT> S = innovation_cov<PT>(P, hp, wp, hq, (PT)th2, xp, (PT)n2, g, rp);
+    // S2 = 2S, S = P- + rI with P- = A P A^T + Jb Q Jb^T, Jb from the prior X (:60-61, :63).
+    // Exactly twice S (see innovation_cov2), so every result below is bit-identical to the
+    // undoubled recursion: (2S)^-1 = S^-1/2, and the constants absorb the factor.
+    const Sym4T<PT> S2 = innovation_cov2<PT>(P, hp, wp, (PT)th2, xp, (PT)n2, PT(2) * g, PT(2) * rp);
     double z[4];
     rk4_closed(x, n2, dt_ns, hw, th2, z);                           // (:62)
 
     if (missing) {
-        // Wahba-skip: no Correction for this record (X = z, P = P-)
+        // Wahba-skip: no Correction for this record (X = z, P = P- = S - rI)
         x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
-        P = {S.a00 - rp, S.a01, S.a02, S.a03, S.a11 - rp, S.a12, S.a13, S.a22 - rp, S.a23, S.a33 - rp};
+        const PT hf = PT(0.5);
+        P = {fma(hf, S2.a00, -rp), hf * S2.a01, hf * S2.a02, hf * S2.a03, fma(hf, S2.a11, -rp),
+             hf * S2.a12, hf * S2.a13, fma(hf, S2.a22, -rp), hf * S2.a23, fma(hf, S2.a33, -rp)};
     } else {
-        // K = P- S^-1 = I - r S^-1  (:64-66)
-        const Sym4T<PT> Si = spd_inverse_schur<PT, true>(S);
+        // K = P- S^-1 = I - r S^-1  (:64-66); Si2 = S^-1 / 2
+        const Sym4T<PT> Si = spd_inverse_schur<PT, true>(S2);
 
         // ---- Correction (ExtendedKalmanFilter.py:70-80) ----
         const double ka = fabs(acc[2]);              // (:71)
@@ -151,19 +154,20 @@ __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> 
         wahba_quat_toward(Wf, Vf, ka, 1.0 - ka, z, v, sc);  // Wahba.py:8-47 + the flip of :73-75: Y = v sc
         const PT e0 = (PT)fma_sub(v[0], sc, z[0]), e1 = (PT)fma_sub(v[1], sc, z[1]);  // e = Y - z
         const PT e2 = (PT)fma_sub(v[2], sc, z[2]), e3 = (PT)fma_sub(v[3], sc, z[3]);
-        // X = z + K e = Y - r S^-1 e (:77), normalised (:79): X ~ Y / r - S^-1 e
+        // X = z + K e = Y - r S^-1 e (:77), normalised (:79): X ~ Y / (2r) - S^-1 e / 2
         const double u0 = Si.a00 * e0 + Si.a01 * e1 + Si.a02 * e2 + Si.a03 * e3;
         const double u1 = Si.a01 * e0 + Si.a11 * e1 + Si.a12 * e2 + Si.a13 * e3;
         const double u2 = Si.a02 * e0 + Si.a12 * e1 + Si.a22 * e2 + Si.a23 * e3;
         const double u3 = Si.a03 * e0 + Si.a13 * e1 + Si.a23 * e2 + Si.a33 * e3;
-        const double sr = sc * irs;
+        const double sr = sc * (0.5 * irs);
         const double x0 = fma(v[0], sr, -u0), x1 = fma(v[1], sr, -u1);
         const double x2 = fma(v[2], sr, -u2), x3 = fma(v[3], sr, -u3);
         const double in = rsqrt<true>(x0 * x0 + x1 * x1 + x2 * x2 + x3 * x3);
         x[0] = x0 * in; x[1] = x1 * in; x[2] = x2 * in; x[3] = x3 * in;
-        // P = P- - K P- = r K = r I - r^2 S^-1 (:78)
-        P = {rp - r2 * Si.a00, -r2 * Si.a01, -r2 * Si.a02, -r2 * Si.a03, rp - r2 * Si.a11,
-             -r2 * Si.a12, -r2 * Si.a13, rp - r2 * Si.a22, -r2 * Si.a23, rp - r2 * Si.a33};
+        // P = P- - K P- = r K = r I - r^2 S^-1 = r I - (2 r^2) Si (:78)
+        const PT rr = PT(2) * r2;
+        P = {rp - rr * Si.a00, -rr * Si.a01, -rr * Si.a02, -rr * Si.a03, rp - rr * Si.a11,
+             -rr * Si.a12, -rr * Si.a13, rp - rr * Si.a22, -rr * Si.a23, rp - rr * Si.a33};
     }
 }
 
