@@ -33,6 +33,7 @@
 namespace pekf {
 
 constexpr double kNsToS = 1e-09;  // ExtendedKalmanFilter.py:32 (10**-9)
+constexpr double kSqrt2 = 1.4142135623730951;
 
 // ------------------------------- literal (per-call) forms -------------------------------------
 
@@ -544,12 +545,54 @@ PEKF_DEV Sym4T<T> innovation_cov2(const Sym4T<T> &P, const T *h, const T *w, T t
     return o;
 }
 
+// The same for the covariance carried as N, P = rI + beta D N D with beta = sqrt(2) r and
+// D = diag(1, 1, -1, -1) (the multi-record stream loop): returns S^ = 2S / beta, for which
+// spd_inverse_schur<NEG = true> gives the next record's N = -D (S^)^-1 D with no scaling at all
+// (P+ = rI - r^2 S^-1 = rI - (2r^2/beta) (S^)^-1 = rI - beta (S^)^-1, since 2r^2 = beta^2), so the
+// update P = rI - r^2 S^-1 costs nothing.  D flips the sign of the off-diagonal 2x2 block: in that
+// form every entry of the negated inverse is a plain sum of products (no negations to
+// materialise), and here the signs ride on the operand modifiers.  With A P A^T = r|h|^2 I + beta A N' A^T
+// (N' = D N D):
+//   S^ = 2 A N' A^T + (2/beta)(r|h|^2 + r) I + (2g/beta)(|x|^2 I - x x^T),
+// innovation_cov2's algebra on N' with gb = 2g/beta, rb = 2r/beta (= sqrt 2) for 2g, 2r, and one
+// operation more (tr N + rb).
+template <typename T>
+PEKF_DEV Sym4T<T> innovation_cov_n(const Sym4T<T> &N, const T *h, const T *w, T th2, const T *x, T n2, T gb, T rb) {
+    const T sp = N.a00 + N.a11, dp = N.a11 - N.a00, sq = N.a22 + N.a33, dq = N.a22 - N.a33;
+    const T tr = sp + sq, d11 = sq - sp, d22 = dp - dq, d33 = dp + dq;
+    const T u0 = fma(d11, h[0], fma(N.a12 - N.a03, w[1], (N.a02 + N.a13) * w[2]));
+    const T u1 = fma(d22, h[1], fma(N.a01 - N.a23, w[2], (N.a03 + N.a12) * w[0]));
+    const T u2 = fma(d33, h[2], fma(N.a13 - N.a02, w[0], -(N.a01 + N.a23) * w[1]));
+    const T uh = fma(u0, h[0], fma(u1, h[1], u2 * h[2]));
+    const T c0 = fma(u1, h[2], -u2 * h[1]), c1 = fma(u2, h[0], -u0 * h[2]);
+    const T c2 = fma(u0, h[1], -u1 * h[0]);
+    const T nt = T(-2) * th2;
+    const T base = fma(th2, tr + rb, fma(gb, n2, rb));
+    const T b0 = base - uh, bk = base + uh;
+    const T gx0 = gb * x[0], gx1 = gb * x[1], gx2 = gb * x[2], gx3 = gb * x[3];
+    Sym4T<T> o;
+    o.a00 = fma(nt, N.a00, fma(-gx0, x[0], b0));
+    o.a01 = fma(nt, N.a01, fma(-gx0, x[1], c0));
+    o.a02 = fma(-nt, N.a02, fma(-gx0, x[2], c1));
+    o.a03 = fma(-nt, N.a03, fma(-gx0, x[3], c2));
+    o.a11 = fma(nt, N.a11, fma(-gx1, x[1], fma(-u0, w[0], bk)));
+    o.a22 = fma(nt, N.a22, fma(-gx2, x[2], fma(-u1, w[1], bk)));
+    o.a33 = fma(nt, N.a33, fma(-gx3, x[3], fma(-u2, w[2], bk)));
+    o.a12 = fma(-nt, N.a12, fma(-gx1, x[2], -fma(u0, h[1], u1 * h[0])));
+    o.a13 = fma(-nt, N.a13, fma(-gx1, x[3], -fma(u0, h[2], u2 * h[0])));
+    o.a23 = fma(nt, N.a23, fma(-gx2, x[3], -fma(u1, h[2], u2 * h[1])));
+    return o;
+}
+
 // Inverse of an SPD 4x4 by 2x2 blocks, S = [[A, B], [B^T, D]]: A^-1 by its adjugate, the Schur
 // complement C = D - B^T A^-1 B (SPD) likewise, then
 //   S^-1 = [[A^-1 + X C^-1 X^T, -X C^-1], [-C^-1 X^T, C^-1]],  X = A^-1 B.
 // Two reciprocals (an LDL^T factorisation needs four, and a v_rcp_f64 issues at 3x an FMA on
 // gfx950, scripts/probe_rates.hip): 38 plain operations + 2 Newton-refined reciprocals.
-template <typename T, bool FAST = true>
+// NEG = true returns -D S^-1 D, D = diag(1, 1, -1, -1), for the same work: with W = X (-C^-1) it is
+// [[-A^-1 + W X^T, W], [W^T, -C^-1]], every entry a plain sum of products (the sign of -C^-1 rides on
+// the second reciprocal, that of -A^-1 on an addend).
+template <typename T, bool FAST = true, bool NEG = false>
 PEKF_DEV Sym4T<T> spd_inverse_schur(const Sym4T<T> &S) {
     const T ia = recip<FAST>(S.a00 * S.a11 - S.a01 * S.a01);
     const T p00 = S.a11 * ia, p01 = -S.a01 * ia, p11 = S.a00 * ia;  // A^-1
@@ -560,12 +603,22 @@ PEKF_DEV Sym4T<T> spd_inverse_schur(const Sym4T<T> &S) {
     const T c00 = S.a22 - S.a02 * x00 - S.a12 * x10;
     const T c01 = S.a23 - S.a02 * x01 - S.a12 * x11;
     const T c11 = S.a33 - S.a03 * x01 - S.a13 * x11;
-    const T ic = recip<FAST>(c00 * c11 - c01 * c01);
-    const T q00 = c11 * ic, q01 = -c01 * ic, q11 = c00 * ic;        // C^-1
+    const T ic = NEG ? recip<FAST>(c01 * c01 - c00 * c11) : recip<FAST>(c00 * c11 - c01 * c01);
+    const T q00 = c11 * ic, q01 = -c01 * ic, q11 = c00 * ic;        // C^-1 (NEG: -C^-1)
+    Sym4T<T> o;
+    if (NEG) {
+        const T w00 = x00 * q00 + x01 * q01, w01 = x00 * q01 + x01 * q11;
+        const T w10 = x10 * q00 + x11 * q01, w11 = x10 * q01 + x11 * q11;
+        o.a00 = w00 * x00 + w01 * x01 - p00;
+        o.a01 = w00 * x10 + w01 * x11 - p01;
+        o.a11 = w10 * x10 + w11 * x11 - p11;
+        o.a02 = w00; o.a03 = w01; o.a12 = w10; o.a13 = w11;
+        o.a22 = q00; o.a23 = q01; o.a33 = q11;
+        return o;
+    }
     // off-diagonal block O = -X C^-1, top-left A^-1 - O X^T
     const T o00 = -(x00 * q00 + x01 * q01), o01 = -(x00 * q01 + x01 * q11);
     const T o10 = -(x10 * q00 + x11 * q01), o11 = -(x10 * q01 + x11 * q11);
-    Sym4T<T> o;
     o.a00 = p00 - o00 * x00 - o01 * x01;
     o.a01 = p01 - o00 * x10 - o01 * x11;
     o.a11 = p11 - o10 * x10 - o11 * x11;

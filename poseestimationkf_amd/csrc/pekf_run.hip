@@ -117,10 +117,36 @@ __device__ __forceinline__ double fma_sub(double a, double b, double c) {
     asm("v_fma_f64 %0, %1, %2, -%3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
     return d;
 }
+// c - a * b, likewise
+__device__ __forceinline__ double fma_rsub(double a, double b, double c) {
+    double d;
+    asm("v_fma_f64 %0, -%1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
 
-template <typename PT, typename Ref>
-__device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> &P, const Ref &Wf, PT g, PT rp,
-                                                PT r2, double irs, const double *gy, double dt_ns, bool missing,
+// Per-launch constants of ekf_record_step.  MC = false: the covariance is carried as P itself;
+// MC = true (the multi-record stream loop): as N with P = rI + beta D N D, beta = sqrt(2) r,
+// D = diag(1, 1, -1, -1), so that the next N = -D (S^)^-1 D comes out of the Schur inverse of
+// innovation_cov_n's S^ with no update arithmetic (pekf_math.hpp).
+template <typename PT>
+struct StepK {
+    PT g2, r2;   // MC: 2g/beta, 2r/beta | P: 2g, 2r (innovation_cov_n / innovation_cov2)
+    PT rp, rr;   // P: r, 2r^2 (P = rI - 2r^2 (2S)^-1); unused for MC
+    double sy;   // Y's weight in the unnormalised X update: MC 1/sqrt(2), P 1/(2r)
+};
+template <typename PT, bool MC>
+__device__ __forceinline__ StepK<PT> step_consts(double qs, double rs) {
+    const double g = 0.25 * qs;  // Jb Q Jb^T = (q/4)(|X|^2 I - X X^T)
+    if (MC) {
+        const double ib = 1.0 / (kSqrt2 * rs);
+        return {(PT)(2.0 * g * ib), (PT)(2.0 * rs * ib), PT(0), PT(0), 1.0 / kSqrt2};
+    }
+    return {(PT)(2.0 * g), (PT)(2.0 * rs), (PT)rs, (PT)(2.0 * (rs * rs)), 0.5 / rs};
+}
+
+template <typename PT, bool MC = false, typename Ref>
+__device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> &P, const Ref &Wf, const StepK<PT> &k,
+                                                const double *gy, double dt_ns, bool missing,
                                                 const double *acc, const double *mag) {
     // ---- Prediction (ExtendedKalmanFilter.py:58-68) ----
     const double hw[3] = {0.5 * gy[0], 0.5 * gy[1], 0.5 * gy[2]};  // 0.5*Omega(w) = Omega(w/2)
@@ -131,7 +157,8 @@ __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> 
     // S2 = 2S, S = P- + rI with P- = A P A^T + Jb Q Jb^T, Jb from the prior X (:60-61, :63).
     // Exactly twice S (see innovation_cov2), so every result below is bit-identical to the
     // undoubled recursion: (2S)^-1 = S^-1/2, and the constants absorb the factor.
-    const Sym4T<PT> S2 = innovation_cov2<PT>(P, hp, wp, (PT)th2, xp, (PT)n2, PT(2) * g, PT(2) * rp);
+    const Sym4T<PT> S2 = MC ? innovation_cov_n<PT>(P, hp, wp, (PT)th2, xp, (PT)n2, k.g2, k.r2)
+                            : innovation_cov2<PT>(P, hp, wp, (PT)th2, xp, (PT)n2, k.g2, k.r2);
     double z[4];
     rk4_closed(x, n2, dt_ns, hw, th2, z);                           // (:62)
 
@@ -139,11 +166,15 @@ __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> 
         // Wahba-skip: no Correction for this record (X = z, P = P- = S - rI)
         x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
         const PT hf = PT(0.5);
-        P = {fma(hf, S2.a00, -rp), hf * S2.a01, hf * S2.a02, hf * S2.a03, fma(hf, S2.a11, -rp),
-             hf * S2.a12, hf * S2.a13, fma(hf, S2.a22, -rp), hf * S2.a23, fma(hf, S2.a33, -rp)};
+        if (MC)  // D N D = (S - 2r I) / beta = S^/2 - rb I
+            P = {fma(hf, S2.a00, -k.r2), hf * S2.a01, -hf * S2.a02, -hf * S2.a03, fma(hf, S2.a11, -k.r2),
+                 -hf * S2.a12, -hf * S2.a13, fma(hf, S2.a22, -k.r2), hf * S2.a23, fma(hf, S2.a33, -k.r2)};
+        else
+            P = {fma(hf, S2.a00, -k.rp), hf * S2.a01, hf * S2.a02, hf * S2.a03, fma(hf, S2.a11, -k.rp),
+                 hf * S2.a12, hf * S2.a13, fma(hf, S2.a22, -k.rp), hf * S2.a23, fma(hf, S2.a33, -k.rp)};
     } else {
-        // K = P- S^-1 = I - r S^-1  (:64-66); Si2 = S^-1 / 2
-        const Sym4T<PT> Si = spd_inverse_schur<PT, true>(S2);
+        // K = P- S^-1 = I - r S^-1  (:64-66); Si = S^-1 / 2, or (MC) the next N = -D (S^)^-1 D
+        const Sym4T<PT> Si = spd_inverse_schur<PT, true, MC>(S2);
 
         // ---- Correction (ExtendedKalmanFilter.py:70-80) ----
         const double ka = fabs(acc[2]);              // (:71)
@@ -152,22 +183,29 @@ __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> 
         make_frame<true>(acc, mag, Vf, 1.0 - ka);
         double v[4], sc;
         wahba_quat_toward(Wf, Vf, ka, 1.0 - ka, z, v, sc);  // Wahba.py:8-47 + the flip of :73-75: Y = v sc
-        const PT e0 = (PT)fma_sub(v[0], sc, z[0]), e1 = (PT)fma_sub(v[1], sc, z[1]);  // e = Y - z
-        const PT e2 = (PT)fma_sub(v[2], sc, z[2]), e3 = (PT)fma_sub(v[3], sc, z[3]);
-        // X = z + K e = Y - r S^-1 e (:77), normalised (:79): X ~ Y / (2r) - S^-1 e / 2
+        // e = Y - z (MC: D e, whose last two components are z - Y)
+        const PT e0 = (PT)fma_sub(v[0], sc, z[0]), e1 = (PT)fma_sub(v[1], sc, z[1]);
+        const PT e2 = (PT)(MC ? fma_rsub(v[2], sc, z[2]) : fma_sub(v[2], sc, z[2]));
+        const PT e3 = (PT)(MC ? fma_rsub(v[3], sc, z[3]) : fma_sub(v[3], sc, z[3]));
+        // X = z + K e = Y - r S^-1 e (:77), normalised (:79): X ~ Y / (2r) - S^-1 e / 2, or (MC,
+        // S^-1 = -(2/beta) D Si D) X ~ Y / sqrt(2) + D Si D e
         const double u0 = Si.a00 * e0 + Si.a01 * e1 + Si.a02 * e2 + Si.a03 * e3;
         const double u1 = Si.a01 * e0 + Si.a11 * e1 + Si.a12 * e2 + Si.a13 * e3;
         const double u2 = Si.a02 * e0 + Si.a12 * e1 + Si.a22 * e2 + Si.a23 * e3;
         const double u3 = Si.a03 * e0 + Si.a13 * e1 + Si.a23 * e2 + Si.a33 * e3;
-        const double sr = sc * (0.5 * irs);
-        const double x0 = fma(v[0], sr, -u0), x1 = fma(v[1], sr, -u1);
+        const double sr = sc * k.sy;
+        const double x0 = fma(v[0], sr, MC ? u0 : -u0), x1 = fma(v[1], sr, MC ? u1 : -u1);
         const double x2 = fma(v[2], sr, -u2), x3 = fma(v[3], sr, -u3);
         const double in = rsqrt<true>(x0 * x0 + x1 * x1 + x2 * x2 + x3 * x3);
         x[0] = x0 * in; x[1] = x1 * in; x[2] = x2 * in; x[3] = x3 * in;
         // P = P- - K P- = r K = r I - r^2 S^-1 = r I - (2 r^2) Si (:78)
-        const PT rr = PT(2) * r2;
-        P = {rp - rr * Si.a00, -rr * Si.a01, -rr * Si.a02, -rr * Si.a03, rp - rr * Si.a11,
-             -rr * Si.a12, -rr * Si.a13, rp - rr * Si.a22, -rr * Si.a23, rp - rr * Si.a33};
+        if (MC) {
+            P = Si;  // P = rI + beta D N D: nothing to compute
+        } else {
+            const PT rp = k.rp, rr = k.rr;
+            P = {rp - rr * Si.a00, -rr * Si.a01, -rr * Si.a02, -rr * Si.a03, rp - rr * Si.a11,
+                 -rr * Si.a12, -rr * Si.a13, rp - rr * Si.a22, -rr * Si.a23, rp - rr * Si.a33};
+        }
     }
 }
 
@@ -212,7 +250,7 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
             const uint32_t word = __float_as_uint(cur.gd.w);
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
-            ekf_record_step<PT>(x, state_norm2(x), P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), 1.0 / rs, gy,
+            ekf_record_step<PT>(x, state_norm2(x), P, Wf, step_consts<PT, false>(qs, rs), gy,
                                 (double)(word & 0x7FFFFFFFu), (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
         }
         if (TRAJ && act) {
@@ -236,9 +274,6 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
         const double m0[3] = {refs[6 * b + 3], refs[6 * b + 4], refs[6 * b + 5]};
         make_frame<true>(a0, m0, Wf);
     }
-    const PT g = (PT)(0.25 * qs);     // Jb Q Jb^T = (q/4)(|X|^2 I - X X^T)
-    const PT rp = (PT)rs, r2 = (PT)(rs * rs);
-    const double irs = 1.0 / rs;
     double x[4];
     Sym4T<PT> P;
     load_state<SOA>(Xio, Pio, b, batch, x, P);
@@ -268,17 +303,19 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
 
     // One record: Prediction + Correction (main_file.py:42-45) on (x, P) in registers.
     auto step = [&](const Rec &cur, int32_t t, double n2, const auto &ref) {
+        // the multi-record loop (RefW) carries M, the one-record launch (Frame) P
+        constexpr bool MC = std::is_same<std::decay_t<decltype(ref)>, RefW>::value;
         if (!COUNTS || t < my_steps) {
             const double gy[3] = {cur.gd.x, cur.gd.y, cur.gd.z};
             const uint32_t word = __float_as_uint(cur.gd.w);
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
-            ekf_record_step<PT>(x, n2, P, ref, g, rp, r2, irs, gy, (double)(word & 0x7FFFFFFFu),
-                                (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
+            ekf_record_step<PT, MC>(x, n2, P, ref, step_consts<PT, MC>(qs, rs), gy, (double)(word & 0x7FFFFFFFu),
+                                    (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
         }
         if (TRAJ) {
             double xo[4] = {x[0], x[1], x[2], x[3]};
-            if constexpr (std::is_same<std::decay_t<decltype(ref)>, RefW>::value) qmul_left<false>(ref.q, x, xo);
+            if constexpr (MC) qmul_left<false>(ref.q, x, xo);
             double2 *o = reinterpret_cast<double2 *>(traj + (int64_t)t * batch * 4) + 2 * (int64_t)lane;
             o[0] = make_double2(xo[0], xo[1]);
             o[1] = make_double2(xo[2], xo[3]);
@@ -300,7 +337,8 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     // A multi-record launch runs the filter in its reference frame's own basis (RefW in
     // pekf_math.hpp: the same filter, with Wahba's rotation 24 operations cheaper per record);
     // the state is rotated in once and out once per launch.  A filter with no records in this
-    // launch (COUNTS) rotates by the identity, which is exact, so it is left untouched.
+    // launch (COUNTS) rotates by the identity, which is exact, and its state is not written back.
+    // Inside the loop the covariance is carried as N, P = rI + beta D N D (StepK).
     RefW Wr;
     Wr.aW = Wf.alpha; Wr.b1W = Wf.beta1; Wr.b2W = Wf.beta2;
     frame_quat(Wf, Wr.q);
@@ -310,6 +348,9 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
         qmul_left<true>(Wr.q, x, xw);
         x[0] = xw[0]; x[1] = xw[1]; x[2] = xw[2]; x[3] = xw[3];
         P = sym_rotate<true>(Wr.q, P);
+        const PT ib = (PT)(1.0 / (kSqrt2 * rs)), rp = (PT)rs;
+        P = {(P.a00 - rp) * ib, P.a01 * ib, -P.a02 * ib, -P.a03 * ib, (P.a11 - rp) * ib,
+             -P.a12 * ib, -P.a13 * ib, (P.a22 - rp) * ib, P.a23 * ib, (P.a33 - rp) * ib};
     }
     // The launch's first record takes |X|^2 from the loaded state; from then on the state is
     // unit and n2 = 1 is a compile-time constant (see state_norm2).  32-bit step counter
@@ -328,7 +369,11 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
         step(ra, t, 1.0, Wr);
         ++t;
     }
+    if (COUNTS && my_steps == 0) return;
     {
+        const PT be = (PT)(kSqrt2 * rs), rp = (PT)rs;
+        P = {fma(be, P.a00, rp), be * P.a01, -be * P.a02, -be * P.a03, fma(be, P.a11, rp),
+             -be * P.a12, -be * P.a13, fma(be, P.a22, rp), be * P.a23, fma(be, P.a33, rp)};
         double xo[4];
         qmul_left<false>(Wr.q, x, xo);
         x[0] = xo[0]; x[1] = xo[1]; x[2] = xo[2]; x[3] = xo[3];
@@ -421,8 +466,7 @@ __global__ __launch_bounds__(kRunBlock) void k_update(int64_t batch, const doubl
     tl.to_lanes(cm, m);
     Frame Wf;
     make_frame<true>(rf, rf + 3, Wf);
-    ekf_record_step<PT>(x, state_norm2(x), P, Wf, (PT)(0.25 * qs), (PT)rs, (PT)(rs * rs), 1.0 / rs, g, dt_ns, miss,
-                        a, m);
+    ekf_record_step<PT>(x, state_norm2(x), P, Wf, step_consts<PT, false>(qs, rs), g, dt_ns, miss, a, m);
     if (act) prev_t[b] = t;
     if constexpr (SOA) {
         if (act) store_state<true>(Xio, Pio, b, batch, x, P);
