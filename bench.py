@@ -290,8 +290,8 @@ def main():
 # loop (scripts/loop_blocks.py on the hipcc -S listing: the fallback bodies sit behind
 # s_cbranch_execz); FP64 instructions and FLOP from scripts/isa_count.py on the same blocks.  The
 # PMC pass in profiles/ counts the executed total (SQ_INSTS_VALU per wave-step).
-ISA_COUNTS = {"f64": {"flop": 454, "fp64_instr": 313, "valu_instr": 317},
-              "mixed": {"flop": 252, "fp64_instr": 200, "valu_instr": 356}}  # mixed: + ~150 f32 instructions
+ISA_COUNTS = {"f64": {"flop": 447, "fp64_instr": 308, "valu_instr": 312},
+              "mixed": {"flop": 240, "fp64_instr": 191, "valu_instr": 329}}  # mixed: + ~130 f32 instructions
 FLOP_PER_STEP = ISA_COUNTS["f64"]["flop"]
 FP64_INSTR_PER_STEP = ISA_COUNTS["f64"]["fp64_instr"]
 

@@ -18,6 +18,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #define PEKF_DEV __device__ __forceinline__
 
@@ -360,8 +361,10 @@ PEKF_DEV void rotm_to_quat_toward(const double *M, const double *z, double *v, d
 // of a product being the product of the quaternions).  R' is the current frame's rows rotated by
 // P2: p e1 - s e2, s e1 + p e2, u3 -- 12 operations instead of the 36 of Fw diag(P2, 1) Fv^T.
 struct RefW {
+    static constexpr bool kRefBasis = true;
     double aW, b1W, b2W;  // the reference pair in its own frame: acc0 = (aW, 0, 0), mag0 = (b1W, b2W, 0)
     double q[4];          // q_W
+    PEKF_DEV void quat(double *o) const { o[0] = q[0]; o[1] = q[1]; o[2] = q[2]; o[3] = q[3]; }
 };
 
 // quaternion of the proper frame [e1 e2 u3] (columns): Shepperd's largest diagonal of 4 q q^T,
@@ -387,6 +390,20 @@ PEKF_DEV void frame_quat(const Frame &F, double *q) {
     const double in = 1.0 / sqrt(v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3);
     q[0] = v0 * in; q[1] = v1 * in; q[2] = v2 * in; q[3] = v3 * in;
 }
+
+// RefW whose q_W is recomputed from the filter's reference pair where it is needed (the rare
+// |q.z| < 1/4 fallback, the launch's end) instead of being held: 8 fewer live VGPRs in the time loop.
+// The recomputation is the same code on the same inputs, so it returns the same q_W bit for bit.
+struct RefWLazy {
+    static constexpr bool kRefBasis = true;
+    double aW, b1W, b2W;
+    const double *pair;  // acc0[3], mag0[3] of this filter
+    PEKF_DEV void quat(double *o) const {
+        Frame F;
+        make_frame<true>(pair, pair + 3, F);
+        frame_quat(F, o);
+    }
+};
 
 // y = q (x) x (CONJ = false) or q^* (x) x (CONJ = true), i.e. L(q) x or L(q)^T x
 template <bool CONJ>
@@ -415,7 +432,8 @@ PEKF_DEV void quat_to_rotm(const double *q, double *M) {
 // whatever formula we use: R' and numpy's SVD rotation differ in the last bits), and an exactly
 // identity world rotation -- the one input where it is deterministic (NaN) -- does not arise from
 // Fw R'.  The well-conditioned Q4 z value is returned instead.
-PEKF_DEV void wahba_quat_toward(const RefW &W, const Frame &V, double ka, double km, const double *z, double *v,
+template <class RW, std::enable_if_t<RW::kRefBasis, int> = 0>
+PEKF_DEV void wahba_quat_toward(const RW &W, const Frame &V, double ka, double km, const double *z, double *v,
                                 double &sc) {
     const double kw = km * W.b2W, kb = km * W.b1W;
     double p = ka * W.aW * V.alpha + kb * V.beta1 + kw * V.beta2;
@@ -434,15 +452,16 @@ PEKF_DEV void wahba_quat_toward(const RefW &W, const Frame &V, double ka, double
     q4_times(R, z, v, nv, t0);
     sc = rsqrt<true>(nv);
     if (PEKF_TAKEN(nv < 1.0, false)) {
-        double Fw[9], Rw[9], zw[4], vw[4];
-        quat_to_rotm(W.q, Fw);
+        double Fw[9], Rw[9], zw[4], vw[4], qw[4];
+        W.quat(qw);
+        quat_to_rotm(qw, Fw);
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
             for (int j = 0; j < 3; ++j) Rw[3 * i + j] = Fw[3 * i] * R[j] + Fw[3 * i + 1] * R[3 + j] + Fw[3 * i + 2] * R[6 + j];
-        qmul_left<false>(W.q, z, zw);
+        qmul_left<false>(qw, z, zw);
         rotm_to_quat_flip_reference(Rw, zw, vw, sc);
-        qmul_left<true>(W.q, vw, v);
+        qmul_left<true>(qw, vw, v);
     }
     (void)t0;
 }
@@ -501,7 +520,8 @@ PEKF_DEV float recip(float x) {
 // (ExtendedKalmanFilter.py:44-47,52-55,61,63), returned DOUBLED: 2S, every entry exactly twice
 // S's (a power-of-two factor commutes with rounding), so that the gyro enters only as w (the raw
 // sample) and h -- S itself would need w/4 as well.  g2 = 2g, r2 = 2r; n2 = |x|^2 (shared with
-// rk4_closed's normalisation); th2 = |h|^2.  The caller folds the factor into its constants:
+// rk4_closed's normalisation); th2 = |h|^2; g2x = 2g / |x|^2 for an x that stands for the unit
+// x / |x| (g2 otherwise).  The caller folds the factor into its constants:
 // (2S)^-1 = S^-1 / 2 exactly, and the update (X normalised, P = rI - r^2 S^-1) is unchanged.
 //
 // Omega(h) is the matrix of right multiplication by the pure quaternion h, v -> v (x) h.  In the
@@ -513,7 +533,8 @@ PEKF_DEV float recip(float x) {
 // u needs only the trace butterflies of P's diagonal and the sums / differences of its off-diagonal
 // pairs: 71 FP64 operations for 2S against 96 for the direct Omega P Omega^T + Jb Q Jb^T + rI.
 template <typename T>
-PEKF_DEV Sym4T<T> innovation_cov2(const Sym4T<T> &P, const T *h, const T *w, T th2, const T *x, T n2, T g2, T r2) {
+PEKF_DEV Sym4T<T> innovation_cov2(const Sym4T<T> &P, const T *h, const T *w, T th2, const T *x, T n2, T g2, T r2,
+                                  T g2x) {
     // U = 4u, U_a = D_aa h_a + sum_{b != a} D_ab h_b with D_ab = tr(L(e_a) R(e_b) P):
     //   D_11 = -P00 - P11 + P22 + P33, D_22 = -P00 + P11 - P22 + P33, D_33 = -P00 + P11 + P22 - P33,
     //   D_12 = 2(P03 - P12), D_21 = -2(P03 + P12), D_13 = -2(P02 + P13), D_31 = 2(P02 - P13),
@@ -530,7 +551,7 @@ PEKF_DEV Sym4T<T> innovation_cov2(const Sym4T<T> &P, const T *h, const T *w, T t
     // diagonal constant: 2 (2|h|^2 tr(P)/4 + g |x|^2 + r), -/+ 4u.h
     const T base = fma(th2, tr, fma(g2, n2, r2));
     const T b0 = base - uh, bk = base + uh;
-    const T gx0 = g2 * x[0], gx1 = g2 * x[1], gx2 = g2 * x[2], gx3 = g2 * x[3];
+    const T gx0 = g2x * x[0], gx1 = g2x * x[1], gx2 = g2x * x[2], gx3 = g2x * x[3];
     Sym4T<T> o;
     o.a00 = fma(nt, P.a00, fma(-gx0, x[0], b0));
     o.a01 = fma(nt, P.a01, fma(-gx0, x[1], c0));
@@ -555,9 +576,10 @@ PEKF_DEV Sym4T<T> innovation_cov2(const Sym4T<T> &P, const T *h, const T *w, T t
 // (N' = D N D):
 //   S^ = 2 A N' A^T + (2/beta)(r|h|^2 + r) I + (2g/beta)(|x|^2 I - x x^T),
 // innovation_cov2's algebra on N' with gb = 2g/beta, rb = 2r/beta (= sqrt 2) for 2g, 2r, and one
-// operation more (tr N + rb).
+// operation more (tr N + rb); gbx = gb / |x|^2 as innovation_cov2's g2x.
 template <typename T>
-PEKF_DEV Sym4T<T> innovation_cov_n(const Sym4T<T> &N, const T *h, const T *w, T th2, const T *x, T n2, T gb, T rb) {
+PEKF_DEV Sym4T<T> innovation_cov_n(const Sym4T<T> &N, const T *h, const T *w, T th2, const T *x, T n2, T gb, T rb,
+                                   T gbx) {
     const T sp = N.a00 + N.a11, dp = N.a11 - N.a00, sq = N.a22 + N.a33, dq = N.a22 - N.a33;
     const T tr = sp + sq, d11 = sq - sp, d22 = dp - dq, d33 = dp + dq;
     const T u0 = fma(d11, h[0], fma(N.a12 - N.a03, w[1], (N.a02 + N.a13) * w[2]));
@@ -569,7 +591,7 @@ PEKF_DEV Sym4T<T> innovation_cov_n(const Sym4T<T> &N, const T *h, const T *w, T 
     const T nt = T(-2) * th2;
     const T base = fma(th2, tr + rb, fma(gb, n2, rb));
     const T b0 = base - uh, bk = base + uh;
-    const T gx0 = gb * x[0], gx1 = gb * x[1], gx2 = gb * x[2], gx3 = gb * x[3];
+    const T gx0 = gbx * x[0], gx1 = gbx * x[1], gx2 = gbx * x[2], gx3 = gbx * x[3];
     Sym4T<T> o;
     o.a00 = fma(nt, N.a00, fma(-gx0, x[0], b0));
     o.a01 = fma(nt, N.a01, fma(-gx0, x[1], c0));
@@ -636,12 +658,15 @@ PEKF_DEV Sym4T<T> spd_inverse_schur(const Sym4T<T> &S) {
 // h_w = w/2 (so Omega(h_w) = 0.5*Omega(w), the reference's W).  z = ca x + cb 0.5*Omega(w) x and,
 // since 0.5*Omega(w) is skew with square -|h_w|^2 I, |z|^2 = (ca^2 + cb^2 |h_w|^2) |x|^2 exactly:
 // the normalisation factor is known before z is formed and folds into ca and cb.  n2 = |x|^2.
-PEKF_DEV void rk4_closed(const double *x, double n2, double dt_ns, const double *hw, double th2, double *z) {
+// kk = ca^2 + cb^2 |h_w|^2 and in = 1 / sqrt(kk n2) are returned for callers that need 1/n2 = in^2 kk.
+PEKF_DEV void rk4_closed(const double *x, double n2, double dt_ns, const double *hw, double th2, double *z,
+                         double &kk, double &in) {
     const double h = dt_ns * kNsToS;
     const double xx = (h * h) * th2;
     const double ca = 1.0 - 0.5 * xx + xx * xx * (1.0 / 24.0);
     const double cb = h * (1.0 - xx * (1.0 / 6.0));
-    const double in = rsqrt<true>((ca * ca + (cb * cb) * th2) * n2);
+    kk = ca * ca + (cb * cb) * th2;
+    in = rsqrt<true>(kk * n2);
     const double a = ca * in, c = cb * in;
     const double w0 = c * hw[0], w1 = c * hw[1], w2 = c * hw[2];
     // z = a x + Omega(c h_w) x, rows of Omega: [0,-w0,-w1,-w2] [w0,0,w2,-w1] [w1,-w2,0,w0] [w2,w1,-w0,0]
@@ -649,6 +674,11 @@ PEKF_DEV void rk4_closed(const double *x, double n2, double dt_ns, const double 
     z[1] = a * x[1] + w0 * x[0] + w2 * x[2] - w1 * x[3];
     z[2] = a * x[2] + w1 * x[0] - w2 * x[1] + w0 * x[3];
     z[3] = a * x[3] + w2 * x[0] + w1 * x[1] - w0 * x[2];
+}
+
+PEKF_DEV void rk4_closed(const double *x, double n2, double dt_ns, const double *hw, double th2, double *z) {
+    double kk, in;
+    rk4_closed(x, n2, dt_ns, hw, th2, z, kk, in);
 }
 
 PEKF_DEV void rk4_closed(const double *x, double n2, double dt_ns, const double *hw, double *z) {

@@ -144,7 +144,12 @@ __device__ __forceinline__ StepK<PT> step_consts(double qs, double rs) {
     return {(PT)(2.0 * g), (PT)(2.0 * rs), (PT)rs, (PT)(2.0 * (rs * rs)), 0.5 / rs};
 }
 
-template <typename PT, bool MC = false, typename Ref>
+// MC (the multi-record loop) also leaves X unnormalised, X = x / |x| with |x| ~ 0.7: its norm
+// folds into the next record's RK4 normalisation (z = rk4(x) / |rk4(x)| whatever |x|) and Jb term
+// (g (|X|^2 I - X X^T) = g I - (g / |x|^2) x x^T, |X|^2 = 1 as state_norm2 snaps it), and
+// 1/|x|^2 = in^2 kk comes from RK4's own rsqrt: 8 operations instead of the 13 of normalising X.
+// LAZY: x arrives that way (n2 ignored); the caller normalises once at the end of the launch.
+template <typename PT, bool MC = false, bool LAZY = false, typename Ref>
 __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> &P, const Ref &Wf, const StepK<PT> &k,
                                                 const double *gy, double dt_ns, bool missing,
                                                 const double *acc, const double *mag) {
@@ -154,13 +159,16 @@ __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> 
     const PT hp[3] = {(PT)hw[0], (PT)hw[1], (PT)hw[2]};
     const PT wp[3] = {(PT)gy[0], (PT)gy[1], (PT)gy[2]};
     const PT xp[4] = {(PT)x[0], (PT)x[1], (PT)x[2], (PT)x[3]};
+    double z[4], kk, irk;
+    rk4_closed(x, LAZY ? x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3] : n2, dt_ns, hw, th2, z, kk,
+               irk);                                                // (:62)
+    const PT g2x = LAZY ? (PT)((irk * irk) * kk) * k.g2 : k.g2;     // 2g / |x|^2
+    const PT n2p = LAZY ? PT(1) : (PT)n2;
     // S2 = 2S, S = P- + rI with P- = A P A^T + Jb Q Jb^T, Jb from the prior X (:60-61, :63).
     // Exactly twice S (see innovation_cov2), so every result below is bit-identical to the
     // undoubled recursion: (2S)^-1 = S^-1/2, and the constants absorb the factor.
-    const Sym4T<PT> S2 = MC ? innovation_cov_n<PT>(P, hp, wp, (PT)th2, xp, (PT)n2, k.g2, k.r2)
-                            : innovation_cov2<PT>(P, hp, wp, (PT)th2, xp, (PT)n2, k.g2, k.r2);
-    double z[4];
-    rk4_closed(x, n2, dt_ns, hw, th2, z);                           // (:62)
+    const Sym4T<PT> S2 = MC ? innovation_cov_n<PT>(P, hp, wp, (PT)th2, xp, n2p, k.g2, k.r2, g2x)
+                            : innovation_cov2<PT>(P, hp, wp, (PT)th2, xp, n2p, k.g2, k.r2, g2x);
 
     if (missing) {
         // Wahba-skip: no Correction for this record (X = z, P = P- = S - rI)
@@ -196,8 +204,12 @@ __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> 
         const double sr = sc * k.sy;
         const double x0 = fma(v[0], sr, MC ? u0 : -u0), x1 = fma(v[1], sr, MC ? u1 : -u1);
         const double x2 = fma(v[2], sr, -u2), x3 = fma(v[3], sr, -u3);
-        const double in = rsqrt<true>(x0 * x0 + x1 * x1 + x2 * x2 + x3 * x3);
-        x[0] = x0 * in; x[1] = x1 * in; x[2] = x2 * in; x[3] = x3 * in;
+        if (MC) {
+            x[0] = x0; x[1] = x1; x[2] = x2; x[3] = x3;
+        } else {
+            const double in = rsqrt<true>(x0 * x0 + x1 * x1 + x2 * x2 + x3 * x3);
+            x[0] = x0 * in; x[1] = x1 * in; x[2] = x2 * in; x[3] = x3 * in;
+        }
         // P = P- - K P- = r K = r I - r^2 S^-1 = r I - (2 r^2) Si (:78)
         if (MC) {
             P = Si;  // P = rI + beta D N D: nothing to compute
@@ -302,25 +314,35 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     auto next = [&](uint64_t o8) -> uint64_t { o8 += row8; return o8 == wrap8 ? 0 : o8; };
 
     // One record: Prediction + Correction (main_file.py:42-45) on (x, P) in registers.
-    auto step = [&](const Rec &cur, int32_t t, double n2, const auto &ref) {
-        // the multi-record loop (RefW) carries M, the one-record launch (Frame) P
-        constexpr bool MC = std::is_same<std::decay_t<decltype(ref)>, RefW>::value;
+    auto step = [&](const Rec &cur, int32_t t, double n2, const auto &ref, auto lazy) {
+        // the multi-record loop (RefW) carries N and an unnormalised X, the one-record launch
+        // (Frame) P and X; lazy: X arrives unnormalised (every multi-record step after the first)
+        constexpr bool MC = !std::is_same<std::decay_t<decltype(ref)>, Frame>::value;
         if (!COUNTS || t < my_steps) {
             const double gy[3] = {cur.gd.x, cur.gd.y, cur.gd.z};
             const uint32_t word = __float_as_uint(cur.gd.w);
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
-            ekf_record_step<PT, MC>(x, n2, P, ref, step_consts<PT, MC>(qs, rs), gy, (double)(word & 0x7FFFFFFFu),
-                                    (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
+            ekf_record_step<PT, MC, decltype(lazy)::value>(x, n2, P, ref, step_consts<PT, MC>(qs, rs), gy,
+                                                           (double)(word & 0x7FFFFFFFu),
+                                                           (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
         }
         if (TRAJ) {
             double xo[4] = {x[0], x[1], x[2], x[3]};
-            if constexpr (MC) qmul_left<false>(ref.q, x, xo);
+            if constexpr (MC) {
+                const double in = rsqrt<true>(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]);
+                const double xn[4] = {x[0] * in, x[1] * in, x[2] * in, x[3] * in};
+                double qw[4];
+                ref.quat(qw);
+                qmul_left<false>(qw, xn, xo);
+            }
             double2 *o = reinterpret_cast<double2 *>(traj + (int64_t)t * batch * 4) + 2 * (int64_t)lane;
             o[0] = make_double2(xo[0], xo[1]);
             o[1] = make_double2(xo[2], xo[3]);
         }
     };
+    using eager = std::false_type;
+    using lazy = std::true_type;
 
     // Time loop, unrolled by two with ping-pong records: the next row's record is always in
     // flight while the current one is processed, and no registers are copied between steps.
@@ -330,7 +352,7 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     uint64_t o8 = (uint64_t)(step0 % window) * row8;
     Rec ra = load_row(o8), rb;
     if constexpr (ONE) {
-        step(ra, 0, state_norm2(x), Wf);
+        step(ra, 0, state_norm2(x), Wf, eager{});
         store_state<SOA>(Xio, Pio, b, batch, x, P);
         return;
     }
@@ -339,15 +361,24 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     // the state is rotated in once and out once per launch.  A filter with no records in this
     // launch (COUNTS) rotates by the identity, which is exact, and its state is not written back.
     // Inside the loop the covariance is carried as N, P = rI + beta D N D (StepK).
-    RefW Wr;
+    // Without trajectory output q_W is recomputed at the launch's end (and in the rare fallback)
+    // rather than held through the loop (RefWLazy: 8 VGPRs).
+    using RW = typename std::conditional<TRAJ, RefW, RefWLazy>::type;
+    RW Wr;
     Wr.aW = Wf.alpha; Wr.b1W = Wf.beta1; Wr.b2W = Wf.beta2;
-    frame_quat(Wf, Wr.q);
-    if (COUNTS && my_steps == 0) { Wr.q[0] = 1.0; Wr.q[1] = Wr.q[2] = Wr.q[3] = 0.0; }
     {
+        double qw[4];
+        frame_quat(Wf, qw);
+        if constexpr (TRAJ) {
+            if (COUNTS && my_steps == 0) { qw[0] = 1.0; qw[1] = qw[2] = qw[3] = 0.0; }
+            Wr.q[0] = qw[0]; Wr.q[1] = qw[1]; Wr.q[2] = qw[2]; Wr.q[3] = qw[3];
+        } else {
+            Wr.pair = refs + 6 * b;
+        }
         double xw[4];
-        qmul_left<true>(Wr.q, x, xw);
+        qmul_left<true>(qw, x, xw);
         x[0] = xw[0]; x[1] = xw[1]; x[2] = xw[2]; x[3] = xw[3];
-        P = sym_rotate<true>(Wr.q, P);
+        P = sym_rotate<true>(qw, P);
         const PT ib = (PT)(1.0 / (kSqrt2 * rs)), rp = (PT)rs;
         P = {(P.a00 - rp) * ib, P.a01 * ib, -P.a02 * ib, -P.a03 * ib, (P.a11 - rp) * ib,
              -P.a12 * ib, -P.a13 * ib, (P.a22 - rp) * ib, P.a23 * ib, (P.a33 - rp) * ib};
@@ -358,15 +389,15 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     const int32_t n32 = (int32_t)n_steps;
     o8 = next(o8);
     rb = load_row(o8);
-    step(ra, 0, state_norm2(x), Wr);
+    step(ra, 0, state_norm2(x), Wr, eager{});
     for (int32_t t = 1; t < n32;) {
         o8 = next(o8);
         ra = load_row(o8);
-        step(rb, t, 1.0, Wr);
+        step(rb, t, 1.0, Wr, lazy{});
         if (++t == n32) break;
         o8 = next(o8);
         rb = load_row(o8);
-        step(ra, t, 1.0, Wr);
+        step(ra, t, 1.0, Wr, lazy{});
         ++t;
     }
     if (COUNTS && my_steps == 0) return;
@@ -374,10 +405,13 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
         const PT be = (PT)(kSqrt2 * rs), rp = (PT)rs;
         P = {fma(be, P.a00, rp), be * P.a01, -be * P.a02, -be * P.a03, fma(be, P.a11, rp),
              -be * P.a12, -be * P.a13, fma(be, P.a22, rp), be * P.a23, fma(be, P.a33, rp)};
-        double xo[4];
-        qmul_left<false>(Wr.q, x, xo);
+        const double in = rsqrt<true>(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]);
+        const double xn[4] = {x[0] * in, x[1] * in, x[2] * in, x[3] * in};
+        double xo[4], qw[4];
+        Wr.quat(qw);
+        qmul_left<false>(qw, xn, xo);
         x[0] = xo[0]; x[1] = xo[1]; x[2] = xo[2]; x[3] = xo[3];
-        P = sym_rotate<false>(Wr.q, P);
+        P = sym_rotate<false>(qw, P);
     }
     store_state<SOA>(Xio, Pio, b, batch, x, P);
 }
