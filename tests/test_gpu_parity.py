@@ -204,6 +204,16 @@ def test_fused_run_other_noise_scales(eng, oracle_c, q, r):
     Xo, Po, to = oracle_c.run(rec, q=q, r=r, want_traj=True)
     assert _maxerr(tr.transpose(1, 0, 2), to) < PREC_GUARD
     assert _maxerr(f.get_state()[1], Po) < PREC_GUARD * max(1.0, r)
+    # the instantiation without trajectory output (q_W recomputed, the covariance carried as N
+    # with beta = sqrt(2) r, X unnormalised between records) in two chunks
+    g = eng.BatchedEKF(K, q=q, r=r)
+    win = eng.IMUWindow.from_records(rec)
+    g.run(win, n_steps=120)
+    g.run(win, n_steps=W - 120, step0=120)
+    X, P = g.get_state()
+    assert _maxerr(X, Xo) < PREC_GUARD
+    assert _maxerr(P, Po) < PREC_GUARD * max(1.0, r)
+    assert np.abs(np.linalg.norm(X, axis=1) - 1.0).max() < 1e-13
 
 
 def test_scale_c2_batch_sampled_against_oracle(eng, oracle_c):
