@@ -1,0 +1,33 @@
+#!/usr/bin/env bash
+# Profile refresh of the committed build on the gpurun box, parametrised by a tag (e.g. r2a):
+# GPU parity suite, smoke, kernel-trace summary of the C3 bench, the two PMC passes (reduced into
+# profiles/<round>/pmc_summary_c3.json), the C3/C2/C5/mixed bench lines, the RCCL path at world
+# size 1 and the kernels beside the headline.  Every step has its own time limit and the session
+# stops at the first crash/abort/timeout (scripts/gpu_session.sh).
+# usage (from the repo root, inside gpurun): scripts/refresh.sh <tag> <round-dir> [quick]
+#   quick: skip the C2/C5/mixed/dist/aux lines
+set -u
+tag=$1; rdir=$2; mode=${3:-full}
+B="python3 bench.py --cpu-baseline none --parity-samples 0"
+O=gpurun_out/$tag
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE"
+mkdir -p "$rdir"
+steps=(
+ "timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread"
+ "timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke()'"
+ "timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $B --steps 3 --warmup 1"
+ "timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- $B --steps 1 --warmup 0"
+ "timeout -s KILL 120 rocprofv3 --pmc $SQ -d $O/pmc_sq -o run --output-format csv -- $B --steps 1 --warmup 0"
+ "python3 scripts/pmc_summary.py $O/pmc_fetch/run_counter_collection.csv $O/pmc_sq/run_counter_collection.csv 1048576 10000 $rdir/pmc_summary_c3.json && cp $rdir/pmc_summary_c3.json $O/ && cp $O/trace/run_kernel_stats.csv $rdir/kernel_stats_c3.csv && cp $O/trace/run_kernel_stats.csv $O/"
+ "timeout -k 10 400 python bench.py > $O/bench_c3_f64.json"
+)
+if [ "$mode" = full ]; then
+ steps+=(
+ "timeout -k 10 300 python bench.py --batch 65536 --cpu-baseline none > $O/bench_c2_f64.json"
+ "timeout -k 10 300 python bench.py --missing --cpu-baseline none > $O/bench_c5_f64.json"
+ "timeout -k 10 300 python bench.py --precision mixed --cpu-baseline none > $O/bench_c3_mixed.json"
+ "timeout -k 10 300 python bench.py --dist --cpu-baseline none --steps 2 > $O/bench_dist1.json"
+ "timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/auxtrace -o aux --output-format csv -- python3 scripts/bench_aux.py > $O/aux_bench.json"
+ )
+fi
+exec scripts/gpu_session.sh "$tag" "${steps[@]}"
