@@ -379,10 +379,11 @@ __global__ __launch_bounds__(64) void k_call1(Blob b, double *out, int32_t *stat
 // (7.6 us round trip with an empty kernel, scripts/sync_probe.hip); a resident one-wave kernel
 // polling a mailbox in coherent pinned host memory answers in ~4 us (scripts/pingpong_probe.hip).
 // Mailbox (host memory, mapped):
-//   request  [0, 512): 8 lines of 64 B = 7 payload doubles + a stamp word (op << 32 | seq).  The
-//            host writes each line's payload, then its stamp; the wave reads all 8 lines with one
-//            512 B load and accepts a request only when the 8 stamps agree (a line is read as one
-//            snapshot, so an agreeing stamp implies that line's payload is the new one).
+//   request  [0, 512): 8 lines of 64 B = 7 payload doubles + a stamp word (hash32 of the line's
+//            payload << 32 | op << 16 | seq16).  The host writes each line's payload, then its
+//            stamp (release); the wave reads all 8 lines with one 512 B load and accepts a request
+//            when the 8 stamps agree on a new sequence number AND every line's payload matches its
+//            stamp's hash (the memory model does not promise a line to be read as one snapshot).
 //   response [1024, ...): outputs (doubles), status, then the sequence number, written last
 //            after a system-scope fence; the host polls it in its own memory.
 // The kernel always ends: it exits on a stop request or after kSvcIdleMs without a request
@@ -394,6 +395,39 @@ constexpr size_t kSvcRespOff = 1024, kSvcStatusOff = kSvcRespOff + 64 * 8, kSvcS
 constexpr size_t kSvcBytes = 2048;
 constexpr uint32_t kSvcStop = 0xFFFFu;
 constexpr int kSvcIdleMs = 5;
+
+// 32-bit mix of one request word and its position, XORed over a line's 7 payload words into the
+// line's stamp; the same function on both sides of the mailbox (32-bit multiplies only).
+__host__ __device__ inline uint32_t svc_mix(uint64_t w, uint32_t pos) {
+    uint32_t h = ((uint32_t)w ^ (pos * 0x9E3779B9u)) * 0x85EBCA6Bu;
+    h ^= ((uint32_t)(w >> 32) + (h >> 15)) * 0xC2B2AE35u;
+    return h ^ (h >> 16);
+}
+
+// XOR over each group of 8 lanes (DPP: quad_perm [1,0,3,2], [2,3,0,1], then row_half_mirror).
+__device__ inline uint32_t xor8(uint32_t h) {
+    h ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)h, 0xB1, 0xF, 0xF, false);
+    h ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)h, 0x4E, 0xF, 0xF, false);
+    h ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)h, 0x141, 0xF, 0xF, false);
+    return h;
+}
+
+// The request's operation on lane 0, out of line so that the polling loop carries none of its
+// hoisted constants (inlined, they were copied through AGPRs on every poll).
+__device__ __noinline__ void svc_run(uint32_t op, double *sh, int32_t *sh_status) {
+    // the payload as the Blob of k_call1 (same operand order, same device functions)
+    double v[kSvcPayload];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int j = 0; j < kSvcLinePayload; ++j) v[k * kSvcLinePayload + j] = sh[k * 8 + j];
+    double o[kCallMaxOut] = {};
+    int32_t st = 0;
+    dispatch1((int)op, v, o, &st);
+#pragma unroll
+    for (int k = 0; k < kCallMaxOut; ++k) sh[k] = o[k];  // static indices: o stays in registers
+    *sh_status = st;
+}
 
 __global__ __launch_bounds__(64) void k_service(char *box, unsigned long long idle_ticks) {
     __shared__ double sh[64];
@@ -408,9 +442,19 @@ __global__ __launch_bounds__(64) void k_service(char *box, unsigned long long id
     for (;;) {
         const uint64_t w = __hip_atomic_load(req + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
-        const uint32_t seq = __builtin_amdgcn_readlane(lo, 7), op = __builtin_amdgcn_readlane(hi, 7);
-        const bool torn = __any((lane & 7) == 7 && (lo != seq || hi != op));
-        if (torn || seq == done) {
+        const uint32_t tag = __builtin_amdgcn_readlane(lo, 7);
+        const uint32_t seq = tag & 0xFFFFu, op = tag >> 16;
+        bool wait = seq == done || __any((lane & 7) == 7 && lo != tag);
+        if (!wait) {
+            // Every line's stamp carries a hash of that line's 7 payload words (svc_mix): a line
+            // whose payload words predate its stamp -- the memory model does not promise a 64 B
+            // line to be read as one snapshot -- fails it and is read again at the next poll.  (A
+            // seqlock re-read behind an acquire fence would cost one more PCIe round trip per
+            // call: measured +1.2 us.)
+            const uint32_t h = xor8((lane & 7) == 7 ? 0u : svc_mix(w, (uint32_t)lane));
+            wait = __any((lane & 7) == 7 && h != hi);
+        }
+        if (wait) {
             if (wall_clock64() - t0 > idle_ticks) break;  // uniform
             __builtin_amdgcn_s_sleep(2);
             continue;
@@ -422,20 +466,7 @@ __global__ __launch_bounds__(64) void k_service(char *box, unsigned long long id
         sh[lane] = __longlong_as_double((long long)w);
         __syncthreads();
         const int n_out = call1_outputs((int)op);
-        if (lane == 0) {
-            // the payload as the Blob of k_call1 (same operand order, same device functions)
-            double v[kSvcPayload];
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-#pragma unroll
-                for (int j = 0; j < kSvcLinePayload; ++j) v[k * kSvcLinePayload + j] = sh[k * 8 + j];
-            double o[kCallMaxOut] = {};
-            int32_t st = 0;
-            dispatch1((int)op, v, o, &st);
-#pragma unroll
-            for (int k = 0; k < kCallMaxOut; ++k) sh[k] = o[k];  // static indices: o stays in registers
-            sh_status = st;
-        }
+        if (lane == 0) svc_run(op, sh, &sh_status);
         __syncthreads();
         if (lane < n_out) __hip_atomic_store(resp + lane, sh[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (lane == 0) __hip_atomic_store(resp_status, sh_status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -463,6 +494,7 @@ class Service {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
         Service &s = instances()[dev];
+        s.dev_ = dev;  // this instance serves device dev (its wall-clock rate sets the idle limit)
         return s.broken_ ? nullptr : &s;
     }
 
@@ -506,7 +538,7 @@ class Service {
             }
             std::memset(box_, 0, kSvcBytes);
             int khz = 0;
-            if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0) != hipSuccess || khz <= 0) khz = 100000;
+            if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_) != hipSuccess || khz <= 0) khz = 100000;
             idle_ticks_ = (unsigned long long)khz * kSvcIdleMs;
             static std::once_flag once;
             std::call_once(once, [] { std::atexit(Service::quiesce_all); });
@@ -529,15 +561,19 @@ class Service {
     }
 
     void post(uint32_t op, const double *in, size_t n_in) {
-        ++seq_;
-        const uint64_t stamp = ((uint64_t)op << 32) | seq_;
+        seq_ = (seq_ + 1) & 0xFFFFu;  // 16-bit sequence number: the stamp's low half is op << 16 | seq
+        const uint32_t tag = (op << 16) | seq_;
         for (int k = 0; k < 8; ++k) {
             double *line = reinterpret_cast<double *>(box_ + 64 * k);
+            uint32_t h = 0;
             for (int j = 0; j < kSvcLinePayload; ++j) {
                 const size_t i = (size_t)k * kSvcLinePayload + j;
                 line[j] = i < n_in ? in[i] : 0.0;
+                uint64_t bits;
+                std::memcpy(&bits, &line[j], sizeof bits);
+                h ^= svc_mix(bits, (uint32_t)(8 * k + j));
             }
-            __atomic_store_n(reinterpret_cast<uint64_t *>(line + 7), stamp, __ATOMIC_RELEASE);
+            __atomic_store_n(reinterpret_cast<uint64_t *>(line + 7), ((uint64_t)h << 32) | tag, __ATOMIC_RELEASE);
         }
     }
 
@@ -583,6 +619,7 @@ class Service {
     hipStream_t stream_ = nullptr;
     char *box_ = nullptr, *box_dev_ = nullptr;
     unsigned long long idle_ticks_ = 0;
+    int dev_ = 0;
     uint32_t seq_ = 0;
     std::atomic<bool> running_{false};  // read without the lock by quiesce_all
     bool broken_ = false;

@@ -329,12 +329,16 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
         }
         if (TRAJ) {
             double xo[4] = {x[0], x[1], x[2], x[3]};
+            // a filter with no records in this launch (COUNTS) repeats its stored X unchanged
+            // (x was rotated by the identity, which is exact; it is not normalised or written back)
             if constexpr (MC) {
-                const double in = rsqrt<true>(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]);
-                const double xn[4] = {x[0] * in, x[1] * in, x[2] * in, x[3] * in};
-                double qw[4];
-                ref.quat(qw);
-                qmul_left<false>(qw, xn, xo);
+                if (!COUNTS || my_steps > 0) {
+                    const double in = rsqrt<true>(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]);
+                    const double xn[4] = {x[0] * in, x[1] * in, x[2] * in, x[3] * in};
+                    double qw[4];
+                    ref.quat(qw);
+                    qmul_left<false>(qw, xn, xo);
+                }
             }
             double2 *o = reinterpret_cast<double2 *>(traj + (int64_t)t * batch * 4) + 2 * (int64_t)lane;
             o[0] = make_double2(xo[0], xo[1]);

@@ -172,12 +172,17 @@ def test_cyclic_window_ragged_batch_and_chunking(eng, oracle_c):
     Xo, Po, _ = oracle_c.run(rec, n_steps=150, step0=5)
     assert _maxerr(Xg, Xo) < PREC_GUARD
     assert _maxerr(Pg, Po) < PREC_GUARD
-    # chunked launches continue exactly where a single launch would be
+    # chunked launches continue where a single launch would be.  Each launch boundary rotates the
+    # state out of and back into the reference frame's basis and converts N <-> P, so the chunked
+    # run rounds differently at the boundary; the gain K = I - r S^-1 damps such ulp-level
+    # differences within a few records.  Checked to a rounding-level tolerance,
+    # not bit for bit: the agreement must not depend on the seed or the noise scales.
     g = eng.BatchedEKF(K)
     g.run(win, n_steps=70, step0=5)
     g.run(win, n_steps=80, step0=75)
     X2, P2 = g.get_state()
-    assert np.array_equal(X2, Xg) and np.array_equal(P2, Pg)
+    assert _maxerr(X2, Xg) <= 1e-15
+    assert _maxerr(P2, Pg) <= 1e-15 * max(1.0, float(np.abs(Pg).max()))
 
 
 def test_set_state_roundtrip_and_resume(eng, oracle_c):

@@ -110,6 +110,31 @@ def test_per_filter_counts_equal_truncated_launches(eng, layout):
         assert eq(tr[c:, sel], np.broadcast_to(Xg[sel], (N - c,) + Xg[sel].shape))
 
 
+@pytest.mark.parametrize("layout", ["aos", "soa"])
+def test_count_zero_filters_keep_a_non_unit_state(eng, layout):
+    """A filter with no records in a counted launch keeps its stored X and P bit for bit, and its
+    trajectory rows repeat that X, also when X is not unit (set_state takes any state)."""
+    K, W, N = 130, 24, 24
+    rec = synth.generate(np.arange(K), W, seed=31, missing=True)
+    win = eng.IMUWindow.from_records(rec)
+    rng = np.random.default_rng(3)
+    X0 = rng.normal(size=(K, 4)) * rng.uniform(0.5, 2.0, size=(K, 1))   # |X| != 1
+    A = rng.normal(size=(K, 4, 4))
+    P0 = np.einsum("kij,klj->kil", A, A) + 0.1 * np.identity(4)
+    counts = np.where(np.arange(K) % 3 == 0, 0, np.arange(K) % 17 + 2).astype(np.int32)
+    f = eng.BatchedEKF(K, layout=layout)
+    f.set_state(X0, P0)
+    tr = f.run(win, n_steps=N, want_traj=True, counts=counts)
+    X, P = f.get_state()
+    zero = counts == 0
+    assert _same(X[zero], X0[zero]) and _same(P[zero], P0[zero])
+    assert _same(tr[:, zero], np.broadcast_to(X0[zero], (N,) + X0[zero].shape))
+    # the other filters: rows after their last record repeat their final (normalised) X
+    for k in np.flatnonzero(~zero)[:8]:
+        assert _same(tr[counts[k]:, k], np.broadcast_to(X[k], (N - counts[k], 4)))
+        assert abs(float(np.linalg.norm(X[k])) - 1.0) < 1e-15
+
+
 def test_ragged_logs_share_one_launch(eng, tmp_path):
     """Two server logs of different lengths in one window: each filter consumes its own records."""
     with gzip.open(os.path.join(GOLDEN, "c1_log.txt.gz"), "rt") as fh:
