@@ -120,7 +120,7 @@ def main():
     ap.add_argument("--precision", choices=["f64", "mixed"], default="f64",
                     help="f64 (default, as the reference) or mixed (covariance recursion in f32)")
     ap.add_argument("--dist", action="store_true",
-                    help="use torch.distributed/RCCL even at world size 1 (exercises the gather path)")
+                    help="use the RCCL path (pekf_gather_dev) even at world size 1 (exercises the gather)")
     args = ap.parse_args()
     out_fd = StdoutForTheResult()
 
@@ -140,16 +140,18 @@ def main():
             cpu["c_oracle"] = {"error": str(e)}
         log("cpu baseline: %.0f steps/s on %d cores" % (cpu["value"], cpu["cores"]))
 
-    torch = dist = None
+    dist = None
     use_dist = world > 1 or args.dist
     if use_dist:
-        import torch  # before libpekf: the library then binds torch's HIP runtime
+        # torch.distributed only for the rendezvous (gloo, CPU): the RCCL id broadcast and the
+        # host barrier.  The data-path collectives are RCCL through libpekf (shard.Communicator).
+        # torch is imported before libpekf so that the process has ONE HIP runtime and ONE RCCL
+        # (the ones PyTorch-ROCm bundles; libpekf binds them by SONAME).
+        import torch  # noqa: F401
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local))  # RCCL over xGMI
+        dist.init_process_group("gloo", rank=rank, world_size=world)
 
     import numpy as np
 
@@ -158,14 +160,14 @@ def main():
     first, B = shard.shard_range(args.batch * world, rank, world)
     N, W = args.records, args.window
 
-    own_stream = None if use_dist else engine.Stream()  # keep the object alive for the whole run
-    stream = torch.cuda.current_stream().cuda_stream if use_dist else own_stream.handle
+    own_stream = engine.Stream()  # keep the object alive for the whole run
+    stream = own_stream.handle
+    comm = shard.Communicator(shard.exchange_unique_id(rank, world), world, rank) if use_dist else None
+    if comm is not None:
+        log("rank %d/%d: RCCL %d communicator on device %d" % (rank, world, shard.rccl_version(), comm.device))
 
     def sync():
-        if use_dist:
-            torch.cuda.synchronize()
-        else:
-            engine.check(engine.lib.pekf_stream_sync(stream))
+        engine.check(engine.lib.pekf_stream_sync(stream))
 
     def barrier():
         if use_dist:
@@ -176,40 +178,38 @@ def main():
     win = engine.IMUWindow(B, W).synthesize(seed=args.seed, first_filter=first, missing=args.missing,
                                             stream=stream)
     filt = engine.BatchedEKF(B, q=1.0, r=0.1, precision=args.precision)
-    xt = torch.empty((B, 4), dtype=torch.float64, device="cuda") if use_dist else None
+    recv = engine.DeviceBuffer(32 * B * world) if (use_dist and rank == 0) else None
     sync()
 
     total = args.warmup + args.steps
     ev = [(engine.Event(), engine.Event()) for _ in range(total)]
-    gathered = None
 
     def bench_step(k):
-        nonlocal gathered
         e0, e1 = ev[k]
         e0.record(stream)
         filt.run_async(win, N, (k * N) % W, stream)
         e1.record(stream)
-        if use_dist:
-            engine.check(engine.lib.pekf_memcpy_d2d(xt.data_ptr(), filt.X.ptr, 32 * B, stream))
-            gathered = shard.gather_quaternions(xt, rank, world, force_collective=True)
+        if use_dist:  # ONE RCCL gather of the final quaternions to rank 0 (pekf_gather_dev)
+            shard.gather_quaternions(comm, filt.X.ptr, B, recv, 0, stream)
 
     for k in range(args.warmup):
         bench_step(k)
         sync()
         log("warmup %d: kernel %.1f ms" % (k, ev[k][0].elapsed_ms(ev[k][1])))
 
-    barrier()
     sync()
+    barrier()
     t0 = time.perf_counter()
     for k in range(args.warmup, total):
         bench_step(k)
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
-    if use_dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    if use_dist:  # the slowest rank's time (RCCL max all-reduce)
+        tb = engine.DeviceBuffer(8).upload(np.array([elapsed], np.float64), stream)
+        comm.allreduce_max(tb.ptr, 1, stream)
+        elapsed = float(tb.download((1,), np.float64, stream)[0])
+        sync()
     kms = [ev[k][0].elapsed_ms(ev[k][1]) for k in range(args.warmup, total)]
     log("timed: %.3f s for %d steps; kernel ms %s" % (elapsed, args.steps, ", ".join("%.1f" % v for v in kms)))
 
@@ -253,7 +253,7 @@ def main():
                     "%d-record resident window replayed cyclically)" % W,
             "config": {"workload": workload_name(B, N, args.missing),
                        "filters_per_gpu": B, "global_filters": B * world, "records_per_step": N,
-                       "window_records": W, "parallelism": "dp%d (filter-batch shards, 1 RCCL gather)" % world},
+                       "window_records": W, "parallelism": "dp%d (filter-batch shards, 1 RCCL gather via pekf_gather_dev)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": (os.path.relpath(tsrc[0], ROOT) + " (2 x FETCH_SIZE, separate "
@@ -276,12 +276,15 @@ def main():
         }
         out_fd.emit(json.dumps(out))
     if use_dist:
-        if rank == 0 and gathered is not None:  # the gathered quaternions are the filters' final X
+        if rank == 0:  # the gathered quaternions are the filters' final X, rank 0's shard first
             Xr, _ = filt.get_state()
-            assert np.array_equal(gathered[:B].cpu().numpy(), Xr), "gather mismatch on rank 0"
-            log("gather: %d quaternions on rank 0 match rank 0's shard" % gathered.shape[0])
+            got = recv.download((world * B, 4), np.float64)
+            assert np.array_equal(got[:B], Xr), "gather mismatch on rank 0"
+            assert np.isfinite(got).all() and np.allclose(np.linalg.norm(got, axis=1), 1.0, atol=1e-12), \
+                "gathered quaternions of other ranks are not unit"
+            log("gather: %d quaternions on rank 0 (RCCL via pekf_gather_dev) match rank 0's shard" % got.shape[0])
+        comm.close()
         dist.destroy_process_group()
-
 
 # FP64 work per filter-step of the fused kernel, counted from its gfx950 ISA hot loop by
 # scripts/isa_count.py (DESIGN.md "FP64 budget"): FP64 VALU instructions, and the FLOP of
@@ -307,17 +310,18 @@ def workload_name(batch, records, missing):
 
 
 def measured_traffic(batch, records):
-    """HBM bytes per launch from the newest committed rocprofv3 PMC summary of the same config."""
-    import glob
-    best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary_*.json"))):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of the current build
+    (profiles/HEADLINE_PMC names it; scripts/refresh.sh produces it), if its config matches."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "HEADLINE_PMC")) as fh:
+            path = os.path.join(ROOT, fh.read().strip())
         with open(path) as fh:
             s = json.load(fh)
-        if s.get("config") == {"batch": batch, "records": records}:
-            best = (path, s)
-    if best is None:
+    except OSError:
         return None, None
-    return best[1]["hbm_traffic_bytes"], best
+    if s.get("config") != {"batch": batch, "records": records}:
+        return None, None
+    return s["hbm_traffic_bytes"], (path, s)
 
 if __name__ == "__main__":
     main()

@@ -38,6 +38,7 @@ extern "C" {
 #define PEKF_ERR_NODEVICE 4 /* no HIP device visible                                     */
 #define PEKF_ERR_SVD 5      /* non-finite Wahba matrix B: np.linalg.svd raises LinAlgError  */
                             /* "SVD did not converge" (Wahba.py:14)                         */
+#define PEKF_ERR_COMM 6     /* collective library (RCCL) unavailable or failed              */
 
 /* Bit 31 of a stream record's dt word: magnetometer sample missing ("Wahba-skip"). */
 #define PEKF_MISSING_MAG_BIT 0x80000000u
@@ -247,6 +248,37 @@ int pekf_filter_run(pekf_filter *f, int64_t n_steps, int64_t window, int64_t ste
 int pekf_synth_dev(int64_t batch, int64_t window, int64_t first_filter, uint32_t seed,
                    int missing_mag, const double *scales, double ar_w, void *plane_gd,
                    void *plane_am, void *plane_my, double *refs, void *stream);
+
+/* ---------------- sharding over GPUs: the one collective of the path ----------------
+ * Filters are independent (ExtendedKalmanFilter.py:6-80 shares nothing between KalmanFilter objects),
+ * so each GPU runs its own contiguous shard of the batch with no per-record exchange; the final
+ * quaternions are gathered to the root by ONE RCCL gather over xGMI (ncclGather, rccl.h:745).
+ * RCCL is loaded on first use (librccl.so.1; the copy already in the process if there is one).
+ * Every collective call below must be made by all ranks of the communicator; PEKF_ERR_COMM reports
+ * an RCCL failure or a missing librccl.
+ *
+ * One process per GPU: rank 0 makes an id, every rank receives it out of band (any channel:
+ * a file, a TCP store, MPI) and calls pekf_comm_init on its current device.
+ * One process for several GPUs: pekf_comm_init_all (ncclCommInitAll, rccl.h:236) gives one
+ * communicator per device, driven from one host thread with pekf_gather_multi_dev. */
+#define PEKF_COMM_ID_BYTES 128
+typedef struct pekf_comm pekf_comm;
+int pekf_comm_version(int *version); /* RCCL's version code, e.g. 22707 */
+int pekf_comm_unique_id(void *id /* PEKF_COMM_ID_BYTES */);
+int pekf_comm_init(const void *id, int nranks, int rank, pekf_comm **out);
+/* devices: ndev device indices (NULL = 0 .. ndev-1); out: ndev communicators, rank i on devices[i] */
+int pekf_comm_init_all(int ndev, const int *devices, pekf_comm **out);
+int pekf_comm_destroy(pekf_comm *c);
+int pekf_comm_rank(const pekf_comm *c, int *rank, int *nranks, int *device); /* outputs may be NULL */
+/* recv[nranks * count] on the root (rows in rank order) <- every rank's send[count]; device
+ * pointers, enqueued on stream.  recv is ignored (may be NULL) on the other ranks. */
+int pekf_gather_dev(pekf_comm *c, const double *send, int64_t count, double *recv, int root, void *stream);
+/* The same gather for the ndev communicators of pekf_comm_init_all, as one RCCL group:
+ * send[i] / streams[i] belong to comms[i]'s device; recv is on comms[root]'s device. */
+int pekf_gather_multi_dev(int ndev, pekf_comm *const *comms, const double *const *send, int64_t count,
+                          double *recv, int root, void *const *streams);
+/* buf[count] <- elementwise max over the ranks (in place), e.g. the slowest rank's wall time. */
+int pekf_allreduce_max_dev(pekf_comm *c, double *buf, int64_t count, void *stream);
 
 #ifdef __cplusplus
 }

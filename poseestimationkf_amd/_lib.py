@@ -19,6 +19,7 @@ PEKF_ERR_HIP = 2
 PEKF_ERR_SINGULAR = 3
 PEKF_ERR_NODEVICE = 4
 PEKF_ERR_SVD = 5
+PEKF_ERR_COMM = 6
 MISSING_MAG_BIT = 0x80000000
 RUN_MIXED_PRECISION = 0x1
 RUN_STATE_SOA = 0x2
@@ -96,6 +97,15 @@ SIGNATURES = {
     "pekf_log_read": [ctypes.c_char_p, _i64, _vp, _vp, _vp, _vp, _dp, _dp, _dp],
     "pekf_quat_to_rpy_dev": [_i64, _vp, _vp, _vp],
     "pekf_synth_dev": [_i64, _i64, _i64, _u32, _int, _dp, _dbl, _vp, _vp, _vp, _vp, _vp],
+    "pekf_comm_version": [_ip],
+    "pekf_comm_unique_id": [ctypes.c_char_p],
+    "pekf_comm_init": [ctypes.c_char_p, _int, _int, ctypes.POINTER(_vp)],
+    "pekf_comm_init_all": [_int, _ip, ctypes.POINTER(_vp)],
+    "pekf_comm_destroy": [_vp],
+    "pekf_comm_rank": [_vp, _ip, _ip, _ip],
+    "pekf_gather_dev": [_vp, _vp, _i64, _vp, _int, _vp],
+    "pekf_gather_multi_dev": [_int, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _i64, _vp, _int, ctypes.POINTER(_vp)],
+    "pekf_allreduce_max_dev": [_vp, _vp, _i64, _vp],
 }
 _RESTYPE = {"pekf_abi_version": ctypes.c_int, "pekf_last_error": ctypes.c_char_p}
 

@@ -1,6 +1,9 @@
-"""N > 1 path on CPU: world_size-2 gloo ranks each take a contiguous filter shard, run it
-(the C oracle stands in for the device here -- test only), and gather final quaternions to
-rank 0 with the same shard.gather_quaternions call bench.py uses over RCCL."""
+"""N > 1 path on CPU: world_size-2 gloo ranks rendezvous exactly as bench.py does (rank 0's
+128-byte RCCL id broadcast by shard.exchange_unique_id over the gloo group), each takes a
+contiguous filter shard and runs it (the C oracle stands in for the device here -- test only),
+and the shards' final quaternions, concatenated in rank order as pekf_gather_dev lays them out on
+the root, equal a single-process run.  The RCCL gather itself needs GPUs: tests/test_gpu_parity.py
+runs it through libpekf at world size 1 (and bench.py --dist on the box)."""
 import os
 import socket
 
@@ -26,12 +29,15 @@ def _rank_main(rank, world, port, global_batch, window, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        uid = shard.exchange_unique_id(rank, world, make_id=lambda: bytes(range(128)))
+        assert uid == bytes(range(128))  # every rank holds rank 0's id (a failure fails the exit code)
         first, count = shard.shard_range(global_batch, rank, world)
         rec = synth.generate(np.arange(first, first + count), window)
         X, _, _ = oracle_c.run(rec)
-        out = shard.gather_quaternions(torch.from_numpy(X), rank, world)
+        bufs = [torch.empty_like(torch.from_numpy(X)) for _ in range(world)] if rank == 0 else None
+        dist.gather(torch.from_numpy(X), gather_list=bufs, dst=0)  # stands in for RCCL (test only)
         if rank == 0:
-            q.put(out.numpy())
+            q.put((uid, torch.cat(bufs, dim=0).numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -54,10 +60,11 @@ def test_two_rank_gather_equals_single_process():
     procs = [ctx.Process(target=_rank_main, args=(r, 2, port, 16, 24, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = q.get(timeout=240)
+    uid, got = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     X, _, _ = oracle_c.run(synth.generate(np.arange(16), 24))
+    assert uid == bytes(range(128))
     assert got.shape == (16, 4)
     assert np.array_equal(got, X)
