@@ -198,6 +198,20 @@ def main():
         log("handle update %s (1M filters, FP64 records): %.3f ms" % (layout, ms))
         del h
     del ub, xo
+    # the same update from HOST arrays (pekf_filter_update: records in over PCIe through the pinned
+    # staging buffer, X out): the PCIe-inclusive rate of the host-buffer boundary (never the headline)
+    hg, ha, hm = (np.ascontiguousarray(rng.normal(size=(B1, 3))) for _ in range(3))
+    h = engine.FilterHandle(a0, m0, layout="soa")
+    for i in range(13):
+        if i == 3:
+            t0 = time.perf_counter()
+        xh = h.update(hg, np.full(B1, 10_000_000 * (i + 1), np.int64), ha, hm)
+    ms = (time.perf_counter() - t0) / 10 * 1e3
+    res["handle_update_host_soa"] = {"filters": B1, "wall_ms": ms, "updates_per_s": B1 / (ms * 1e-3),
+                                     "pcie_bytes_per_filter": 80 + 32,
+                                     "pcie_gbs": B1 * 112 / (ms * 1e-3) / 1e9, "x_finite": bool(np.isfinite(xh).all())}
+    log("handle update from host arrays (1M filters, PCIe-inclusive): %.3f ms" % ms)
+    del h
 
     # ---- per-call operators at n = 1M (device pointers)
     n = 1 << 20

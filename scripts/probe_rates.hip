@@ -32,6 +32,10 @@ __global__ __launch_bounds__(256) void k_probe(double *out, double seed) {
     if (KIND == 4) CHAINS(asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(f[c]) : "v"(f[(c + 1) & 7])))
     if (KIND == 5) CHAINS(v[c] = v[c] * a)
     if (KIND == 6) CHAINS(f[c] = __builtin_amdgcn_rsqf(f[c]))
+    if (KIND == 7) CHAINS(asm volatile("v_cvt_f32_f64 %0, %1" : "+v"(f[c]) : "v"(v[c])))
+    if (KIND == 8) CHAINS(f[c] = __builtin_amdgcn_rcpf(f[c]))
+    if (KIND == 9) CHAINS(f[c] = fmaf(f[c], (float)a, (float)b))
+    if (KIND == 10) CHAINS(v[c] = v[c] + a)
     double s = 0;
     for (int c = 0; c < 8; ++c) s += v[c] + f[c];
     if (s == 12345.678) out[threadIdx.x] = s;  // keep the chains alive
@@ -56,10 +60,11 @@ float run(double *out) {
 int main() {
     double *out;
     CK(hipMalloc(&out, 4096));
-    const char *names[] = {"v_fma_f64", "v_rsq_f64", "v_rcp_f64", "v_cvt_f64_f32",
-                           "v_cndmask_b32", "v_mul_f64", "v_rsq_f32"};
-    float t[7] = {run<0>(out), run<1>(out), run<2>(out), run<3>(out), run<4>(out), run<5>(out), run<6>(out)};
-    for (int k = 0; k < 7; ++k)
+    const char *names[] = {"v_fma_f64", "v_rsq_f64", "v_rcp_f64", "v_cvt_f64_f32", "v_cndmask_b32", "v_mul_f64",
+                           "v_rsq_f32", "v_cvt_f32_f64", "v_rcp_f32", "v_fma_f32", "v_add_f64"};
+    float t[11] = {run<0>(out), run<1>(out), run<2>(out), run<3>(out), run<4>(out), run<5>(out),
+                   run<6>(out), run<7>(out), run<8>(out), run<9>(out), run<10>(out)};
+    for (int k = 0; k < 11; ++k)
         printf("%-40s %8.3f ms  cost %.2f x v_fma_f64\n", names[k], t[k], t[k] / t[0]);
     CK(hipFree(out));
     return 0;
