@@ -293,7 +293,7 @@ def main():
 # loop (scripts/loop_blocks.py on the hipcc -S listing: the fallback bodies sit behind
 # s_cbranch_execz); FP64 instructions and FLOP from scripts/isa_count.py on the same blocks.  The
 # PMC pass in profiles/ counts the executed total (SQ_INSTS_VALU per wave-step).
-ISA_COUNTS = {"f64": {"flop": 447, "fp64_instr": 308, "valu_instr": 312},
+ISA_COUNTS = {"f64": {"flop": 436, "fp64_instr": 298, "valu_instr": 301},
               "mixed": {"flop": 240, "fp64_instr": 191, "valu_instr": 329}}  # mixed: + ~130 f32 instructions
 FLOP_PER_STEP = ISA_COUNTS["f64"]["flop"]
 FP64_INSTR_PER_STEP = ISA_COUNTS["f64"]["fp64_instr"]

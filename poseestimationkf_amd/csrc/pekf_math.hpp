@@ -180,14 +180,75 @@ PEKF_DEV double recip(double x) {
     return r;
 }
 
-template <bool FAST>
+// ------------------------------- VOP3 output modifier (omod) ---------------------------------
+// An exact halving folded into the instruction that produces the value (omod div:2): no separate
+// v_mul_f64 by 0.5.  The hardware applies omod only with the MODE register's IEEE bit clear and
+// FP64 denormals flushed (scripts/omod_probe.hip, profiles/r2/probes/omod_probe.txt: with either
+// left at the compute default the modifier is silently ignored), so only code between
+// OmodMode::enter() and leave() may use these.  Halving commutes with rounding, so each result is
+// bit-identical to the multiply by 0.5 it replaces; none of the values is denormal, and the one
+// difference -- omod turns -0 into +0 -- reaches no result (it only ever feeds further sums).
+PEKF_DEV double fma_half(double a, double b, double c) {  // (a b + c) / 2
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3 div:2" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+PEKF_DEV double fma_half_nc(double a, double b, double c) {  // (a b - c) / 2
+    double d;
+    asm("v_fma_f64 %0, %1, %2, -%3 div:2" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+PEKF_DEV double mul_half(double a, double b) {  // a b / 2
+    double d;
+    asm("v_mul_f64 %0, %1, %2 div:2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+PEKF_DEV double add_half(double a, double b) {  // (a + b) / 2
+    double d;
+    asm("v_add_f64 %0, %1, %2 div:2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+PEKF_DEV double sub_half(double a, double b) {  // (a - b) / 2
+    double d;
+    asm("v_add_f64 %0, %1, -%2 div:2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+PEKF_DEV double newton_half(double t, double y) {  // (t y + 1) / 2
+    double d;
+    asm("v_fma_f64 %0, %1, %2, 1.0 div:2" : "=v"(d) : "v"(t), "v"(y));
+    return d;
+}
+
+// MODE register (hwreg 1) bits 9:6 = IEEE, DX10_CLAMP, FP_DENORM(f64/f16) hi/lo.  enter() clears
+// IEEE and flushes FP64/FP16 denormals (DX10_CLAMP kept), leave() restores what the wave had.  The
+// compiler models s_setreg of MODE as a definition every FP instruction reads, so no arithmetic
+// moves across either call.  Away from min/max (not used between them) and denormal values (none
+// arise: every quantity is a normalised sensor sample, a unit quaternion, a covariance entry of
+// order r or their products), the arithmetic is that of the default mode.
+struct OmodMode {
+    static constexpr int kField = 1 | (6 << 6) | (3 << 11);  // hwreg(HW_REG_MODE, 6, 4)
+    unsigned saved = 0;
+    PEKF_DEV void enter() {
+        saved = (unsigned)__builtin_amdgcn_s_getreg(kField);
+        __builtin_amdgcn_s_setreg(kField, (int)(saved & 0x4u));
+    }
+    PEKF_DEV void leave() const { __builtin_amdgcn_s_setreg(kField, (int)saved); }
+};
+
+// FAST = 0: IEEE; 1: hardware seed + one Newton step; 2: the same step with its 1/2 folded into
+// the fma by omod (bit-identical to 1; only inside OmodMode).
+template <int FAST>
 PEKF_DEV double rsqrt(double x) {
     if (!FAST) return 1.0 / sqrt(x);
     double y = __builtin_amdgcn_rsq(x);
 #pragma unroll
     for (int it = 0; it < kNewtonSteps; ++it) {
-        const double e = fma(-x * y, y, 1.0);  // 1 - x y^2
-        y = fma(y, 0.5 * e, y);
+        if (FAST == 2) {
+            y = fma(y, newton_half(-x * y, y), y);  // (1 - x y^2) / 2 in one instruction
+        } else {
+            const double e = fma(-x * y, y, 1.0);  // 1 - x y^2
+            y = fma(y, 0.5 * e, y);
+        }
     }
     return y;
 }
@@ -203,7 +264,7 @@ struct Frame {
     double alpha, beta1, beta2;
 };
 
-template <bool FAST = false>
+template <int FAST = 0>
 PEKF_DEV void make_frame(const double *a, const double *m, Frame &F, double sg = 1.0) {
     const double sa = a[0] * a[0] + a[1] * a[1] + a[2] * a[2];
     const double ia = rsqrt<FAST>(sa);
@@ -432,13 +493,13 @@ PEKF_DEV void quat_to_rotm(const double *q, double *M) {
 // whatever formula we use: R' and numpy's SVD rotation differ in the last bits), and an exactly
 // identity world rotation -- the one input where it is deterministic (NaN) -- does not arise from
 // Fw R'.  The well-conditioned Q4 z value is returned instead.
-template <class RW, std::enable_if_t<RW::kRefBasis, int> = 0>
+template <int F = 1, class RW, std::enable_if_t<RW::kRefBasis, int> = 0>
 PEKF_DEV void wahba_quat_toward(const RW &W, const Frame &V, double ka, double km, const double *z, double *v,
                                 double &sc) {
     const double kw = km * W.b2W, kb = km * W.b1W;
     double p = ka * W.aW * V.alpha + kb * V.beta1 + kw * V.beta2;
     double s = kw * V.beta1 - kb * V.beta2;
-    const double ih = rsqrt<true>(p * p + s * s);
+    const double ih = rsqrt<F>(p * p + s * s);
     p *= ih;
     s *= ih;
     double R[9];
@@ -450,7 +511,7 @@ PEKF_DEV void wahba_quat_toward(const RW &W, const Frame &V, double ka, double k
     }
     double nv, t0;
     q4_times(R, z, v, nv, t0);
-    sc = rsqrt<true>(nv);
+    sc = rsqrt<F>(nv);
     if (PEKF_TAKEN(nv < 1.0, false)) {
         double Fw[9], Rw[9], zw[4], vw[4], qw[4];
         W.quat(qw);
@@ -467,6 +528,7 @@ PEKF_DEV void wahba_quat_toward(const RW &W, const Frame &V, double ka, double k
 }
 
 // Y = v * sc in the world basis (the per-record kernels)
+template <int F = 1>
 PEKF_DEV void wahba_quat_toward(const Frame &W, const Frame &V, double ka, double km, const double *z, double *v,
                                 double &sc) {
     double R[9];
@@ -606,6 +668,40 @@ PEKF_DEV Sym4T<T> innovation_cov_n(const Sym4T<T> &N, const T *h, const T *w, T 
     return o;
 }
 
+// innovation_cov_n in FP64 from the raw gyro sample w alone, for the omod build of the multi-record
+// loop (OmodMode): every product with h = w/2 becomes the product with w halved by the instruction
+// that forms it (omod div:2), and th2x2 = 2|h|^2 = |w|^2/2 replaces both |h|^2 and -2|h|^2 (the
+// latter as a negated operand), so the gyro needs no scaling at all.  Every value equals
+// innovation_cov_n's bit for bit: d_aa h_a = (d_aa/2) w_a, u.h = (u.w)/2 and u x h = (u x w)/2 with
+// each rounding of a halved exact sum, |h|^2 (tr + rb) = th2x2 ((tr + rb)/2).  rbh = rb / 2.
+PEKF_DEV Sym4 innovation_cov_n_w(const Sym4 &N, const double *w, double th2x2, const double *x, double n2, double gb,
+                                 double rb, double rbh, double gbx) {
+    const double sp = N.a00 + N.a11, dp = N.a11 - N.a00, sq = N.a22 + N.a33, dq = N.a22 - N.a33;
+    const double trh = add_half(sp, sq) + rbh;  // (tr + rb) / 2
+    const double d11h = sub_half(sq, sp), d22h = sub_half(dp, dq), d33h = add_half(dp, dq);
+    const double u0 = fma(d11h, w[0], fma(N.a12 - N.a03, w[1], (N.a02 + N.a13) * w[2]));
+    const double u1 = fma(d22h, w[1], fma(N.a01 - N.a23, w[2], (N.a03 + N.a12) * w[0]));
+    const double u2 = fma(d33h, w[2], fma(N.a13 - N.a02, w[0], -(N.a01 + N.a23) * w[1]));
+    const double uh = fma_half(u0, w[0], fma(u1, w[1], u2 * w[2]));
+    const double c0 = fma_half_nc(u1, w[2], u2 * w[1]), c1 = fma_half_nc(u2, w[0], u0 * w[2]);
+    const double c2 = fma_half_nc(u0, w[1], u1 * w[0]);
+    const double base = fma(th2x2, trh, fma(gb, n2, rb));
+    const double b0 = base - uh, bk = base + uh;
+    const double gx0 = gbx * x[0], gx1 = gbx * x[1], gx2 = gbx * x[2], gx3 = gbx * x[3];
+    Sym4 o;
+    o.a00 = fma(-th2x2, N.a00, fma(-gx0, x[0], b0));
+    o.a01 = fma(-th2x2, N.a01, fma(-gx0, x[1], c0));
+    o.a02 = fma(th2x2, N.a02, fma(-gx0, x[2], c1));
+    o.a03 = fma(th2x2, N.a03, fma(-gx0, x[3], c2));
+    o.a11 = fma(-th2x2, N.a11, fma(-gx1, x[1], fma(-u0, w[0], bk)));
+    o.a22 = fma(-th2x2, N.a22, fma(-gx2, x[2], fma(-u1, w[1], bk)));
+    o.a33 = fma(-th2x2, N.a33, fma(-gx3, x[3], fma(-u2, w[2], bk)));
+    o.a12 = fma(th2x2, N.a12, fma(-gx1, x[2], -fma_half(u0, w[1], u1 * w[0])));
+    o.a13 = fma(th2x2, N.a13, fma(-gx1, x[3], -fma_half(u0, w[2], u2 * w[0])));
+    o.a23 = fma(-th2x2, N.a23, fma(-gx2, x[3], -fma_half(u1, w[2], u2 * w[1])));
+    return o;
+}
+
 // Inverse of an SPD 4x4 by 2x2 blocks, S = [[A, B], [B^T, D]]: A^-1 by its adjugate, the Schur
 // complement C = D - B^T A^-1 B (SPD) likewise, then
 //   S^-1 = [[A^-1 + X C^-1 X^T, -X C^-1], [-C^-1 X^T, C^-1]],  X = A^-1 B.
@@ -670,6 +766,24 @@ PEKF_DEV void rk4_closed(const double *x, double n2, double dt_ns, const double 
     const double a = ca * in, c = cb * in;
     const double w0 = c * hw[0], w1 = c * hw[1], w2 = c * hw[2];
     // z = a x + Omega(c h_w) x, rows of Omega: [0,-w0,-w1,-w2] [w0,0,w2,-w1] [w1,-w2,0,w0] [w2,w1,-w0,0]
+    z[0] = a * x[0] - w0 * x[1] - w1 * x[2] - w2 * x[3];
+    z[1] = a * x[1] + w0 * x[0] + w2 * x[2] - w1 * x[3];
+    z[2] = a * x[2] + w1 * x[0] - w2 * x[1] + w0 * x[3];
+    z[3] = a * x[3] + w2 * x[0] + w1 * x[1] - w0 * x[2];
+}
+
+// rk4_closed from the raw gyro sample w and th2x2 = 2|h_w|^2 = |w|^2/2 (omod build, OmodMode): the
+// same values bit for bit, every halving done by the instruction that forms the product.
+PEKF_DEV void rk4_closed_w(const double *x, double n2, double dt_ns, const double *w, double th2x2, double *z,
+                           double &kk, double &in) {
+    const double h = dt_ns * kNsToS;
+    const double xx = mul_half(h * h, th2x2);  // h^2 |h_w|^2
+    const double ca = 1.0 - 0.5 * xx + xx * xx * (1.0 / 24.0);
+    const double cb = h * (1.0 - xx * (1.0 / 6.0));
+    kk = fma(ca, ca, mul_half(cb, cb) * th2x2);
+    in = rsqrt<2>(kk * n2);
+    const double a = ca * in, c = cb * in;
+    const double w0 = mul_half(c, w[0]), w1 = mul_half(c, w[1]), w2 = mul_half(c, w[2]);
     z[0] = a * x[0] - w0 * x[1] - w1 * x[2] - w2 * x[3];
     z[1] = a * x[1] + w0 * x[0] + w2 * x[2] - w1 * x[3];
     z[2] = a * x[2] + w1 * x[0] - w2 * x[1] + w0 * x[3];

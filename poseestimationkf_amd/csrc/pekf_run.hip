@@ -131,7 +131,7 @@ __device__ __forceinline__ double fma_rsub(double a, double b, double c) {
 template <typename PT>
 struct StepK {
     PT g2, r2;   // MC: 2g/beta, 2r/beta | P: 2g, 2r (innovation_cov_n / innovation_cov2)
-    PT rp, rr;   // P: r, 2r^2 (P = rI - 2r^2 (2S)^-1); unused for MC
+    PT rp, rr;   // P: r, 2r^2 (P = rI - 2r^2 (2S)^-1) | MC: r2 / 2 (innovation_cov_n_w), unused
     double sy;   // Y's weight in the unnormalised X update: MC 1/sqrt(2), P 1/(2r)
 };
 template <typename PT, bool MC>
@@ -139,7 +139,7 @@ __device__ __forceinline__ StepK<PT> step_consts(double qs, double rs) {
     const double g = 0.25 * qs;  // Jb Q Jb^T = (q/4)(|X|^2 I - X X^T)
     if (MC) {
         const double ib = 1.0 / (kSqrt2 * rs);
-        return {(PT)(2.0 * g * ib), (PT)(2.0 * rs * ib), PT(0), PT(0), 1.0 / kSqrt2};
+        return {(PT)(2.0 * g * ib), (PT)(2.0 * rs * ib), (PT)(rs * ib), PT(0), 1.0 / kSqrt2};
     }
     return {(PT)(2.0 * g), (PT)(2.0 * rs), (PT)rs, (PT)(2.0 * (rs * rs)), 0.5 / rs};
 }
@@ -149,26 +149,41 @@ __device__ __forceinline__ StepK<PT> step_consts(double qs, double rs) {
 // (g (|X|^2 I - X X^T) = g I - (g / |x|^2) x x^T, |X|^2 = 1 as state_norm2 snaps it), and
 // 1/|x|^2 = in^2 kk comes from RK4's own rsqrt: 8 operations instead of the 13 of normalising X.
 // LAZY: x arrives that way (n2 ignored); the caller normalises once at the end of the launch.
-template <typename PT, bool MC = false, bool LAZY = false, typename Ref>
+// OM (the FP64 multi-record loop, inside OmodMode): the exact halvings fold into the instructions
+// that form the products (omod, pekf_math.hpp) -- the gyro is never scaled to h = w/2, and the
+// Newton steps of the rsqrt seeds need no separate multiply by 1/2: 9 VALU fewer per record, the
+// same values bit for bit.
+template <typename PT, bool MC = false, bool LAZY = false, bool OM = false, typename Ref>
 __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> &P, const Ref &Wf, const StepK<PT> &k,
                                                 const double *gy, double dt_ns, bool missing,
                                                 const double *acc, const double *mag) {
+    static_assert(!OM || (MC && std::is_same<PT, double>::value), "omod form: FP64 multi-record loop only");
+    constexpr int F = OM ? 2 : 1;  // rsqrt form
     // ---- Prediction (ExtendedKalmanFilter.py:58-68) ----
-    const double hw[3] = {0.5 * gy[0], 0.5 * gy[1], 0.5 * gy[2]};  // 0.5*Omega(w) = Omega(w/2)
-    const double th2 = hw[0] * hw[0] + hw[1] * hw[1] + hw[2] * hw[2];
-    const PT hp[3] = {(PT)hw[0], (PT)hw[1], (PT)hw[2]};
-    const PT wp[3] = {(PT)gy[0], (PT)gy[1], (PT)gy[2]};
-    const PT xp[4] = {(PT)x[0], (PT)x[1], (PT)x[2], (PT)x[3]};
+    const double n2x = LAZY ? x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3] : n2;
     double z[4], kk, irk;
-    rk4_closed(x, LAZY ? x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3] : n2, dt_ns, hw, th2, z, kk,
-               irk);                                                // (:62)
-    const PT g2x = LAZY ? (PT)((irk * irk) * kk) * k.g2 : k.g2;     // 2g / |x|^2
-    const PT n2p = LAZY ? PT(1) : (PT)n2;
-    // S2 = 2S, S = P- + rI with P- = A P A^T + Jb Q Jb^T, Jb from the prior X (:60-61, :63).
-    // Exactly twice S (see innovation_cov2), so every result below is bit-identical to the
-    // undoubled recursion: (2S)^-1 = S^-1/2, and the constants absorb the factor.
-    const Sym4T<PT> S2 = MC ? innovation_cov_n<PT>(P, hp, wp, (PT)th2, xp, n2p, k.g2, k.r2, g2x)
-                            : innovation_cov2<PT>(P, hp, wp, (PT)th2, xp, n2p, k.g2, k.r2, g2x);
+    Sym4T<PT> S2;
+    if constexpr (OM) {
+        // th2x2 = 2 |h|^2 = |w|^2 / 2 (0.5*Omega(w) = Omega(h), h = w/2)
+        const double th2x2 = fma_half(gy[2], gy[2], fma(gy[1], gy[1], gy[0] * gy[0]));
+        rk4_closed_w(x, n2x, dt_ns, gy, th2x2, z, kk, irk);                  // (:62)
+        const double g2x = LAZY ? ((irk * irk) * kk) * k.g2 : k.g2;           // 2g / |x|^2
+        S2 = innovation_cov_n_w(P, gy, th2x2, x, LAZY ? 1.0 : n2, k.g2, k.r2, k.rp, g2x);
+    } else {
+        const double hw[3] = {0.5 * gy[0], 0.5 * gy[1], 0.5 * gy[2]};  // 0.5*Omega(w) = Omega(w/2)
+        const double th2 = hw[0] * hw[0] + hw[1] * hw[1] + hw[2] * hw[2];
+        const PT hp[3] = {(PT)hw[0], (PT)hw[1], (PT)hw[2]};
+        const PT wp[3] = {(PT)gy[0], (PT)gy[1], (PT)gy[2]};
+        const PT xp[4] = {(PT)x[0], (PT)x[1], (PT)x[2], (PT)x[3]};
+        rk4_closed(x, n2x, dt_ns, hw, th2, z, kk, irk);                    // (:62)
+        const PT g2x = LAZY ? (PT)((irk * irk) * kk) * k.g2 : k.g2;         // 2g / |x|^2
+        const PT n2p = LAZY ? PT(1) : (PT)n2;
+        // S2 = 2S, S = P- + rI with P- = A P A^T + Jb Q Jb^T, Jb from the prior X (:60-61, :63).
+        // Exactly twice S (see innovation_cov2), so every result below is bit-identical to the
+        // undoubled recursion: (2S)^-1 = S^-1/2, and the constants absorb the factor.
+        S2 = MC ? innovation_cov_n<PT>(P, hp, wp, (PT)th2, xp, n2p, k.g2, k.r2, g2x)
+                : innovation_cov2<PT>(P, hp, wp, (PT)th2, xp, n2p, k.g2, k.r2, g2x);
+    }
 
     if (missing) {
         // Wahba-skip: no Correction for this record (X = z, P = P- = S - rI)
@@ -188,9 +203,9 @@ __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> 
         const double ka = fabs(acc[2]);              // (:71)
         Frame Vf;
         // ka = |acc_z| >= 0, so wahba_sign(ka, km) is the sign of km = 1 - ka (never -0)
-        make_frame<true>(acc, mag, Vf, 1.0 - ka);
+        make_frame<F>(acc, mag, Vf, 1.0 - ka);
         double v[4], sc;
-        wahba_quat_toward(Wf, Vf, ka, 1.0 - ka, z, v, sc);  // Wahba.py:8-47 + the flip of :73-75: Y = v sc
+        wahba_quat_toward<F>(Wf, Vf, ka, 1.0 - ka, z, v, sc);  // Wahba.py:8-47 + the flip of :73-75: Y = v sc
         // e = Y - z (MC: D e, whose last two components are z - Y)
         const PT e0 = (PT)fma_sub(v[0], sc, z[0]), e1 = (PT)fma_sub(v[1], sc, z[1]);
         const PT e2 = (PT)(MC ? fma_rsub(v[2], sc, z[2]) : fma_sub(v[2], sc, z[2]));
@@ -323,9 +338,9 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
             const uint32_t word = __float_as_uint(cur.gd.w);
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
-            ekf_record_step<PT, MC, decltype(lazy)::value>(x, n2, P, ref, step_consts<PT, MC>(qs, rs), gy,
-                                                           (double)(word & 0x7FFFFFFFu),
-                                                           (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
+            ekf_record_step<PT, MC, decltype(lazy)::value, MC && !MIXED>(
+                x, n2, P, ref, step_consts<PT, MC>(qs, rs), gy, (double)(word & 0x7FFFFFFFu),
+                (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
         }
         if (TRAJ) {
             double xo[4] = {x[0], x[1], x[2], x[3]};
@@ -393,6 +408,9 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     const int32_t n32 = (int32_t)n_steps;
     o8 = next(o8);
     rb = load_row(o8);
+    // the FP64 loop folds its exact halvings into output modifiers, which need this MODE
+    OmodMode mode;
+    if constexpr (!MIXED) mode.enter();
     step(ra, 0, state_norm2(x), Wr, eager{});
     for (int32_t t = 1; t < n32;) {
         o8 = next(o8);
@@ -404,6 +422,7 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
         step(ra, t, 1.0, Wr, lazy{});
         ++t;
     }
+    if constexpr (!MIXED) mode.leave();
     if (COUNTS && my_steps == 0) return;
     {
         const PT be = (PT)(kSqrt2 * rs), rp = (PT)rs;
