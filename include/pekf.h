@@ -226,6 +226,10 @@ int pekf_filter_get_state(pekf_filter *f, double *X, double *P);
 /* previousT of every filter (host [batch]); the stream path (pekf_filter_run) uses dt records and
  * leaves it untouched, so set it before switching back to pekf_filter_update. */
 int pekf_filter_set_time(pekf_filter *f, const int64_t *t_ns);
+/* previousT of every filter (host [batch]; KalmanFilter.previousT, ExtendedKalmanFilter.py:8,67), as the
+ * last pekf_filter_update left it (work enqueued by pekf_filter_update_dev on another stream must be
+ * synchronised by the caller first, as for pekf_filter_get_state). */
+int pekf_filter_get_time(pekf_filter *f, int64_t *t_ns);
 /* Device addresses of the state (layout per flags) and refs[batch*6], e.g. for a collective. */
 int pekf_filter_device_state(pekf_filter *f, double **X, double **P, double **refs);
 /* One record per filter, FP64: Prediction(gyro, t_ns) then Correction(mag, acc) (main_file.py:42-45),

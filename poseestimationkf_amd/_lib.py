@@ -85,6 +85,7 @@ SIGNATURES = {
     "pekf_filter_set_state": [_vp, _vp, _vp],
     "pekf_filter_get_state": [_vp, _vp, _vp],
     "pekf_filter_set_time": [_vp, _vp],
+    "pekf_filter_get_time": [_vp, _vp],
     "pekf_filter_device_state": [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp)],
     "pekf_filter_update": [_vp] * 7,
     "pekf_filter_update_dev": [_vp] * 8,

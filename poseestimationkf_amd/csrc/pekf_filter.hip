@@ -216,6 +216,14 @@ int pekf_filter_set_time(pekf_filter *f, const int64_t *t_ns) {
     return PEKF_OK;
 }
 
+int pekf_filter_get_time(pekf_filter *f, int64_t *t_ns) {
+    if (int st = check_handle(f)) return st;
+    PEKF_CHECK_ARG(t_ns != nullptr, "null pointer");
+    PEKF_HIP(hipMemcpyAsync(t_ns, f->prev_t, 8 * (size_t)f->batch, hipMemcpyDeviceToHost, f->stream));
+    PEKF_HIP(hipStreamSynchronize(f->stream));
+    return PEKF_OK;
+}
+
 int pekf_filter_device_state(pekf_filter *f, double **X, double **P, double **refs) {
     if (int st = check_handle(f)) return st;
     if (X) *X = f->X;

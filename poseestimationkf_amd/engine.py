@@ -427,6 +427,12 @@ class FilterHandle:
         t = np.ascontiguousarray(t_ns, np.int64).reshape(self.batch)
         check(lib.pekf_filter_set_time(self.h, t.ctypes.data))
 
+    def get_time(self):
+        """previousT of every filter (B,) int64 ns (KalmanFilter.previousT)."""
+        t = np.empty(self.batch, np.int64)
+        check(lib.pekf_filter_get_time(self.h, t.ctypes.data))
+        return t
+
     def close(self):
         if getattr(self, "h", None):
             lib.pekf_filter_destroy(self.h)

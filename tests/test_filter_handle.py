@@ -68,6 +68,10 @@ def test_update_fp64_records_against_numpy_restatement(eng):
     for i in range(N):
         t += dt[i]
         X = h.update(gyro[i], t, acc[i], mag[i])
+    assert np.array_equal(h.get_time(), t)  # previousT advanced to each filter's last T (:67)
+    h.set_time(t - 5)
+    assert np.array_equal(h.get_time(), t - 5)
+    h.set_time(t)
     for k in range(K):
         Xo, Po, _ = npo.run_filter(gyro[:, k], dt[:, k].astype(np.float64), acc[:, k], mag[:, k], rec.acc0[k],
                                    rec.mag0[k], record=False)
