@@ -15,6 +15,9 @@
 namespace pekf {
 
 constexpr int kFeBlock = 256;
+#ifndef PEKF_FE_RING
+#define PEKF_FE_RING 9
+#endif
 enum : uint32_t { kEvAcc = 0, kEvGyro = 1, kEvMag = 2 };
 
 struct V3 {
@@ -157,19 +160,22 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
         mag1_set = m1s && !emit;
     };
     if (n_events > 0) {
-        float4 ring[kFlush];
+        constexpr int kRing = PEKF_FE_RING;  // events in flight per lane (a multiple of kFlush)
+        static_assert(kRing % kFlush == 0, "the ring depth must be a multiple of the flush period");
+        float4 ring[kRing];
 #pragma unroll
-        for (int k = 0; k < kFlush; ++k) ring[k] = load(k);
-        for (int64_t e0 = 0; e0 < n_events; e0 += kFlush) {
+        for (int k = 0; k < kRing; ++k) ring[k] = load(k);
+        for (int64_t e0 = 0; e0 < n_events; e0 += kRing) {
 #pragma unroll
-            for (int k = 0; k < kFlush; ++k) {
+            for (int k = 0; k < kRing; ++k) {
                 if (e0 + k >= n_events) break;  // uniform
                 const float4 v4 = ring[k];
-                ring[k] = load(e0 + k + kFlush);
+                ring[k] = load(e0 + k + kRing);
                 event(v4);
+                if ((k + 1) % kFlush == 0) flush();
             }
-            flush();
         }
+        flush();  // a record completed in a trailing partial group
     }
     counts[b] = (int32_t)(r < r_max ? r : r_max);
     if (bad && err) atomicOr(err, bad);
