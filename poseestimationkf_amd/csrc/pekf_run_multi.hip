@@ -1,0 +1,38 @@
+// pekf_run_multi.hip -- the multi-record instantiations of the fused stream kernel (pekf_step.hpp):
+// the headline launch of main_file.py:38-47 over a whole resident window (config 3: 10,000 records
+// per launch).  A file of its own because it is compiled with the max-ILP machine scheduler
+// (Makefile RUNMULTIFLAGS): the time loop's record is ~300 dependent FP64 VALU instructions with
+// seven transcendental seeds, and at its 3-4 waves per SIMD (1 at config 2) the interleaving the
+// scheduler finds is worth more than the occupancy-first default (same box: config 3 -0.9 %,
+// config 2 -4.5 %, profiles/r2/ab_sched_maxilp/).  The one-record and per-record kernels, which move
+// state through HBM and want occupancy, stay in pekf_run.hip with the default scheduler.
+// Scheduling moves instructions, never their arithmetic: the two files' variants round identically.
+#include "pekf_step.hpp"
+
+namespace pekf {
+
+int launch_run_multi(int64_t batch, int64_t n_steps, int64_t window, int64_t step0, const float4 *gd,
+                     const float4 *am, const float2 *my, const double *refs, double *X, double *P, double q,
+                     double r, double *traj, const int32_t *counts, bool mixed, bool soa, hipStream_t stream) {
+    const dim3 grid(grid_for(batch, kRunBlock)), block(kRunBlock);
+#define PEKF_LAUNCH_RUN(TR, MX, SO, CN)                                                                      \
+    hipLaunchKernelGGL((k_run<TR, MX, SO, CN, false>), grid, block, 0, stream, batch, n_steps, window, step0, gd, \
+                       am, my, refs, X, P, q, r, traj, counts)
+#define PEKF_LAUNCH_RUN1(TR, MX, SO) \
+    do { if (counts) PEKF_LAUNCH_RUN(TR, MX, SO, true); else PEKF_LAUNCH_RUN(TR, MX, SO, false); } while (0)
+#define PEKF_LAUNCH_RUN2(TR, MX) \
+    do { if (soa) PEKF_LAUNCH_RUN1(TR, MX, true); else PEKF_LAUNCH_RUN1(TR, MX, false); } while (0)
+    if (traj) {
+        if (mixed) PEKF_LAUNCH_RUN2(true, true); else PEKF_LAUNCH_RUN2(true, false);
+    } else {
+        if (mixed) PEKF_LAUNCH_RUN2(false, true); else PEKF_LAUNCH_RUN2(false, false);
+    }
+#undef PEKF_LAUNCH_RUN2
+#undef PEKF_LAUNCH_RUN1
+#undef PEKF_LAUNCH_RUN
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "k_run");
+    return PEKF_OK;
+}
+
+}  // namespace pekf
