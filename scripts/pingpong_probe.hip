@@ -41,6 +41,74 @@ __global__ void k_resident(unsigned *req, unsigned *resp, const double *in, doub
     }
 }
 
+// The same responder with K polls in flight: a new load of the request word is issued every
+// `gap` s_sleep units while the K - 1 older ones are still travelling, so a posted request is seen
+// by the next poll to return rather than by one issued after it lands.
+template <int K>
+__global__ void k_resident_pipelined(unsigned *req, unsigned *resp, const double *in, double *out, unsigned n,
+                                     unsigned long long idle_ticks) {
+    if (threadIdx.x != 0) return;
+    unsigned last = 0;
+    unsigned long long t0 = wall_clock64();
+    unsigned r[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        r[k] = __hip_atomic_load(req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_s_sleep(4);
+    }
+    while (last < n) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const unsigned v = r[k];  // the oldest poll in flight
+            r[k] = __hip_atomic_load(req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (v != last && last < n) {
+                __atomic_thread_fence(__ATOMIC_ACQUIRE);
+                double w[4];
+                for (int j = 0; j < 4; ++j) w[j] = __hip_atomic_load(in + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                for (int j = 0; j < 4; ++j) __hip_atomic_store(out + j, w[j] * 2.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(resp, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                last = v;
+                t0 = wall_clock64();
+            }
+            __builtin_amdgcn_s_sleep(4);
+        }
+        if (wall_clock64() - t0 > idle_ticks) break;
+    }
+}
+
+template <int K>
+int run_pipelined(unsigned *dreq, unsigned *dresp, volatile unsigned *hreq, volatile unsigned *hresp, double *din,
+                  double *dout, hipStream_t s, unsigned long long idle) {
+    const unsigned N = 3000;
+    *hreq = 0;
+    *hresp = 0;
+    hipLaunchKernelGGL(k_resident_pipelined<K>, dim3(1), dim3(64), 0, s, dreq, dresp, din, dout, N, idle);
+    CK(hipGetLastError());
+    std::vector<double> us;
+    bool lost = false;
+    for (unsigned i = 1; i <= N && !lost; ++i) {
+        auto t0 = std::chrono::steady_clock::now();
+        __atomic_store_n(hreq, i, __ATOMIC_RELEASE);
+        while (__atomic_load_n(hresp, __ATOMIC_ACQUIRE) != i) {
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 0.1) {
+                lost = true;
+                break;
+            }
+        }
+        us.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    }
+    CK(hipStreamSynchronize(s));
+    if (lost) {
+        std::printf("pipelined K=%d: no response within 100 ms\n", K);
+        return 0;
+    }
+    std::vector<double> tail(us.begin() + 500, us.end());
+    std::sort(tail.begin(), tail.end());
+    std::printf("resident round trip, %d polls in flight: median %.2f us  p10 %.2f  p90 %.2f  p99 %.2f\n", K,
+                tail[tail.size() / 2], tail[tail.size() / 10], tail[tail.size() * 9 / 10], tail[tail.size() * 99 / 100]);
+    return 0;
+}
+
 int main() {
     int rate_khz = 0;
     CK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0));
@@ -85,6 +153,9 @@ int main() {
                     tail[tail.size() / 2], tail[tail.size() / 10], tail[tail.size() * 9 / 10],
                     tail[tail.size() * 99 / 100]);
     }
+    run_pipelined<2>(dreq, dresp, hreq, hresp, din, dout, s, idle);
+    run_pipelined<4>(dreq, dresp, hreq, hresp, din, dout, s, idle);
+    run_pipelined<8>(dreq, dresp, hreq, hresp, din, dout, s, idle);
     // Variant: the request word in fine-grained device memory written by the CPU through the
     // BAR mapping (if the platform maps it), the response in pinned host memory.
     unsigned *vreq = nullptr;
