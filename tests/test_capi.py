@@ -62,6 +62,11 @@ def test_no_cpu_fallback_without_device():
     p = ctypes.c_void_p()
     assert _lib.lib.pekf_malloc(ctypes.byref(p), 64) == _lib.PEKF_ERR_NODEVICE
     assert "no HIP device" in _lib.last_error()
+    from poseestimationkf_amd import shard  # the collective refuses too (RCCL is never loaded)
+    with pytest.raises(_lib.NoDeviceError):
+        shard.Communicator.unique_id()
+    with pytest.raises(_lib.NoDeviceError):
+        shard.Communicator(bytes(128), 1, 0)
 
 
 def test_fastcall_binding_checks_shapes():
@@ -76,6 +81,11 @@ def test_fastcall_binding_checks_shapes():
 
 def test_invalid_arguments_are_reported_not_crashed():
     from poseestimationkf_amd import _lib
+    h = ctypes.c_void_p()
+    assert _lib.lib.pekf_comm_init(bytes(128), 2, 2, ctypes.byref(h)) == _lib.PEKF_ERR_INVALID  # rank >= nranks
+    assert "rank" in _lib.last_error()
+    assert _lib.lib.pekf_gather_dev(None, None, 4, None, 0, None) == _lib.PEKF_ERR_INVALID
+    assert _lib.lib.pekf_comm_destroy(None) == _lib.PEKF_OK
     st = _lib.lib.pekf_run_dev(-1, 1, 1, 0, None, None, None, None, None, None, 1.0, 0.1, None, None, 0, None)
     assert st == _lib.PEKF_ERR_INVALID and "negative" in _lib.last_error()
     st = _lib.lib.pekf_run_dev(4, 1, 1, 0, None, None, None, None, None, None, 1.0, 0.1, None, None, 0, None)
