@@ -247,14 +247,19 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
                                                    double qs, double rs, double *__restrict__ traj,
                                                    const int32_t *__restrict__ counts) {
     using PT = typename std::conditional<MIXED, float, double>::type;
-    if constexpr (ONE && !SOA) {
-        // one-record launch on AoS state: the state is most of the traffic, so it moves in
-        // coalesced wave tiles (pekf_tile.hpp) instead of 128 B-strided per-lane accesses
-        __shared__ double pool[kRunBlock / kWave * tile_doubles<16>()];
-        const WaveTile t(pool, tile_doubles<16>(), batch);
+    if constexpr (ONE) {
+        // one-record launch (online serving): the state and the reference pair are most of the
+        // traffic.  The AoS state and the [batch][6] reference pairs move in coalesced wave tiles
+        // (pekf_tile.hpp) instead of 128 / 48 B-strided per-lane accesses; the SoA state is read and
+        // written per lane, one contiguous 512 B access per component and wave.
+        constexpr int kTile = SOA ? 6 : 16;
+        __shared__ double pool[kRunBlock / kWave * tile_doubles<kTile>()];
+        const WaveTile t(pool, tile_doubles<kTile>(), batch);
         double cx[4], cp[16], cr[6];
-        t.gather(Xio, cx);
-        t.gather(Pio, cp);
+        if constexpr (!SOA) {
+            t.gather(Xio, cx);
+            t.gather(Pio, cp);
+        }
         t.gather(refs, cr);
         const bool act = t.active();
         const uint32_t lane = act ? (uint32_t)(t.first + t.lane) : 0u;  // idle lanes read a valid row
@@ -262,12 +267,17 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
         const Rec cur = {(gd + base)[lane], (am + base)[lane], (my + base)[lane]};
         const bool run = act && (!COUNTS || counts[lane] > 0);
         double x[4], pv[16], rf[6];
-        t.to_lanes(cx, x);
-        t.to_lanes(cp, pv);
+        Sym4T<PT> P;
+        if constexpr (SOA) {
+            load_state<true>(Xio, Pio, lane, batch, x, P);
+        } else {
+            t.to_lanes(cx, x);
+            t.to_lanes(cp, pv);
+            P = sym_from16<PT>(pv);
+        }
         t.to_lanes(cr, rf);
         Frame Wf;
         make_frame<true>(rf, rf + 3, Wf);
-        Sym4T<PT> P = sym_from16<PT>(pv);
         if (run) {
             const double gy[3] = {cur.gd.x, cur.gd.y, cur.gd.z};
             const uint32_t word = __float_as_uint(cur.gd.w);
@@ -281,9 +291,13 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
             o[0] = make_double2(x[0], x[1]);
             o[1] = make_double2(x[2], x[3]);
         }
-        sym_to16(P, pv);
-        t.store(Xio, x);
-        t.store(Pio, pv);
+        if constexpr (SOA) {
+            if (act) store_state<true>(Xio, Pio, lane, batch, x, P);
+        } else {
+            sym_to16(P, pv);
+            t.store(Xio, x);
+            t.store(Pio, pv);
+        }
         return;
     }
     const int64_t b = (int64_t)blockIdx.x * kRunBlock + threadIdx.x;
@@ -366,11 +380,6 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     // instantiation, which has no prefetch: there its 40 B would be an eighth of the traffic.
     uint64_t o8 = (uint64_t)(step0 % window) * row8;
     Rec ra = load_row(o8), rb;
-    if constexpr (ONE) {
-        step(ra, 0, state_norm2(x), Wf, eager{});
-        store_state<SOA>(Xio, Pio, b, batch, x, P);
-        return;
-    }
     // A multi-record launch runs the filter in its reference frame's own basis (RefW in
     // pekf_math.hpp: the same filter, with Wahba's rotation 24 operations cheaper per record);
     // the state is rotated in once and out once per launch.  A filter with no records in this
