@@ -75,6 +75,57 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void *row, int6
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(row), 0, (int)(uint32_t)bytes, 0x00020000);
 }
 
+// The rows of the three record planes a multi-record launch walks through (row r of a plane is
+// batch x 16 B for gd / am, batch x 8 B for my; the window wraps).  Rows are read through buffer
+// descriptors of a CHUNK of consecutive rows with the row's offset inside the chunk in the
+// instruction's scalar offset (soffset), so moving to the next row is two scalar adds and a compare,
+// and the descriptors are rebuilt only when a chunk ends: chunk offsets stay below 2^31 (128 rows at
+// config 3, the whole 1,024-row window at config 2).  Each descriptor's record count is its chunk's
+// byte size and the range check covers soffset (measured: scripts/buffer_range_probe.hip), so an
+// offset past the chunk would read zeros, never another allocation.
+struct RowCursor {
+    const char *g, *a, *m;
+    uint32_t row16, row8;
+    int32_t window, chunk_rows;
+    int32_t row = 0, end = 0;
+    uint32_t s16 = 0, s8 = 0;
+    __amdgpu_buffer_rsrc_t rg, ra, rm;
+
+    __device__ __forceinline__ RowCursor(const float4 *gd, const float4 *am, const float2 *my, int64_t batch,
+                                         int64_t win)
+        : g(reinterpret_cast<const char *>(gd)), a(reinterpret_cast<const char *>(am)),
+          m(reinterpret_cast<const char *>(my)), row16((uint32_t)batch * 16u), row8((uint32_t)batch * 8u),
+          window((int32_t)win) {
+        const uint32_t c = (1u << 31) / row16;
+        chunk_rows = c ? (int32_t)c : 1;
+    }
+    __device__ __forceinline__ void start(int32_t r) {
+        row = r;
+        end = (window - r < chunk_rows) ? window : r + chunk_rows;
+        const uint64_t n = (uint64_t)(end - r);
+        rg = row_rsrc(g + (uint64_t)r * row16, (int64_t)(n * row16));
+        ra = row_rsrc(a + (uint64_t)r * row16, (int64_t)(n * row16));
+        rm = row_rsrc(m + (uint64_t)r * row8, (int64_t)(n * row8));
+        s16 = 0;
+        s8 = 0;
+    }
+    __device__ __forceinline__ void advance() {
+        if (++row == end) {
+            start(row == window ? 0 : row);
+        } else {
+            s16 += row16;
+            s8 += row8;
+        }
+    }
+    __device__ __forceinline__ Rec load(uint32_t off16, uint32_t off8) const {
+        Rec v;
+        v.gd = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, off16, s16, PEKF_REC_AUX));
+        v.am = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, off16, s16, PEKF_REC_AUX));
+        v.my = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rm, off8, s8, PEKF_REC_AUX));
+        return v;
+    }
+};
+
 // AoS P (full 4x4) <-> its upper triangle, for state moved through a WaveTile
 template <typename PT>
 __device__ __forceinline__ Sym4T<PT> sym_from16(const double (&p)[16]) {
@@ -315,29 +366,13 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     Sym4T<PT> P;
     load_state<SOA>(Xio, Pio, b, batch, x, P);
 
-    // Record of stream row r: raw buffer loads whose resource (the row's base address, scalar
-    // registers) is rebuilt per row and whose 32-bit lane offset is fixed, so no per-step vector
-    // address arithmetic (batch < 2^28 is checked on the host, so the offsets fit).  The row is
-    // tracked as one wave-uniform byte offset (row * batch * 8, advanced by an add and wrapped by a
-    // compare per step; the 16 B planes sit at twice it) instead of a 64-bit row * batch multiply.
+    // Record of stream row r: raw buffer loads whose lane offset is fixed and whose row offset is
+    // the wave-uniform soffset within a chunk of rows (RowCursor), so a record costs two scalar adds
+    // and a compare of address work, no per-step vector address arithmetic (batch < 2^28 is checked
+    // on the host, so the offsets fit).
     const uint32_t lane = (uint32_t)b;
     const uint32_t off16 = lane * 16u, off8 = lane * 8u;
-    const uint64_t row8 = (uint64_t)batch * 8u, wrap8 = (uint64_t)window * row8;
-    auto load_row = [&](uint64_t o8) -> Rec {
-        Rec v;
-        const char *g = reinterpret_cast<const char *>(gd) + 2 * o8;
-        const char *a = reinterpret_cast<const char *>(am) + 2 * o8;
-        const char *m = reinterpret_cast<const char *>(my) + o8;
-        const auto g4 = __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(g, batch * 16), off16, 0, PEKF_REC_AUX);
-        const auto a4 = __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(a, batch * 16), off16, 0, PEKF_REC_AUX);
-        const auto m2 = __builtin_amdgcn_raw_buffer_load_b64(row_rsrc(m, batch * 8), off8, 0, PEKF_REC_AUX);
-        v.gd = __builtin_bit_cast(float4, g4);
-        v.am = __builtin_bit_cast(float4, a4);
-        v.my = __builtin_bit_cast(float2, m2);
-        return v;
-    };
-    auto next = [&](uint64_t o8) -> uint64_t { o8 += row8; return o8 == wrap8 ? 0 : o8; };
-
+    RowCursor rows(gd, am, my, batch, window);
     // One record: Prediction + Correction (main_file.py:42-45) on (x, P) in registers.
     auto step = [&](const Rec &cur, int32_t t, double n2, const auto &ref, auto lazy) {
         // the multi-record loop (RefW) carries N and an unnormalised X, the one-record launch
@@ -378,8 +413,8 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     // The prefetch is unconditional (the row wraps inside the resident window, so it is always
     // a valid address); n_steps >= 1 here.  One-record launches (online serving) use the ONE
     // instantiation, which has no prefetch: there its 40 B would be an eighth of the traffic.
-    uint64_t o8 = (uint64_t)(step0 % window) * row8;
-    Rec ra = load_row(o8), rb;
+    rows.start((int32_t)(step0 % window));
+    Rec ra = rows.load(off16, off8), rb;
     // A multi-record launch runs the filter in its reference frame's own basis (RefW in
     // pekf_math.hpp: the same filter, with Wahba's rotation 24 operations cheaper per record);
     // the state is rotated in once and out once per launch.  A filter with no records in this
@@ -411,19 +446,19 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     // unit and n2 = 1 is a compile-time constant (see state_norm2).  32-bit step counter
     // (n_steps < 2^31 is checked on the host).
     const int32_t n32 = (int32_t)n_steps;
-    o8 = next(o8);
-    rb = load_row(o8);
+    rows.advance();
+    rb = rows.load(off16, off8);
     // the FP64 loop folds its exact halvings into output modifiers, which need this MODE
     OmodMode mode;
     if constexpr (!MIXED) mode.enter();
     step(ra, 0, state_norm2(x), Wr, eager{});
     for (int32_t t = 1; t < n32;) {
-        o8 = next(o8);
-        ra = load_row(o8);
+        rows.advance();
+        ra = rows.load(off16, off8);
         step(rb, t, 1.0, Wr, lazy{});
         if (++t == n32) break;
-        o8 = next(o8);
-        rb = load_row(o8);
+        rows.advance();
+        rb = rows.load(off16, off8);
         step(ra, t, 1.0, Wr, lazy{});
         ++t;
     }
