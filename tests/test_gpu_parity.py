@@ -263,6 +263,26 @@ def test_full_size_configs_sampled_against_oracle(eng, oracle_c, name, batch, mi
     assert err < ATOL_Q and err < PREC_GUARD
 
 
+def test_row_chunks_wrap_and_offset_start(eng, oracle_c):
+    """Records are read through descriptors of a chunk of rows with the row offset in soffset
+    (RowCursor, csrc/pekf_step.hpp).  At 16M filters a row of the 16 B planes is 256 MiB, so a chunk
+    is 8 rows: a 13-row window started at row 5 and run for 30 records crosses chunk ends inside the
+    window, the window's short last chunk and wraps twice; a second launch resumes at row 9."""
+    B, W = 1 << 24, 13
+    win = eng.IMUWindow(B, W).synthesize(seed=5)
+    f = eng.BatchedEKF(B)
+    f.run(win, n_steps=30, step0=5)
+    f.run(win, n_steps=11, step0=9)
+    X = f.X.download((B, 4), np.float64)
+    cols = np.array([0, 1, 63, 64, 12345, B // 2, B - 65, B - 1])
+    rec = synth.generate(cols, W, seed=5)
+    Xo, Po, _ = oracle_c.run(rec, n_steps=30, step0=5)
+    Xo, _, _ = oracle_c.run(rec, n_steps=11, step0=9, X=Xo, P=Po)
+    err = _maxerr(X[cols], Xo)
+    print("row chunks (16M filters, 8-row chunks, 13-row window): max |dq| = %.3e" % err)
+    assert err < ATOL_Q and err < PREC_GUARD
+
+
 def test_batch_of_one(eng, traj):
     sl = slice(0, 1)
     win = eng.IMUWindow.from_planes(traj["gd"][:, sl], traj["am"][:, sl], traj["my"][:, sl],
