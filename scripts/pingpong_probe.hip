@@ -109,6 +109,72 @@ int run_pipelined(unsigned *dreq, unsigned *dresp, volatile unsigned *hreq, vola
     return 0;
 }
 
+// NW polling waves, staggered: wave k starts k * gap sleep units late, so a posted request is first
+// seen by whichever wave's poll lands next; the wave that sees it claims it with an atomic CAS on a
+// device-memory word (the others skip it) and answers.
+__global__ void k_resident_multi(unsigned *req, unsigned *resp, unsigned *claim, const double *in, double *out,
+                                 unsigned n, unsigned long long idle_ticks, int gap) {
+    if (threadIdx.x % 64 != 0) return;
+    const int wave = threadIdx.x / 64;
+    for (int k = 0; k < wave * gap; ++k) __builtin_amdgcn_s_sleep(1);
+    unsigned long long t0 = wall_clock64();
+    for (;;) {
+        const unsigned r = __hip_atomic_load(req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned c = __hip_atomic_load(claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c >= n) break;
+        if (r != c) {
+            unsigned expect = c;
+            if (__hip_atomic_compare_exchange_strong(claim, &expect, r, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)) {
+                double w[4];
+                for (int j = 0; j < 4; ++j) w[j] = __hip_atomic_load(in + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                for (int j = 0; j < 4; ++j) __hip_atomic_store(out + j, w[j] * 2.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(resp, r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            t0 = wall_clock64();
+        } else if (wall_clock64() - t0 > idle_ticks) {
+            break;
+        }
+    }
+}
+
+int run_multi(int nw, int gap, unsigned *dreq, unsigned *dresp, volatile unsigned *hreq, volatile unsigned *hresp,
+              double *din, double *dout, hipStream_t s, unsigned long long idle) {
+    const unsigned N = 3000;
+    unsigned *claim;
+    CK(hipMalloc(&claim, 4));
+    CK(hipMemset(claim, 0, 4));
+    *hreq = 0;
+    *hresp = 0;
+    hipLaunchKernelGGL(k_resident_multi, dim3(1), dim3(64 * nw), 0, s, dreq, dresp, claim, din, dout, N, idle, gap);
+    CK(hipGetLastError());
+    std::vector<double> us;
+    bool lost = false;
+    for (unsigned i = 1; i <= N && !lost; ++i) {
+        auto t0 = std::chrono::steady_clock::now();
+        __atomic_store_n(hreq, i, __ATOMIC_RELEASE);
+        while (__atomic_load_n(hresp, __ATOMIC_ACQUIRE) != i) {
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 0.1) {
+                lost = true;
+                break;
+            }
+        }
+        us.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    }
+    CK(hipStreamSynchronize(s));
+    CK(hipFree(claim));
+    if (lost) {
+        std::printf("%d waves gap %d: no response within 100 ms\n", nw, gap);
+        return 0;
+    }
+    std::vector<double> tail(us.begin() + 500, us.end());
+    std::sort(tail.begin(), tail.end());
+    std::printf("resident round trip, %d staggered polling waves (gap %d): median %.2f us  p10 %.2f  p90 %.2f  p99 %.2f\n",
+                nw, gap, tail[tail.size() / 2], tail[tail.size() / 10], tail[tail.size() * 9 / 10],
+                tail[tail.size() * 99 / 100]);
+    return 0;
+}
+
 int main() {
     int rate_khz = 0;
     CK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0));
@@ -153,6 +219,11 @@ int main() {
                     tail[tail.size() / 2], tail[tail.size() / 10], tail[tail.size() * 9 / 10],
                     tail[tail.size() * 99 / 100]);
     }
+    run_multi(1, 0, dreq, dresp, hreq, hresp, din, dout, s, idle);
+    run_multi(2, 8, dreq, dresp, hreq, hresp, din, dout, s, idle);
+    run_multi(4, 4, dreq, dresp, hreq, hresp, din, dout, s, idle);
+    run_multi(8, 2, dreq, dresp, hreq, hresp, din, dout, s, idle);
+    run_multi(16, 1, dreq, dresp, hreq, hresp, din, dout, s, idle);
     run_pipelined<2>(dreq, dresp, hreq, hresp, din, dout, s, idle);
     run_pipelined<4>(dreq, dresp, hreq, hresp, din, dout, s, idle);
     run_pipelined<8>(dreq, dresp, hreq, hresp, din, dout, s, idle);
