@@ -263,6 +263,21 @@ def test_full_size_configs_sampled_against_oracle(eng, oracle_c, name, batch, mi
     assert err < ATOL_Q and err < PREC_GUARD
 
 
+@pytest.mark.parametrize("W,step0,n", [(1, 0, 7), (2, 1, 7), (3, 2, 8)])
+def test_tiny_windows_replayed(eng, oracle_c, W, step0, n):
+    """Windows of 1-3 rows replayed for more records than they hold (every record advances the row
+    cursor past the window's end), odd and even launch lengths, against the C oracle."""
+    K = 96
+    rec = synth.generate(np.arange(K), W, seed=17 + W)
+    win = eng.IMUWindow.from_records(rec)
+    f = eng.BatchedEKF(K)
+    f.run(win, n_steps=n, step0=step0)
+    Xg, Pg = f.get_state()
+    Xo, Po, _ = oracle_c.run(rec, n_steps=n, step0=step0)
+    assert _maxerr(Xg, Xo) < PREC_GUARD
+    assert _maxerr(Pg, Po) < PREC_GUARD
+
+
 def test_row_chunks_wrap_and_offset_start(eng, oracle_c):
     """Records are read through descriptors of a chunk of rows with the row offset in soffset
     (RowCursor, csrc/pekf_step.hpp).  At 16M filters a row of the 16 B planes is 256 MiB, so a chunk
