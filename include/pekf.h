@@ -207,6 +207,17 @@ int pekf_frontend_dev(int64_t batch, int64_t n_events, const void *ev_planes, co
                       void *plane_gd, void *plane_am, void *plane_my, int32_t *counts, double *refs,
                       int *dev_error, void *stream);
 
+/* Phase 2 of the server's Parser (KFS/Parser.cpp:36-58,84-140; KFS/InitialValues.cpp) on the device: per
+ * filter, the mean and sample variance of the first n_avg (the server: 100) samples of each sensor type,
+ * and the time phase 3 continues from.  Events as for pekf_frontend_dev (ev_planes [n_events][batch], word
+ * = gap << 2 | type, the first gap from t_start[b]).  A filter is ready once every sensor has had a sample
+ * after its first n_avg and one more event has arrived (the KalmanFilter construction, :41-55); later
+ * events move t_init to their time (:57-62).  Outputs (device): init[batch*6] = raw means {acc xyz, mag
+ * xyz} and t_init[batch] -- pekf_frontend_dev's init / t_init --, ready[batch] (0: not enough phase-2
+ * events; init is then NaN), stats[batch*12] (optional) = {gyro mean, acc / mag / gyro variance}. */
+int pekf_frontend_init_dev(int64_t batch, int64_t n_events, const void *ev_planes, const int64_t *t_start,
+                           int n_avg, double *init, int64_t *t_init, double *stats, int32_t *ready, void *stream);
+
 /* X = [1,0,0,0], P = I for every filter (main_file.py:23,26). */
 int pekf_reset_state_dev(int64_t batch, double *X, double *P, void *stream);
 

@@ -112,3 +112,46 @@ def run_frontend(types, values, times, init_acc, init_mag, t_init, alpha=0.1):
             mag0, t_mag0 = mag1, t_mag1
     return (np.asarray(out_g, np.float64).reshape(-1, 3), np.asarray(out_dt, np.int64),
             np.asarray(out_a, np.float64).reshape(-1, 3), np.asarray(out_m, np.float64).reshape(-1, 3))
+
+
+def initial_values(types, values, times, n_avg=100):
+    """One filter's phase-2 events -> dict(ready, acc, mag, gyro (means), var_acc, var_mag, var_gyro, t_init).
+
+    Parser::ProcessString phase '2' (Parser.cpp:36-58): while any sensor is not initialised, the
+    event goes to initialMeanAndCovariance (:84-140) -- the first n_avg samples of its type are
+    averaged (InitialValues::setValuesforAverage: a sequential float64 sum; compute_mean_and_variance:
+    sum / n, then sum((x - mean)^2) / (n - 1), InitialValues.cpp:20-66) and the sensor counts as
+    initialised at its next sample; the first event after all three are initialised builds the
+    KalmanFilter at its time, and every later one moves acc_0 / mag_0's time and previousT to its
+    own (:41-62).  PARITY UNPINNED (C++ source that cannot be built here, no fixtures)."""
+    keys = (ACC, GYRO, MAG)
+    sums = {k: [0.0, 0.0, 0.0] for k in keys}
+    samples = {k: [] for k in keys}
+    done = {k: False for k in keys}
+    kalman, t_last = False, None
+    for ty, v, t in zip(types, values, times):
+        ty, t = int(ty), int(t)
+        if not all(done.values()):
+            if ty in sums:
+                if len(samples[ty]) < n_avg:
+                    x = [float(c) for c in v]
+                    samples[ty].append(x)
+                    for j in range(3):
+                        sums[ty][j] += x[j]
+                else:
+                    done[ty] = True
+        else:
+            kalman, t_last = True, t
+    out = dict(ready=kalman, t_init=t_last)
+    for k, name in ((ACC, "acc"), (MAG, "mag"), (GYRO, "gyro")):
+        if not kalman:
+            out[name] = out["var_" + name] = [float("nan")] * 3
+            continue
+        mean = [sums[k][j] / n_avg for j in range(3)]
+        var = [0.0, 0.0, 0.0]
+        for x in samples[k]:
+            for j in range(3):
+                var[j] += (x[j] - mean[j]) * (x[j] - mean[j])
+        out[name] = mean
+        out["var_" + name] = [var[j] / (n_avg - 1) for j in range(3)]
+    return out

@@ -181,9 +181,106 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
     if (bad && err) atomicOr(err, bad);
 }
 
+// Phase 2 of the server's Parser (ProcessString, Parser.cpp:36-58; initialMeanAndCovariance,
+// :84-140; InitialValues.cpp): the first n_avg samples of each sensor type are averaged (a
+// sequential FP64 sum divided by n_avg) and their sample variance formed ((x - mean)^2 summed in
+// order, divided by n_avg - 1).  A sensor counts as initialised at its first sample after those
+// n_avg; the first event after all three are initialised builds the KalmanFilter (T0 = its time,
+// acc_0 / mag_0 = the raw means at that time), and every later phase-2 event moves the acc_0 / mag_0
+// time and previousT to its own (setAcc0 / setMag0, UpdateLatestPreviousTime).  So phase 3 starts
+// from init = {mean acc, mean mag} at t_init = the last phase-2 event's time -- exactly the inputs of
+// pekf_frontend_dev.  Same event planes as phase 3; two passes over them (the variance needs the
+// mean first, as InitialValues::compute_mean_and_variance has it).
+__global__ __launch_bounds__(kFeBlock) void k_frontend_init(int64_t batch, int64_t n_events, const float4 *__restrict__ ev,
+                                                            const int64_t *__restrict__ t_start, int n_avg,
+                                                            double *__restrict__ init, int64_t *__restrict__ t_init,
+                                                            double *__restrict__ stats, int32_t *__restrict__ ready) {
+    const int64_t b = (int64_t)blockIdx.x * kFeBlock + threadIdx.x;
+    if (b >= batch) return;
+    const uint32_t lane = (uint32_t)b;
+    double sum[3][3] = {};  // [type][xyz]
+    int cnt[3] = {0, 0, 0};
+    bool done[3] = {false, false, false};  // Acc_ / Gyr_ / Mag_initialized
+    bool kalman = false;
+    int64_t t = t_start[b], t_last = t;
+    for (int64_t e = 0; e < n_events; ++e) {
+        const float4 v4 = (ev + e * batch)[lane];
+        const uint32_t word = __float_as_uint(v4.w);
+        const int ty = (int)(word & 3u);
+        t += (int64_t)(word >> 2);
+        if (!(done[0] && done[1] && done[2])) {
+            if (ty <= 2) {
+                if (cnt[ty] < n_avg) {
+                    sum[ty][0] += (double)v4.x;
+                    sum[ty][1] += (double)v4.y;
+                    sum[ty][2] += (double)v4.z;
+                    ++cnt[ty];
+                } else {
+                    done[ty] = true;
+                }
+            }
+        } else {
+            kalman = true;  // the KalmanFilter is built at the first such event, later ones move its time
+            t_last = t;
+        }
+    }
+    double mean[3][3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) mean[k][j] = sum[k][j] / (double)n_avg;
+    // second pass: the variance of the first n_avg samples of each type, in their order
+    double var[3][3] = {};
+    int c2[3] = {0, 0, 0};
+    for (int64_t e = 0; e < n_events; ++e) {
+        if (c2[0] >= n_avg && c2[1] >= n_avg && c2[2] >= n_avg) break;
+        const float4 v4 = (ev + e * batch)[lane];
+        const int ty = (int)(__float_as_uint(v4.w) & 3u);
+        if (ty <= 2 && c2[ty] < n_avg) {
+#pragma clang fp contract(off)
+            const double d0 = (double)v4.x - mean[ty][0], d1 = (double)v4.y - mean[ty][1], d2 = (double)v4.z - mean[ty][2];
+            var[ty][0] += d0 * d0;
+            var[ty][1] += d1 * d1;
+            var[ty][2] += d2 * d2;
+            ++c2[ty];
+        }
+    }
+    const double nan = __builtin_nan("");
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        init[6 * b + j] = kalman ? mean[kEvAcc][j] : nan;
+        init[6 * b + 3 + j] = kalman ? mean[kEvMag][j] : nan;
+    }
+    t_init[b] = t_last;
+    ready[b] = kalman ? 1 : 0;
+    if (stats) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            stats[12 * b + j] = kalman ? mean[kEvGyro][j] : nan;
+            stats[12 * b + 3 + j] = kalman ? var[kEvAcc][j] / (double)(n_avg - 1) : nan;
+            stats[12 * b + 6 + j] = kalman ? var[kEvMag][j] / (double)(n_avg - 1) : nan;
+            stats[12 * b + 9 + j] = kalman ? var[kEvGyro][j] / (double)(n_avg - 1) : nan;
+        }
+    }
+}
+
 }  // namespace pekf
 
 using namespace pekf;
+
+extern "C" int pekf_frontend_init_dev(int64_t batch, int64_t n_events, const void *ev_planes, const int64_t *t_start,
+                                      int n_avg, double *init, int64_t *t_init, double *stats, int32_t *ready,
+                                      void *stream) {
+    PEKF_CHECK_ARG(batch >= 0 && n_events >= 0, "negative size");
+    PEKF_CHECK_ARG(n_avg >= 2, "n_avg must be >= 2 (the variance divides by n_avg - 1)");
+    if (batch == 0) return PEKF_OK;
+    PEKF_CHECK_ARG(ev_planes && t_start && init && t_init && ready, "null pointer");
+    hipLaunchKernelGGL(k_frontend_init, dim3(grid_for(batch, kFeBlock)), dim3(kFeBlock), 0, as_stream(stream), batch,
+                       n_events, static_cast<const float4 *>(ev_planes), t_start, n_avg, init, t_init, stats, ready);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "k_frontend_init");
+    return PEKF_OK;
+}
 
 extern "C" int pekf_frontend_dev(int64_t batch, int64_t n_events, const void *ev_planes, const double *init,
                                  const int64_t *t_init, double alpha, int64_t r_max, void *plane_gd, void *plane_am, void *plane_my, int32_t *counts, double *refs,

@@ -275,6 +275,24 @@ def run_frontend(ev, alpha=0.1, r_max=None):
     return win, win.counts
 
 
+def frontend_init(ev, n_avg=100):
+    """Phase-2 events (synth.generate_events layout; ev["t_init"] = the time before the first one) ->
+    dict(init (K, 6) raw {acc, mag} means, t_init (K,) int64, ready (K,) bool, gyro_mean (K, 3),
+    var_acc / var_mag / var_gyro (K, 3)) by pekf_frontend_init_dev: the inputs run_frontend needs
+    for phase 3 (KFS/Parser.cpp:36-58,84-140, KFS/InitialValues.cpp)."""
+    planes = synth.pack_events(ev)
+    E, K = planes.shape[:2]
+    evb = DeviceBuffer(planes.nbytes).upload(planes)
+    tsb = DeviceBuffer(8 * K).upload(np.ascontiguousarray(ev["t_init"], np.int64))
+    ib, tib, sb, rb = DeviceBuffer(48 * K), DeviceBuffer(8 * K), DeviceBuffer(96 * K), DeviceBuffer(4 * K)
+    check(lib.pekf_frontend_init_dev(K, E, evb.ptr, tsb.ptr, int(n_avg), ib.ptr, tib.ptr, sb.ptr, rb.ptr, None))
+    check(lib.pekf_device_sync())
+    st = sb.download((K, 12), np.float64)
+    return dict(init=ib.download((K, 6), np.float64), t_init=tib.download((K,), np.int64),
+                ready=rb.download((K,), np.int32).astype(bool), gyro_mean=st[:, 0:3], var_acc=st[:, 3:6],
+                var_mag=st[:, 6:9], var_gyro=st[:, 9:12])
+
+
 # ------------------------------------------------------------------ the batched filter
 
 class BatchedEKF:

@@ -1,4 +1,5 @@
-"""Server front-end: raw phone events -> records -> filter.
+"""Server front-end: raw phone events -> records -> filter, and the phase-2
+initial means / variances that phase 3 starts from (KFS/Parser.cpp:36-58,84-140, InitialValues.cpp).
 
 PARTLY PINNED: the checker is oracle/frontend_numpy.py, a restatement of the C++ front-end
 (KFS/Parser.cpp, KFS/KalmanFilter.cpp), which cannot be built here (Eigen, Windows headers) and
@@ -163,3 +164,94 @@ def test_frontend_zero_time_gaps_follow_ieee_like_the_cpp(eng):
         fin = np.isfinite(a)
         assert _f32_ulps(rec.acc[:r, k][fin], a[fin]) <= 1
         assert _f32_ulps(rec.mag[:r, k], m) <= 1
+
+
+# ------------------------------------------------------------------ phase 2: initial means / variances
+
+def test_oracle_initial_values_state_machine():
+    """Parser.cpp:36-58,84-140 with n_avg = 2: each sensor is initialised at its first sample after
+    two, the KalmanFilter at the next event after all three, and later events move t_init."""
+    A, G, M = synth.EV_ACC, synth.EV_GYRO, synth.EV_MAG
+    spec = [(A, 10), (A, 10), (G, 10), (G, 10), (M, 10), (M, 10), (A, 10), (G, 10)]
+    ev = _events(1, spec)
+    o = fe.initial_values(ev["types"][:, 0], ev["values"][:, 0], ev["times"][:, 0], n_avg=2)
+    assert not o["ready"]                                   # the magnetometer has no third sample yet
+    ev = _events(1, spec + [(M, 10), (A, 10), (G, 20)])     # M initialises it; A builds the filter; G moves time
+    o = fe.initial_values(ev["types"][:, 0], ev["values"][:, 0], ev["times"][:, 0], n_avg=2)
+    assert o["ready"] and o["t_init"] == int(ev["times"][-1, 0])
+    acc = ev["values"][:2, 0].astype(np.float64)           # the first two acc samples only
+    assert np.allclose(o["acc"], acc.mean(0), rtol=0, atol=1e-15)
+    assert np.allclose(o["var_acc"], acc.var(0, ddof=1), rtol=1e-15, atol=1e-15)
+
+
+def test_oracle_initial_values_match_numpy_statistics():
+    ev = synth.generate_events(np.arange(3), 700, seed=21)
+    for k in range(3):
+        o = fe.initial_values(ev["types"][:, k], ev["values"][:, k], ev["times"][:, k])
+        assert o["ready"] and o["t_init"] == int(ev["times"][-1, k])
+        for ty, name in ((synth.EV_ACC, "acc"), (synth.EV_MAG, "mag"), (synth.EV_GYRO, "gyro")):
+            x = ev["values"][:, k][ev["types"][:, k] == ty][:100].astype(np.float64)
+            assert np.allclose(o[name], x.mean(0), rtol=1e-15, atol=1e-12)
+            assert np.allclose(o["var_" + name], x.var(0, ddof=1), rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("E,n_avg", [(700, 100), (520, 100), (40, 2)])
+def test_frontend_init_kernel_vs_oracle(eng, E, n_avg):
+    """pekf_frontend_init_dev against the restatement, bit for bit (the same sequential FP64 sums and
+    IEEE divisions), including filters that never get ready (520 events: about a third lack a
+    magnetometer sample after their first 100)."""
+    K = 300
+    ev = synth.generate_events(np.arange(K), E, seed=8)
+    got = eng.frontend_init(ev, n_avg=n_avg)
+    n_ready = 0
+    for k in range(K):
+        o = fe.initial_values(ev["types"][:, k], ev["values"][:, k], ev["times"][:, k], n_avg=n_avg)
+        assert got["ready"][k] == o["ready"]
+        if not o["ready"]:
+            assert np.isnan(got["init"][k]).all()
+            continue
+        n_ready += 1
+        assert got["t_init"][k] == o["t_init"]
+        assert np.array_equal(got["init"][k], np.array(o["acc"] + o["mag"]))
+        assert np.array_equal(got["gyro_mean"][k], np.array(o["gyro"]))
+        for name in ("acc", "mag", "gyro"):
+            assert np.array_equal(got["var_" + name][k], np.array(o["var_" + name]))
+    assert n_ready > 0 and (E != 520 or n_ready < K)
+
+
+@pytest.mark.gpu
+def test_phase2_then_phase3_events_to_filter(eng, oracle_c):
+    """The whole server front-end on the device: phase-2 events -> initial means and time
+    (pekf_frontend_init_dev) -> phase-3 events -> records (pekf_frontend_dev) -> the fused filter,
+    against the oracle chain (restatements of both phases + the C filter)."""
+    K = 96
+    ph2 = synth.generate_events(np.arange(K), 800, seed=31)
+    ini = eng.frontend_init(ph2)
+    assert ini["ready"].all()
+    ph3 = synth.generate_events(np.arange(K), 400, seed=32)
+    # phase 3 continues from the phase-2 means at the last phase-2 event's time
+    shift = ini["t_init"] - ph3["t_init"]
+    ph3 = dict(ph3, times=ph3["times"] + shift[None, :], t_init=ini["t_init"],
+               init_acc=ini["init"][:, :3], init_mag=ini["init"][:, 3:])
+    win, counts = eng.run_frontend(ph3)
+    cols = np.array([0, 1, 47, 95])
+    for k in cols:
+        o = fe.initial_values(ph2["types"][:, k], ph2["values"][:, k], ph2["times"][:, k])
+        assert o["t_init"] == ini["t_init"][k] and np.array_equal(np.array(o["acc"] + o["mag"]), ini["init"][k])
+    n = int(counts[cols].min())
+    gy, dtw, acc, mag = [], [], [], []
+    for k in cols:
+        g, dt, a, m = _oracle_records(ph3, k)
+        gy.append(g[:n]); dtw.append(dt[:n]); acc.append(a[:n]); mag.append(m[:n])
+    refs = win.refs.download((K, 6), np.float64)[cols]
+    rec = synth.Records(np.stack(gy, 1).astype(np.float32), np.stack(acc, 1).astype(np.float32),
+                        np.stack(mag, 1).astype(np.float32), np.stack(dtw, 1).astype(np.uint32),
+                        refs[:, :3], refs[:, 3:])
+    Xo, _, _ = oracle_c.run(rec)
+    f2 = eng.BatchedEKF(K)
+    f2.run(win, n_steps=n, counts=np.full(K, n))
+    X2, _ = f2.get_state()
+    err = float(np.abs(X2[cols] - Xo).max())
+    print("phase 2 + phase 3 + filter vs oracle chain: max |dq| = %.3e over %d records" % (err, n))
+    assert err < 1e-9
