@@ -203,25 +203,37 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend_init(int64_t batch, int64
     bool done[3] = {false, false, false};  // Acc_ / Gyr_ / Mag_initialized
     bool kalman = false;
     int64_t t = t_start[b], t_last = t;
-    for (int64_t e = 0; e < n_events; ++e) {
-        const float4 v4 = (ev + e * batch)[lane];
-        const uint32_t word = __float_as_uint(v4.w);
-        const int ty = (int)(word & 3u);
-        t += (int64_t)(word >> 2);
-        if (!(done[0] && done[1] && done[2])) {
-            if (ty <= 2) {
-                if (cnt[ty] < n_avg) {
-                    sum[ty][0] += (double)v4.x;
-                    sum[ty][1] += (double)v4.y;
-                    sum[ty][2] += (double)v4.z;
-                    ++cnt[ty];
-                } else {
-                    done[ty] = true;
+    // events come kInitRing rows at a time, all loads issued before the first is used (the loop body
+    // is a few adds, so without it each wave would wait out one memory latency per event); rows past
+    // the end are clamped to the last row and not processed
+    constexpr int kInitRing = 8;
+    auto row = [&](int64_t e) -> float4 { return (ev + (e < n_events ? e : n_events - 1) * batch)[lane]; };
+    for (int64_t e0 = 0; e0 < n_events; e0 += kInitRing) {
+        float4 r[kInitRing];
+#pragma unroll
+        for (int k = 0; k < kInitRing; ++k) r[k] = row(e0 + k);
+#pragma unroll
+        for (int k = 0; k < kInitRing; ++k) {
+            if (e0 + k >= n_events) break;  // uniform
+            const float4 v4 = r[k];
+            const uint32_t word = __float_as_uint(v4.w);
+            const int ty = (int)(word & 3u);
+            t += (int64_t)(word >> 2);
+            if (!(done[0] && done[1] && done[2])) {
+                if (ty <= 2) {
+                    if (cnt[ty] < n_avg) {
+                        sum[ty][0] += (double)v4.x;
+                        sum[ty][1] += (double)v4.y;
+                        sum[ty][2] += (double)v4.z;
+                        ++cnt[ty];
+                    } else {
+                        done[ty] = true;
+                    }
                 }
+            } else {
+                kalman = true;  // the KalmanFilter is built at the first such event, later ones move its time
+                t_last = t;
             }
-        } else {
-            kalman = true;  // the KalmanFilter is built at the first such event, later ones move its time
-            t_last = t;
         }
     }
     double mean[3][3];
@@ -232,17 +244,25 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend_init(int64_t batch, int64
     // second pass: the variance of the first n_avg samples of each type, in their order
     double var[3][3] = {};
     int c2[3] = {0, 0, 0};
-    for (int64_t e = 0; e < n_events; ++e) {
+    for (int64_t e0 = 0; e0 < n_events; e0 += kInitRing) {
         if (c2[0] >= n_avg && c2[1] >= n_avg && c2[2] >= n_avg) break;
-        const float4 v4 = (ev + e * batch)[lane];
-        const int ty = (int)(__float_as_uint(v4.w) & 3u);
-        if (ty <= 2 && c2[ty] < n_avg) {
+        float4 r[kInitRing];
+#pragma unroll
+        for (int k = 0; k < kInitRing; ++k) r[k] = row(e0 + k);
+#pragma unroll
+        for (int k = 0; k < kInitRing; ++k) {
+            if (e0 + k >= n_events) break;  // uniform
+            const float4 v4 = r[k];
+            const int ty = (int)(__float_as_uint(v4.w) & 3u);
+            if (ty <= 2 && c2[ty] < n_avg) {
 #pragma clang fp contract(off)
-            const double d0 = (double)v4.x - mean[ty][0], d1 = (double)v4.y - mean[ty][1], d2 = (double)v4.z - mean[ty][2];
-            var[ty][0] += d0 * d0;
-            var[ty][1] += d1 * d1;
-            var[ty][2] += d2 * d2;
-            ++c2[ty];
+                const double d0 = (double)v4.x - mean[ty][0], d1 = (double)v4.y - mean[ty][1],
+                             d2 = (double)v4.z - mean[ty][2];
+                var[ty][0] += d0 * d0;
+                var[ty][1] += d1 * d1;
+                var[ty][2] += d2 * d2;
+                ++c2[ty];
+            }
         }
     }
     const double nan = __builtin_nan("");

@@ -136,6 +136,24 @@ def main():
                        "events_per_s": K * E / (ms * 1e-3), "gbs": byts / (ms * 1e-3) / 1e9,
                        "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM, "bytes": byts}
     log("frontend: %.2f ms, %.2e events/s, %.0f GB/s" % (ms, K * E / (ms * 1e-3), byts / (ms * 1e-3) / 1e9))
+    # phase 2 on the same event planes: two passes (the means, then the variances of the first 100
+    # samples of each type; the second pass stops once every type has had its 100)
+    ib2, tb2, sb2, rb2 = (engine.DeviceBuffer(k * K) for k in (48, 8, 96, 4))
+    ms = timed(lambda: check(lib.pekf_frontend_init_dev(K, E, evb.ptr, tb.ptr, 100, ib2.ptr, tb2.ptr, sb2.ptr,
+                                                        rb2.ptr, s)), s)
+    # algorithmic bytes: pass 1 reads every event; pass 2 a filter's events up to the one that brings
+    # its last sensor type to 100 samples
+    ty = ev["types"]
+    last = np.zeros(K0, np.int64)
+    for t in (synth.EV_ACC, synth.EV_GYRO, synth.EV_MAG):
+        c = np.cumsum(ty == t, axis=0)
+        last = np.maximum(last, np.argmax(c >= 100, axis=0) + 1)
+    byts = 16 * (K * E + tile * int(last.sum()))
+    res["frontend_init"] = {"filters": K, "events_per_filter": E, "kernel_ms": ms, "events_per_s": K * E / (ms * 1e-3),
+                            "ready": int(rb2.download((K,), np.int32).sum()), "bytes": byts,
+                            "gbs": byts / (ms * 1e-3) / 1e9, "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM}
+    log("frontend phase 2: %.2f ms" % ms)
+    del ib2, tb2, sb2, rb2
     del evb, win
 
     # ---- side outputs on a config-3-sized window
