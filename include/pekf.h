@@ -207,6 +207,18 @@ int pekf_frontend_dev(int64_t batch, int64_t n_events, const void *ev_planes, co
                       void *plane_gd, void *plane_am, void *plane_my, int32_t *counts, double *refs,
                       int *dev_error, void *stream);
 
+/* The server's phase 3 with the filter fused in: pekf_frontend_dev's records are not
+ * written anywhere -- each is applied to the filter's state on the same lane (Prediction + Correction,
+ * main_file.py:42-45) as soon as the wave runs its next filter step.  Same events, init, t_init, alpha
+ * and refs as pekf_frontend_dev; X[batch*4], P[batch*16] (AoS, FP64) are the filters' state, read at
+ * the start and written at the end (left untouched for a filter with no record); q, r as pekf_run_dev.
+ * counts[b] receives the number of records filter b applied.  The final state equals pekf_frontend_dev
+ * followed by pekf_run_dev with those counts, bit for bit.  *dev_error |= 1 if a record dt does not fit
+ * 31 bits (no r_max: there is no record window). */
+int pekf_live_dev(int64_t batch, int64_t n_events, const void *ev_planes, const double *init,
+                  const int64_t *t_init, double alpha, double *X, double *P, double q, double r,
+                  int32_t *counts, double *refs, int *dev_error, void *stream);
+
 /* Phase 2 of the server's Parser (KFS/Parser.cpp:36-58,84-140; KFS/InitialValues.cpp) on the device: per
  * filter, the mean and sample variance of the first n_avg (the server: 100) samples of each sensor type,
  * and the time phase 3 continues from.  Events as for pekf_frontend_dev (ev_planes [n_events][batch], word

@@ -95,6 +95,7 @@ SIGNATURES = {
     "pekf_quat_to_rpy": [_i64, _vp, _vp],
     "pekf_frontend_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "pekf_frontend_init_dev": [_i64, _i64, _vp, _vp, _int, _vp, _vp, _vp, _vp, _vp],
+    "pekf_live_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _vp, _vp, _dbl, _dbl, _vp, _vp, _vp, _vp],
     "pekf_log_scan": [ctypes.c_char_p, ctypes.POINTER(_i64)],
     "pekf_log_read": [ctypes.c_char_p, _i64, _vp, _vp, _vp, _vp, _dp, _dp, _dp],
     "pekf_quat_to_rpy_dev": [_i64, _vp, _vp, _vp],

@@ -31,6 +31,13 @@ inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s);
 
 inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
 
+// One record of the stream as it sits in the three planes (include/pekf.h, pekf_run_dev)
+struct Rec {
+    float4 gd;  // gx, gy, gz, bits(dt word)
+    float4 am;  // ax, ay, az, mx
+    float2 my;  // my, mz
+};
+
 // Host-pointer calls: inputs are packed into one coherent, mapped pinned buffer.  Small calls
 // (<= kZeroCopyMaxBytes of inputs + outputs, e.g. the n = 1 calls of main_file.py) run
 // zero-copy: the kernel reads and writes that buffer over PCIe, so a call is one launch and one

@@ -1,0 +1,252 @@
+// pekf_live.hip -- the live server's whole per-event loop on the device in one pass (SURVEY.md §8f-2:
+// the front-end fused into the filter kernel): raw phone events -> phase-3 records (pekf_phase3.hpp,
+// Parser::WriteKalmanFilterMeasurement / ExecuteKalmanFilter, KFS/Parser.cpp:148-267) -> Prediction +
+// Correction of each record (pekf_step.hpp, ExtendedKalmanFilter.py:58-80 as main_file.py:42-45 calls
+// them).  One lane per filter holds its front-end state, X and covariance in registers; records never
+// touch memory.  The split pipeline -- pekf_frontend_dev writing records to the stream planes, then
+// pekf_run_dev with counts reading them back -- pays a 40 B record write that scatters into 96 B of
+// sectors (each lane's record count drifts, so a wave's stores land in 64 different rows) plus the
+// 40 B read; here the only HBM traffic is the 16 B event.
+//
+// Lanes complete records at different events (a record needs a gyro, an acc and a mag sample after the
+// previous one: every ~10 events on the synthetic streams, never closer than 3), but a filter step is
+// ~300 FP64 instructions that the wave executes for every lane at once.  Running it whenever some lane
+// has a record would run it at nearly every emit with a few lanes active, so each lane queues its
+// records (kQueue deep) and the wave runs one filter step -- the oldest queued record of every lane
+// that has one -- at the end of a block of kRing events when at least kQuorum lanes have a record
+// queued, or when some lane's queue could overflow within the next block, and until empty after the
+// last event (scripts/live_queue_sim.py: 0.79 of the lanes busy per step at 3 / 6 / 56 against 0.28
+// when every block drains).  Per lane the records apply in order with the same arithmetic as
+// pekf_run_dev's multi-record kernel (reference basis, N, omod), so the final state equals the split
+// pipeline's bit for bit.
+#include "pekf_phase3.hpp"
+#include "pekf_step.hpp"
+
+namespace pekf {
+
+// Tuned on the box (scripts/ab_live.sh, profiles/r2/live/): the kernel is register-bound -- front-end
+// state, filter state and a filter step's temporaries -- so the record queue lives in LDS and the
+// launch is held to 2 waves per SIMD (256 registers; a few spills) with a 3-event ring: 5.7 ms at
+// 1M filters x 1,024 events, against 8.7 ms for 6 events and the queue in registers at 1 wave/SIMD.
+#ifndef PEKF_LIVE_RING
+#define PEKF_LIVE_RING 3  // event rows in flight per lane; a filter step may run after each block of them
+#endif
+#ifndef PEKF_LIVE_QUEUE
+#define PEKF_LIVE_QUEUE 6  // records a lane can hold (40 B of LDS each)
+#endif
+#ifndef PEKF_LIVE_QUORUM
+#define PEKF_LIVE_QUORUM 56  // lanes of 64 with a queued record that trigger a filter step
+#endif
+#ifndef PEKF_LIVE_LDS_QUEUE
+#define PEKF_LIVE_LDS_QUEUE 1  // 0: the queue in registers (RecordQueue)
+#endif
+#ifndef PEKF_LIVE_ATTR
+#define PEKF_LIVE_ATTR __attribute__((amdgpu_waves_per_eu(2)))
+#endif
+
+// component-wise c ? a : b of a record (a struct-valued ?: would go through scratch memory)
+__device__ __forceinline__ Rec sel(bool c, const Rec &a, const Rec &b) {
+    Rec o;
+    o.gd = make_float4(c ? a.gd.x : b.gd.x, c ? a.gd.y : b.gd.y, c ? a.gd.z : b.gd.z, c ? a.gd.w : b.gd.w);
+    o.am = make_float4(c ? a.am.x : b.am.x, c ? a.am.y : b.am.y, c ? a.am.z : b.am.z, c ? a.am.w : b.am.w);
+    o.my = make_float2(c ? a.my.x : b.my.x, c ? a.my.y : b.my.y);
+    return o;
+}
+
+// A lane's records waiting for the wave's next filter step, oldest first, in registers: slots are
+// separate variables (an array, even statically indexed, was left in scratch) and a push selects
+// its slot.
+template <int Q>
+struct RecQueue;
+template <>
+struct RecQueue<0> {
+    __device__ __forceinline__ void put(int, const Rec &) {}
+    __device__ __forceinline__ void shift(Rec &) {}
+};
+template <int Q>
+struct RecQueue {
+    Rec head;
+    RecQueue<Q - 1> tail;
+    // slot i (0 = oldest) takes r
+    __device__ __forceinline__ void put(int i, const Rec &r) {
+        head = sel(i == 0, r, head);
+        tail.put(i - 1, r);
+    }
+    // every slot moves up one (slot 0 into `out`)
+    __device__ __forceinline__ void shift(Rec &out) {
+        out = head;
+        tail.shift(head);
+    }
+};
+template <int Q>
+struct RecordQueue {
+    RecQueue<Q> slots;
+    int n = 0;
+    __device__ __forceinline__ void push(const Rec &r) {
+        slots.put(n, r);
+        ++n;
+    }
+    // the oldest record (meaningful when n > 0)
+    __device__ __forceinline__ Rec pop() {
+        Rec r;
+        slots.shift(r);
+        n = n > 0 ? n - 1 : 0;
+        return r;
+    }
+};
+
+// The same queue in LDS: a ring of Q slots per lane, [slot][lane] so that a wave's accesses fall in
+// distinct banks whatever slot each lane is at.  A push or pop is a few address operations and three
+// LDS accesses instead of selects / moves over every slot, and the records' registers are free.
+template <int Q>
+struct LdsQueue {
+    float4 (*gd)[kRunBlock];
+    float4 (*am)[kRunBlock];
+    float2 (*my)[kRunBlock];
+    int head = 0, n = 0;
+    __device__ __forceinline__ void push(const Rec &r) {
+        const int slot = head + n < Q ? head + n : head + n - Q;
+        gd[slot][threadIdx.x] = r.gd;
+        am[slot][threadIdx.x] = r.am;
+        my[slot][threadIdx.x] = r.my;
+        ++n;
+    }
+    __device__ __forceinline__ Rec pop() {
+        const Rec r = {gd[head][threadIdx.x], am[head][threadIdx.x], my[head][threadIdx.x]};
+        if (n > 0) {
+            head = head + 1 < Q ? head + 1 : 0;
+            --n;
+        }
+        return r;
+    }
+};
+
+__global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(int64_t batch, int64_t n_events, const float4 *__restrict__ ev,
+                                                    const double *__restrict__ init, const int64_t *__restrict__ t_init,
+                                                    double alpha, double qs, double rs, double *__restrict__ Xio,
+                                                    double *__restrict__ Pio, int32_t *__restrict__ counts,
+                                                    double *__restrict__ refs, int *__restrict__ err) {
+    constexpr int kRing = PEKF_LIVE_RING, kFlush = 3, kQueue = PEKF_LIVE_QUEUE, kQuorum = PEKF_LIVE_QUORUM;
+    constexpr int kPush = kRing / kFlush;  // records a lane can complete within one block
+    static_assert(kRing % kFlush == 0, "the ring depth must be a multiple of the emit period");
+    static_assert(kQueue >= kPush, "the queue must hold a block's records");
+    const int64_t b = (int64_t)blockIdx.x * kRunBlock + threadIdx.x;
+    if (b >= batch) return;
+
+    Phase3 fe;
+    fe.start(init + 6 * b, t_init[b], alpha);
+    double rf[6];
+    fe.refs(rf);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) refs[6 * b + k] = rf[k];
+
+    // the filter in its reference frame's basis, covariance as N (pekf_step.hpp), as k_run does it
+    Frame Wf;
+    make_frame<true>(rf, rf + 3, Wf);
+    double x[4];
+    Sym4T<double> P;
+    load_state<false>(Xio, Pio, b, batch, x, P);
+    RefWLazy Wr;
+    Wr.aW = Wf.alpha; Wr.b1W = Wf.beta1; Wr.b2W = Wf.beta2;
+    Wr.pair = refs + 6 * b;
+    {
+        double qw[4];
+        frame_quat(Wf, qw);
+        to_ref_basis(qw, x, P, rs);
+    }
+    const StepK<double> kc = step_consts<double, true>(qs, rs);
+
+#if PEKF_LIVE_LDS_QUEUE
+    __shared__ float4 q_gd[kQueue][kRunBlock], q_am[kQueue][kRunBlock];
+    __shared__ float2 q_my[kQueue][kRunBlock];
+    LdsQueue<kQueue> queue;
+    queue.gd = q_gd; queue.am = q_am; queue.my = q_my;
+#else
+    RecordQueue<kQueue> queue;
+#endif
+    int32_t applied = 0;
+    int bad = 0;
+    // One filter step for every lane with a queued record: its oldest, Prediction + Correction with
+    // the multi-record kernel's arithmetic (the first record of the launch from the loaded |X|^2,
+    // every later one lazy; front-end records always carry a magnetometer sample).
+    auto filter_step = [&]() {
+        const bool has = queue.n > 0;
+        const Rec cur = queue.pop();
+        OmodMode mode;
+        mode.enter();
+        if (has) {
+            const double gy[3] = {cur.gd.x, cur.gd.y, cur.gd.z};
+            const double dt = (double)(__float_as_uint(cur.gd.w) & 0x7FFFFFFFu);
+            const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
+            const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
+            if (applied == 0)
+                ekf_record_step<double, true, false, true>(x, state_norm2(x), P, Wr, kc, gy, dt, false, acc, mag);
+            else
+                ekf_record_step<double, true, true, true>(x, 1.0, P, Wr, kc, gy, dt, false, acc, mag);
+            ++applied;
+        }
+        mode.leave();
+    };
+    auto flush = [&]() {
+        if (fe.pend) queue.push(fe.emit(bad));
+    };
+
+    // Events stream through a register ring of kRing rows loaded kRing events ahead (the loop is
+    // unrolled by kRing so every ring index is static; rows past the end are clamped to the last one).
+    const uint32_t lane = (uint32_t)b;
+    auto load = [&](int64_t e) -> float4 {
+        const int64_t row = e < n_events ? e : n_events - 1;
+        return (ev + row * batch)[lane];
+    };
+    if (n_events > 0) {
+        float4 ring[kRing];
+#pragma unroll
+        for (int k = 0; k < kRing; ++k) ring[k] = load(k);
+        for (int64_t e0 = 0; e0 < n_events; e0 += kRing) {
+#pragma unroll
+            for (int k = 0; k < kRing; ++k) {
+                if (e0 + k >= n_events) break;  // uniform
+                const float4 v4 = ring[k];
+                ring[k] = load(e0 + k + kRing);
+                fe.event(v4);
+                if ((k + 1) % kFlush == 0) flush();
+            }
+            flush();  // a record completed in a trailing partial block (nothing pending after a full one)
+            // wave-uniform: a step while some lane could overflow in the next block, then one more if
+            // a quorum of lanes has a record; after the last event until every queue is empty
+            const bool last = e0 + kRing >= n_events;
+            for (;;) {
+                const uint64_t queued = __ballot(queue.n > 0);
+                if (queued == 0) break;
+                if (!(last || __any(queue.n > kQueue - kPush) || __popcll(queued) >= kQuorum)) break;
+                filter_step();
+            }
+        }
+    }
+    counts[b] = applied;
+    if (bad && err) atomicOr(err, bad);
+    if (applied == 0) return;  // no record: the state is left as it was (as pekf_run_dev with counts)
+    from_ref_basis(Wr, x, P, rs);
+    store_state<false>(Xio, Pio, b, batch, x, P);
+}
+
+}  // namespace pekf
+
+using namespace pekf;
+
+extern "C" int pekf_live_dev(int64_t batch, int64_t n_events, const void *ev_planes, const double *init,
+                             const int64_t *t_init, double alpha, double *X, double *P, double q, double r,
+                             int32_t *counts, double *refs, int *dev_error, void *stream) {
+    PEKF_CHECK_ARG(batch >= 0 && n_events >= 0, "negative size");
+    if (batch == 0) return PEKF_OK;
+    PEKF_CHECK_ARG(batch < ((int64_t)1 << 28), "batch must be < 2^28 filters per launch");
+    PEKF_CHECK_ARG(ev_planes && init && t_init && X && P && counts && refs, "null pointer");
+    PEKF_CHECK_ARG((uintptr_t)ev_planes % 16 == 0, "misaligned event planes");
+    PEKF_CHECK_ARG(r > 0.0, "r must be > 0 (S = P- + rI must be SPD)");
+    hipLaunchKernelGGL(k_live, dim3(grid_for(batch, kRunBlock)), dim3(kRunBlock), 0, as_stream(stream), batch,
+                       n_events, static_cast<const float4 *>(ev_planes), init, t_init, alpha, q, r, X, P, counts,
+                       refs, dev_error);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "k_live");
+    return PEKF_OK;
+}

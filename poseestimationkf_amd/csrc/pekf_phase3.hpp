@@ -1,0 +1,163 @@
+// pekf_phase3.hpp -- phase 3 of the live server's front-end for one filter on one
+// lane: raw phone events in, the 40 B records the filter consumes out.  Shared by k_frontend
+// (pekf_frontend.hip: records written to the stream planes) and k_live (pekf_live.hip: records fed
+// straight into the filter on the same lane), so both produce the same records bit for bit.
+//
+// The event step is Parser::WriteKalmanFilterMeasurement (KFS/Parser.cpp:148-219); a record is
+// ExecuteKalmanFilter (Parser.cpp:229-257): acc / mag interpolated to the gyro time (:259-267),
+// normalised (:221-228), low-pass filtered (alpha, from a zero state: KalmanFilter.cpp:16-18,21-24,
+// 279-303), dt = gyro time - the previous record's (KalmanFilter.cpp:306-308).  FP64 arithmetic (one
+// reciprocal / rsqrt with a Newton step instead of IEEE divisions: ~1e-15 relative), records rounded
+// to f32 like every record of the stream.  The arithmetic is contracted as the compiler's default
+// (fp contract fast) whatever the including file is compiled with: every function with arithmetic
+// opens with that pragma, so k_live's records are k_frontend's.
+#pragma once
+
+#include "pekf_internal.hpp"
+#include "pekf_math.hpp"
+
+namespace pekf {
+
+enum : uint32_t { kEvAcc = 0, kEvGyro = 1, kEvMag = 2 };
+
+struct V3 {
+    double x, y, z;
+};
+struct F3 {
+    float x, y, z;
+};
+__device__ __forceinline__ V3 widen(const F3 &f) { return {f.x, f.y, f.z}; }
+// component-wise c ? a : b (a struct-valued ?: would go through scratch memory)
+__device__ __forceinline__ V3 sel(bool c, const V3 &a, const V3 &b) {
+    return {c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z};
+}
+__device__ __forceinline__ F3 sel(bool c, const F3 &a, const F3 &b) {
+    return {c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z};
+}
+
+// Parser::NormalizeValues (:221-228) with one rsqrt instead of a sqrt and three divisions
+__device__ __forceinline__ V3 normalised(const V3 &v) {
+#pragma clang fp contract(fast)
+    const double in = rsqrt<true>((v.x * v.x + v.y * v.y) + v.z * v.z);
+    return {v.x * in, v.y * in, v.z * in};
+}
+
+struct Phase3 {
+    // phase-2 state: acc_0 / mag_0 = raw means at the initialisation time (Parser.cpp:44-53)
+    V3 acc0, mag0;
+    double t_acc0, t_mag0, prev_t, t;
+    V3 acc1, mag1;  // sensor samples (exact f32 values, kept widened)
+    F3 gyro;
+    double t_acc1, t_mag1, t_gyro;
+    bool gyro_set, acc1_set, mag1_set;
+    V3 lpf_acc, lpf_mag;
+    double alpha, beta;
+
+    // Emission is deferred: when a lane completes a record, only its inputs are copied aside
+    // (pend), and the expensive part -- two interpolations with a reciprocal, two normalisations
+    // with an rsqrt, the low-pass and the f32 packing (emit) -- runs for the whole wave once every
+    // few events instead of on every event some lane completes one (which, with 64 lanes, is nearly
+    // every event).  A lane needs at least 3 events (gyro, acc, mag) between two records, so when
+    // emit runs every 3 events it never has two pending.  Arithmetic is unchanged: the time
+    // differences are formed at emission, exactly as lerp_to would form them.
+    bool pend;
+    F3 p_gyro;
+    V3 p_acc0, p_mag0, p_acc1, p_mag1;
+    double p_dt, p_an, p_ad, p_mn, p_md;  // dt, acc / mag lerp num and den
+
+    __device__ __forceinline__ void start(const double *init6, int64_t t_start, double a) {
+        acc0 = {init6[0], init6[1], init6[2]};
+        mag0 = {init6[3], init6[4], init6[5]};
+        t = t_acc0 = t_mag0 = prev_t = (double)t_start;
+        acc1 = mag1 = lpf_acc = lpf_mag = {0, 0, 0};
+        gyro = {0, 0, 0};
+        t_acc1 = t_mag1 = t_gyro = 0;
+        gyro_set = acc1_set = mag1_set = false;
+        alpha = a;
+        beta = 1.0 - a;
+        pend = false;
+        p_gyro = {0, 0, 0};
+        p_acc0 = p_mag0 = p_acc1 = p_mag1 = {0, 0, 0};
+        p_dt = p_an = p_mn = 0;
+        p_ad = p_md = 1;
+    }
+
+    // the filter's reference vectors: the normalised phase-2 means (Parser.cpp:48-49); call after start
+    __device__ __forceinline__ void refs(double (&r)[6]) const {
+        const V3 a = normalised(acc0), m = normalised(mag0);
+        r[0] = a.x; r[1] = a.y; r[2] = a.z;
+        r[3] = m.x; r[4] = m.y; r[5] = m.z;
+    }
+
+    // One event {x, y, z, bits(word)}: the word carries the type and the ns gap to the previous event.
+    // Parser::WriteKalmanFilterMeasurement (Parser.cpp:148-219), branch-free: each state variable is
+    // one select, so nothing is copied between divergent paths.
+    //   before a gyro sample: acc -> acc_0, mag -> mag_0, gyro -> gyro (gyro_is_set);
+    //   after it: acc -> acc_1, mag -> mag_1 (set); a new gyro replaces the gyro and shifts a set
+    //   acc_1 -> acc_0 / mag_1 -> mag_0, clearing both flags.
+    __device__ __forceinline__ void event(const float4 v4) {
+#pragma clang fp contract(fast)
+        const uint32_t word = __float_as_uint(v4.w);
+        const uint32_t ty = word & 3u;
+        t += (double)(word >> 2);
+        const bool isA = ty == kEvAcc, isM = ty == kEvMag, isG = ty == kEvGyro;
+        const bool gs = gyro_set;
+        const double vx = v4.x, vy = v4.y, vz = v4.z;
+        const bool wA1 = isA && gs, wM1 = isM && gs;
+        acc1 = sel(wA1, V3{vx, vy, vz}, acc1);
+        t_acc1 = wA1 ? t : t_acc1;
+        mag1 = sel(wM1, V3{vx, vy, vz}, mag1);
+        t_mag1 = wM1 ? t : t_mag1;
+        const bool a1s = wA1 || (acc1_set && !(isG && gs)), m1s = wM1 || (mag1_set && !(isG && gs));
+        const bool sA = isG && gs && acc1_set, sM = isG && gs && mag1_set;  // gyro shift
+        // ExecuteKalmanFilter (Parser.cpp:229-257) once acc_1 and mag_1 are both set: record its
+        // inputs (pending until the next emit), then acc_0 <- acc_1, mag_0 <- mag_1, flags cleared
+        const bool done = a1s && m1s;
+        if (done) {
+            asm volatile("");  // keeps this a branch: masked 64-bit moves, not two selects per double
+            pend = true;
+            p_gyro = gyro; p_dt = t_gyro - prev_t;
+            p_acc0 = acc0; p_acc1 = acc1; p_an = t_gyro - t_acc0; p_ad = t_acc1 - t_acc0;
+            p_mag0 = mag0; p_mag1 = mag1; p_mn = t_gyro - t_mag0; p_md = t_mag1 - t_mag0;
+            prev_t = t_gyro;
+        }
+        const bool wA0 = isA && !gs, wM0 = isM && !gs;
+        const bool cA = sA || done, cM = sM || done;  // acc_0 <- acc_1 (shift or after a record)
+        acc0 = sel(wA0, V3{vx, vy, vz}, sel(cA, acc1, acc0));
+        t_acc0 = wA0 ? t : (cA ? t_acc1 : t_acc0);
+        mag0 = sel(wM0, V3{vx, vy, vz}, sel(cM, mag1, mag0));
+        t_mag0 = wM0 ? t : (cM ? t_mag1 : t_mag0);
+        gyro = sel(isG, F3{v4.x, v4.y, v4.z}, gyro);
+        t_gyro = isG ? t : t_gyro;
+        gyro_set = (gs || isG) && !done;
+        acc1_set = a1s && !done;
+        mag1_set = m1s && !done;
+    }
+
+    // The pending record (call only when pend): interpolation, normalisation, low-pass, f32 packing.
+    // bad |= 1 if its dt does not fit the 31-bit dt word of the stream.
+    __device__ __forceinline__ Rec emit(int &bad) {
+#pragma clang fp contract(fast)
+        pend = false;
+        // Parser::LinearInterpolationSensor (:259-267): (y2 - y1) / (t2 - t1) * (t3 - t1) + y1, the
+        // division taken as one reciprocal.  Timestamps are integer ns held in doubles (exact below
+        // 2^53), so t3 - t1 and t2 - t1 are the exact differences (double)t3 - (double)t1 gives.
+        const double fa = p_an * recip<true>(p_ad), fm = p_mn * recip<true>(p_md);
+        const V3 a1 = p_acc1, m1 = p_mag1;
+        const V3 a = normalised({(a1.x - p_acc0.x) * fa + p_acc0.x, (a1.y - p_acc0.y) * fa + p_acc0.y,
+                                 (a1.z - p_acc0.z) * fa + p_acc0.z});
+        const V3 m = normalised({(m1.x - p_mag0.x) * fm + p_mag0.x, (m1.y - p_mag0.y) * fm + p_mag0.y,
+                                 (m1.z - p_mag0.z) * fm + p_mag0.z});
+        lpf_mag = {alpha * m.x + beta * lpf_mag.x, alpha * m.y + beta * lpf_mag.y, alpha * m.z + beta * lpf_mag.z};
+        lpf_acc = {alpha * a.x + beta * lpf_acc.x, alpha * a.y + beta * lpf_acc.y, alpha * a.z + beta * lpf_acc.z};
+        if (!(p_dt >= 0.0 && p_dt < 2147483648.0)) bad |= 1;
+        Rec r;
+        r.gd = make_float4((float)p_gyro.x, (float)p_gyro.y, (float)p_gyro.z,
+                           __uint_as_float((uint32_t)fmin(fmax(p_dt, 0.0), 2147483647.0)));
+        r.am = make_float4((float)lpf_acc.x, (float)lpf_acc.y, (float)lpf_acc.z, (float)lpf_mag.x);
+        r.my = make_float2((float)lpf_mag.y, (float)lpf_mag.z);
+        return r;
+    }
+};
+
+}  // namespace pekf

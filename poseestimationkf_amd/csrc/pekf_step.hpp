@@ -22,12 +22,6 @@ constexpr int kRunBlock = 256;
 #define PEKF_REC_AUX 2
 #endif
 
-struct Rec {
-    float4 gd;  // gx, gy, gz, bits(dt word)
-    float4 am;  // ax, ay, az, mx
-    float2 my;  // my, mz
-};
-
 // Filter state in HBM.  AoS (default, the ABI's natural layout): X[b][4], P[b][4][4].  SoA
 // (PEKF_RUN_STATE_SOA): X[4][batch] and the 10 unique entries of P as P[10][batch]
 // (00 01 02 03 11 12 13 22 23 33): every state load / store of a wave is one contiguous
@@ -283,6 +277,33 @@ __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> 
     }
 }
 
+// A multi-record launch runs the filter in its reference frame's own basis (RefW in pekf_math.hpp)
+// with the covariance carried as N, P = rI + beta D N D (StepK).  to_ref_basis: the state entering
+// the launch, x -> q_W^* x, P -> N of q_W^* P q_W; from_ref_basis: back at its end, X normalised.
+template <typename PT>
+__device__ __forceinline__ void to_ref_basis(const double *qw, double *x, Sym4T<PT> &P, double rs) {
+    double xw[4];
+    qmul_left<true>(qw, x, xw);
+    x[0] = xw[0]; x[1] = xw[1]; x[2] = xw[2]; x[3] = xw[3];
+    P = sym_rotate<true>(qw, P);
+    const PT ib = (PT)(1.0 / (kSqrt2 * rs)), rp = (PT)rs;
+    P = {(P.a00 - rp) * ib, P.a01 * ib, -P.a02 * ib, -P.a03 * ib, (P.a11 - rp) * ib,
+         -P.a12 * ib, -P.a13 * ib, (P.a22 - rp) * ib, P.a23 * ib, (P.a33 - rp) * ib};
+}
+template <typename PT, typename RW>
+__device__ __forceinline__ void from_ref_basis(const RW &Wr, double *x, Sym4T<PT> &P, double rs) {
+    const PT be = (PT)(kSqrt2 * rs), rp = (PT)rs;
+    P = {fma(be, P.a00, rp), be * P.a01, -be * P.a02, -be * P.a03, fma(be, P.a11, rp),
+         -be * P.a12, -be * P.a13, fma(be, P.a22, rp), be * P.a23, fma(be, P.a33, rp)};
+    const double in = rsqrt<true>(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]);
+    const double xn[4] = {x[0] * in, x[1] * in, x[2] * in, x[3] * in};
+    double xo[4], qw[4];
+    Wr.quat(qw);
+    qmul_left<false>(qw, xn, xo);
+    x[0] = xo[0]; x[1] = xo[1]; x[2] = xo[2]; x[3] = xo[3];
+    P = sym_rotate<false>(qw, P);
+}
+
 // MIXED = false: every operation in FP64 (the headline path).
 // MIXED = true (opt-in, PEKF_RUN_MIXED_PRECISION): the covariance recursion (P-, S^-1, K, P)
 // in FP32 while RK4, Wahba, R->q and the X update stay FP64 (~2e-8 vs FP64).
@@ -434,13 +455,7 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
         } else {
             Wr.pair = refs + 6 * b;
         }
-        double xw[4];
-        qmul_left<true>(qw, x, xw);
-        x[0] = xw[0]; x[1] = xw[1]; x[2] = xw[2]; x[3] = xw[3];
-        P = sym_rotate<true>(qw, P);
-        const PT ib = (PT)(1.0 / (kSqrt2 * rs)), rp = (PT)rs;
-        P = {(P.a00 - rp) * ib, P.a01 * ib, -P.a02 * ib, -P.a03 * ib, (P.a11 - rp) * ib,
-             -P.a12 * ib, -P.a13 * ib, (P.a22 - rp) * ib, P.a23 * ib, (P.a33 - rp) * ib};
+        to_ref_basis(qw, x, P, rs);
     }
     // The launch's first record takes |X|^2 from the loaded state; from then on the state is
     // unit and n2 = 1 is a compile-time constant (see state_norm2).  32-bit step counter
@@ -464,18 +479,7 @@ __global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_step
     }
     if constexpr (!MIXED) mode.leave();
     if (COUNTS && my_steps == 0) return;
-    {
-        const PT be = (PT)(kSqrt2 * rs), rp = (PT)rs;
-        P = {fma(be, P.a00, rp), be * P.a01, -be * P.a02, -be * P.a03, fma(be, P.a11, rp),
-             -be * P.a12, -be * P.a13, fma(be, P.a22, rp), be * P.a23, fma(be, P.a33, rp)};
-        const double in = rsqrt<true>(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]);
-        const double xn[4] = {x[0] * in, x[1] * in, x[2] * in, x[3] * in};
-        double xo[4], qw[4];
-        Wr.quat(qw);
-        qmul_left<false>(qw, xn, xo);
-        x[0] = xo[0]; x[1] = xo[1]; x[2] = xo[2]; x[3] = xo[3];
-        P = sym_rotate<false>(qw, P);
-    }
+    from_ref_basis(Wr, x, P, rs);
     store_state<SOA>(Xio, Pio, b, batch, x, P);
 }
 

@@ -380,6 +380,33 @@ class BatchedEKF:
             return tb.download((n_steps, self.batch, 4), np.float64)
         return None
 
+    def run_events_async(self, ev_planes, n_events, init, t_init, counts, refs, alpha=0.1, err=None, stream=None):
+        """Enqueue pekf_live_dev: device event planes [n_events][batch][4] f32 (synth.pack_events), init
+        (batch, 6), t_init (batch,) int64; counts (batch,) int32 and refs (batch, 6) outputs -- DeviceBuffers."""
+        if self.layout != "aos" or self.flags & RUN_MIXED_PRECISION:
+            raise ValueError("the fused front-end + filter kernel runs the FP64 filter on AoS state")
+        check(lib.pekf_live_dev(self.batch, int(n_events), ev_planes.ptr, init.ptr, t_init.ptr, float(alpha), self.X.ptr,
+                                self.P.ptr, self.q, self.r, counts.ptr, refs.ptr,
+                                err.ptr if err is not None else None, stream))
+
+    def run_events(self, ev, alpha=0.1):
+        """Raw phone events (synth.generate_events layout) -> front-end -> filter, fused in one launch
+        (pekf_live_dev).  Returns (counts (batch,) int32 records applied, refs (batch, 6)
+        the filters' acc0 / mag0).  Raises if a record dt does not fit the 31-bit field."""
+        planes = synth.pack_events(ev)
+        assert planes.shape[1] == self.batch
+        evb = DeviceBuffer(planes.nbytes).upload(planes)
+        init = DeviceBuffer(48 * self.batch).upload(
+            np.concatenate([ev["init_acc"], ev["init_mag"]], axis=1).astype(np.float64))
+        tib = DeviceBuffer(8 * self.batch).upload(np.ascontiguousarray(ev["t_init"], np.int64))
+        cnt, refs = DeviceBuffer(4 * self.batch), DeviceBuffer(48 * self.batch)
+        errb = DeviceBuffer(4).upload(np.zeros(1, np.int32))
+        self.run_events_async(evb, planes.shape[0], init, tib, cnt, refs, alpha, errb)
+        check(lib.pekf_device_sync())
+        if int(errb.download((1,), np.int32)[0]) & 1:
+            raise ValueError("a record's dt does not fit the 31-bit ns field of the stream")
+        return cnt.download((self.batch,), np.int32), refs.download((self.batch, 6), np.float64)
+
 
 class FilterHandle:
     """B KalmanFilter objects behind one native handle (pekf_filter_*).

@@ -3,6 +3,9 @@
 
   frontend      pekf_frontend_dev: raw phone events -> records; HBM-bound:
                 16 B read per event + 40 B written per record
+  frontend_then_filter   the filter over those records (pekf_run_dev with counts): the split pipeline
+  live          pekf_live_dev: the same events -> filter in one launch (no record window); 16 B read per
+                event + the state once (PEKF_AUX_ONLY=live stops after it)
   gyro_chain    pekf_gyro_chain_dev (§8f-3): 16 B read per filter-record
   wahba_stream  pekf_wahba_stream_dev (§8f-3): 24 B read + 32 B written per filter-record
   predict_dev / correct_dev   per-call operators at n = 1M items (device pointers)
@@ -154,7 +157,32 @@ def main():
                             "gbs": byts / (ms * 1e-3) / 1e9, "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM}
     log("frontend phase 2: %.2f ms" % ms)
     del ib2, tb2, sb2, rb2
-    del evb, win
+    # the filter over the front-end's records (split pipeline, second half): one multi-record launch
+    # with counts, as engine.BatchedEKF.run does for a front-end window
+    n_rec = int(counts.max())
+    f = engine.BatchedEKF(K)
+    ms_run = timed(lambda: f.run_async(win, n_rec, 0, s, None, cnt), s)
+    del f
+    res["frontend_then_filter"] = {"filters": K, "records": recs, "frontend_ms": res["frontend"]["kernel_ms"],
+                                   "filter_ms": ms_run, "total_ms": res["frontend"]["kernel_ms"] + ms_run}
+    log("split pipeline: front-end %.2f + filter %.2f ms" % (res["frontend"]["kernel_ms"], ms_run))
+    del win
+    # the same events -> filter in one launch (pekf_live_dev): 16 B read per event, the state
+    # (160 B per filter) read and written once
+    f = engine.BatchedEKF(K)
+    cnt2, refs2 = engine.DeviceBuffer(4 * K), engine.DeviceBuffer(48 * K)
+    ms = timed(lambda: f.run_events_async(evb, E, ib, tb, cnt2, refs2, 0.1, err, s), s)
+    assert np.array_equal(cnt2.download((K,), np.int32), counts)
+    byts = K * E * 16 + K * (160 + 160 + 48 + 48 + 8 + 4)
+    res["live"] = {"filters": K, "events_per_filter": E, "records": recs, "kernel_ms": ms,
+                   "events_per_s": K * E / (ms * 1e-3), "records_per_s": recs / (ms * 1e-3), "bytes": byts,
+                   "gbs": byts / (ms * 1e-3) / 1e9, "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM,
+                   "vs_split": res["frontend_then_filter"]["total_ms"] / ms}
+    log("fused front-end + filter: %.2f ms (split %.2f ms)" % (ms, res["frontend_then_filter"]["total_ms"]))
+    del f, cnt2, refs2, evb
+    if os.environ.get("PEKF_AUX_ONLY") == "live":
+        print(json.dumps(res))
+        return
 
     # ---- side outputs on a config-3-sized window
     B, W, N = 1 << 20, 1024, 10000

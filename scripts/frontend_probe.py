@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """The front-end kernel alone (the bench_aux.py workload: 16K generated event streams tiled x64 ->
-1,048,576 filters x 1,024 events), for rocprofv3 PMC passes that should see only k_frontend.
+1,048,576 filters x 1,024 events), for rocprofv3 PMC passes that should see only k_frontend; with
+--live the fused front-end + filter kernel (pekf_live_dev) on the same events instead.
 
-usage: python3 scripts/frontend_probe.py [reps]
+usage: python3 scripts/frontend_probe.py [reps] [--live]
 """
 from __future__ import annotations
 
@@ -19,7 +20,9 @@ from poseestimationkf_amd._lib import check, lib  # noqa: E402
 
 
 def main():
-    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    live = "--live" in sys.argv
+    reps = int(args[0]) if args else 3
     st = engine.Stream()
     s = st.handle
     K0, E, tile = 16384, 1024, 64
@@ -32,20 +35,25 @@ def main():
     ib = engine.DeviceBuffer(init.nbytes).upload(init)
     tb = engine.DeviceBuffer(tinit.nbytes).upload(tinit.astype(np.int64))
     r_max = E // 3 + 1
-    win = engine.IMUWindow(K, r_max)
+    win = engine.IMUWindow(K, 1 if live else r_max)
     cnt = engine.DeviceBuffer(4 * K)
     err = engine.DeviceBuffer(4).upload(np.zeros(1, np.int32))
     e0, e1 = engine.Event(), engine.Event()
     times = []
+    f = engine.BatchedEKF(K) if live else None
     for _ in range(reps):
         e0.record(s)
-        check(lib.pekf_frontend_dev(K, E, evb.ptr, ib.ptr, tb.ptr, 0.1, r_max, win.gd.ptr, win.am.ptr,
-                                    win.my.ptr, cnt.ptr, win.refs.ptr, err.ptr, s))
+        if live:
+            f.run_events_async(evb, E, ib, tb, cnt, win.refs, 0.1, err, s)
+        else:
+            check(lib.pekf_frontend_dev(K, E, evb.ptr, ib.ptr, tb.ptr, 0.1, r_max, win.gd.ptr, win.am.ptr,
+                                        win.my.ptr, cnt.ptr, win.refs.ptr, err.ptr, s))
         e1.record(s)
         e1.sync()
         times.append(e0.elapsed_ms(e1))
     recs = int(cnt.download((K,), np.int32).sum())
-    print("frontend_probe: %d filters x %d events, %d records, ms %s" % (K, E, recs, ["%.3f" % t for t in times]))
+    print("frontend_probe%s: %d filters x %d events, %d records, ms %s"
+          % (" --live" if live else "", K, E, recs, ["%.3f" % t for t in times]))
 
 
 if __name__ == "__main__":

@@ -92,6 +92,10 @@ def test_invalid_arguments_are_reported_not_crashed():
     assert st == _lib.PEKF_ERR_INVALID and "null" in _lib.last_error()
     st = _lib.lib.pekf_run_dev(4, 1, 1, 0, None, None, None, None, None, None, 1.0, 0.1, None, None, 0x4, None)
     assert st == _lib.PEKF_ERR_INVALID and "flags" in _lib.last_error()
+    st = _lib.lib.pekf_live_dev(-1, 8, None, None, None, 0.1, None, None, 1.0, 0.1, None, None, None, None)
+    assert st == _lib.PEKF_ERR_INVALID and "negative" in _lib.last_error()
+    st = _lib.lib.pekf_live_dev(4, 8, None, None, None, 0.1, None, None, 1.0, 0.1, None, None, None, None)
+    assert st == _lib.PEKF_ERR_INVALID and "null" in _lib.last_error()
     st = _lib.lib.pekf_state_layout_dev(4, None, None, None, None, 1, None)
     assert st == _lib.PEKF_ERR_INVALID and "null" in _lib.last_error()
     h = ctypes.c_void_p()

@@ -1,0 +1,121 @@
+"""The front-end fused into the filter (pekf_live_dev): raw phone events -> records ->
+Prediction + Correction in one launch, no record window.
+
+Checked two ways: bit for bit against the split pipeline it replaces (pekf_frontend_dev writing the
+records, pekf_run_dev with counts applying them), and against the oracle chain (oracle/frontend_numpy.py
+records -> the C oracle filter), whose front-end half is partly pinned (see tests/test_frontend.py)."""
+import numpy as np
+import pytest
+
+from poseestimationkf_amd import synth
+
+from .test_frontend import _events, _oracle_records
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from poseestimationkf_amd import engine
+    from poseestimationkf_amd._lib import device_count
+    assert device_count() > 0, "GPU tests need a HIP device"
+    return engine
+
+
+def _split(eng, ev, K, X0=None, P0=None):
+    win, counts = eng.run_frontend(ev)
+    f = eng.BatchedEKF(K)
+    if X0 is not None:
+        f.set_state(X0, P0)
+    if counts.max(initial=0) > 0:
+        f.run(win, n_steps=int(counts.max()))
+    X, P = f.get_state()
+    return X, P, counts, win.refs.download((K, 6), np.float64)
+
+
+def _fused(eng, ev, K, X0=None, P0=None):
+    f = eng.BatchedEKF(K)
+    if X0 is not None:
+        f.set_state(X0, P0)
+    counts, refs = f.run_events(ev)
+    X, P = f.get_state()
+    return X, P, counts, refs
+
+
+def _same(a, b):
+    for u, v in zip(a, b):
+        assert np.array_equal(u, v, equal_nan=True)
+
+
+@pytest.mark.parametrize("K,E,seed", [(1000, 1500, 21), (64, 37, 22), (4096, 300, 23)])
+def test_live_equals_split_pipeline_bit_for_bit(eng, K, E, seed):
+    """Ragged record counts, a partial last wave (K = 1000), an event count that is no multiple of the
+    ring (E = 37) and short streams where the end-of-stream drain does most of the steps."""
+    ev = synth.generate_events(np.arange(K), E, seed=seed)
+    fused, split = _fused(eng, ev, K), _split(eng, ev, K)
+    assert fused[2].min() >= 0 and fused[2].max() > 0
+    _same(fused, split)
+
+
+def test_live_continues_from_a_given_state(eng):
+    """Not from reset: random unit X and SPD P going in, as a filter resumed from a checkpoint."""
+    K, E = 512, 400
+    rng = np.random.default_rng(5)
+    X0 = rng.standard_normal((K, 4))
+    X0 /= np.linalg.norm(X0, axis=1, keepdims=True)
+    A = rng.standard_normal((K, 4, 4)) * 0.3
+    P0 = A @ A.transpose(0, 2, 1) + 0.5 * np.eye(4)
+    ev = synth.generate_events(np.arange(K), E, seed=24)
+    _same(_fused(eng, ev, K, X0, P0), _split(eng, ev, K, X0, P0))
+
+
+def test_live_vs_oracle_chain(eng, oracle_c):
+    """Each filter's own records (ragged) through the oracle front-end and the C oracle filter."""
+    K, E = 256, 1200
+    ev = synth.generate_events(np.arange(K), E, seed=25)
+    X, _, counts, refs = _fused(eng, ev, K)
+    worst = 0.0
+    for k in range(0, K, 23):
+        g, dt, a, m = _oracle_records(ev, k)
+        assert counts[k] == len(dt)
+        rec = synth.Records(g[:, None].astype(np.float32), a[:, None].astype(np.float32),
+                            m[:, None].astype(np.float32), dt[:, None].astype(np.uint32),
+                            refs[k:k + 1, :3], refs[k:k + 1, 3:])
+        Xo, _, _ = oracle_c.run(rec)
+        worst = max(worst, float(np.abs(X[k] - Xo[0]).max()))
+    print("fused events -> filter vs oracle chain: max |dq| = %.3e" % worst)
+    assert worst < 1e-9
+
+
+def test_live_streams_without_records_leave_the_state(eng):
+    K = 70
+    rng = np.random.default_rng(6)
+    X0 = rng.standard_normal((K, 4))
+    X0 /= np.linalg.norm(X0, axis=1, keepdims=True)
+    P0 = np.tile(np.eye(4) * 0.7, (K, 1, 1))
+    for spec in ([], [(synth.EV_ACC, 10), (synth.EV_MAG, 10)] * 5,
+                 [(synth.EV_GYRO, 10), (synth.EV_ACC, 10), (synth.EV_GYRO, 10)] * 3):
+        X, P, counts, _ = _fused(eng, _events(K, spec), K, X0, P0)
+        assert np.all(counts == 0)
+        assert np.array_equal(X, X0) and np.array_equal(P, P0)
+
+
+def test_live_lockstep_streams(eng):
+    """Every lane completes its records on the same events (one record per 3 events: the densest
+    stream, so every block pushes the most records a queue must hold)."""
+    K = 192
+    spec = [(synth.EV_GYRO, 1000), (synth.EV_ACC, 1000), (synth.EV_MAG, 1000)] * 40
+    ev = _events(K, spec)
+    fused = _fused(eng, ev, K)
+    assert np.all(fused[2] == 40)
+    _same(fused, _split(eng, ev, K))
+
+
+def test_live_reports_a_dt_past_31_bits(eng):
+    K = 4
+    g = (1 << 30) - 1
+    spec = [(synth.EV_GYRO, g), (synth.EV_GYRO, g), (synth.EV_GYRO, g), (synth.EV_ACC, 10), (synth.EV_MAG, 10)]
+    with pytest.raises(ValueError, match="31-bit"):
+        eng.BatchedEKF(K).run_events(_events(K, spec))
+    with pytest.raises(ValueError, match="FP64 filter on AoS"):
+        eng.BatchedEKF(K, layout="soa").run_events(_events(K, spec))
