@@ -42,11 +42,16 @@ __device__ __forceinline__ V3 normalised(const V3 &v) {
     return {v.x * in, v.y * in, v.z * in};
 }
 
+// Samples are f32 values, so the state machine moves them as f32 (one select per component instead
+// of two, no conversions per event); they are widened only when a record is emitted.  acc_0 / mag_0
+// start as the phase-2 means (FP64, not f32 values): a flag says a slot still holds the mean.
 struct Phase3 {
     // phase-2 state: acc_0 / mag_0 = raw means at the initialisation time (Parser.cpp:44-53)
-    V3 acc0, mag0;
+    V3 mean_acc, mean_mag;
+    F3 acc0, mag0;
+    bool acc0_mean, mag0_mean;  // acc_0 / mag_0 is still the phase-2 mean
     double t_acc0, t_mag0, prev_t, t;
-    V3 acc1, mag1;  // sensor samples (exact f32 values, kept widened)
+    F3 acc1, mag1;
     F3 gyro;
     double t_acc1, t_mag1, t_gyro;
     bool gyro_set, acc1_set, mag1_set;
@@ -62,15 +67,17 @@ struct Phase3 {
     // differences are formed at emission, exactly as lerp_to would form them.
     bool pend;
     F3 p_gyro;
-    V3 p_acc0, p_mag0, p_acc1, p_mag1;
+    F3 p_acc0, p_mag0, p_acc1, p_mag1;
+    bool p_acc0_mean, p_mag0_mean;
     double p_dt, p_an, p_ad, p_mn, p_md;  // dt, acc / mag lerp num and den
 
     __device__ __forceinline__ void start(const double *init6, int64_t t_start, double a) {
-        acc0 = {init6[0], init6[1], init6[2]};
-        mag0 = {init6[3], init6[4], init6[5]};
+        mean_acc = {init6[0], init6[1], init6[2]};
+        mean_mag = {init6[3], init6[4], init6[5]};
+        acc0 = mag0 = acc1 = mag1 = gyro = {0, 0, 0};
+        acc0_mean = mag0_mean = true;
         t = t_acc0 = t_mag0 = prev_t = (double)t_start;
-        acc1 = mag1 = lpf_acc = lpf_mag = {0, 0, 0};
-        gyro = {0, 0, 0};
+        lpf_acc = lpf_mag = {0, 0, 0};
         t_acc1 = t_mag1 = t_gyro = 0;
         gyro_set = acc1_set = mag1_set = false;
         alpha = a;
@@ -78,13 +85,14 @@ struct Phase3 {
         pend = false;
         p_gyro = {0, 0, 0};
         p_acc0 = p_mag0 = p_acc1 = p_mag1 = {0, 0, 0};
+        p_acc0_mean = p_mag0_mean = true;
         p_dt = p_an = p_mn = 0;
         p_ad = p_md = 1;
     }
 
     // the filter's reference vectors: the normalised phase-2 means (Parser.cpp:48-49); call after start
     __device__ __forceinline__ void refs(double (&r)[6]) const {
-        const V3 a = normalised(acc0), m = normalised(mag0);
+        const V3 a = normalised(mean_acc), m = normalised(mean_mag);
         r[0] = a.x; r[1] = a.y; r[2] = a.z;
         r[3] = m.x; r[4] = m.y; r[5] = m.z;
     }
@@ -102,11 +110,11 @@ struct Phase3 {
         t += (double)(word >> 2);
         const bool isA = ty == kEvAcc, isM = ty == kEvMag, isG = ty == kEvGyro;
         const bool gs = gyro_set;
-        const double vx = v4.x, vy = v4.y, vz = v4.z;
+        const F3 v = {v4.x, v4.y, v4.z};
         const bool wA1 = isA && gs, wM1 = isM && gs;
-        acc1 = sel(wA1, V3{vx, vy, vz}, acc1);
+        acc1 = sel(wA1, v, acc1);
         t_acc1 = wA1 ? t : t_acc1;
-        mag1 = sel(wM1, V3{vx, vy, vz}, mag1);
+        mag1 = sel(wM1, v, mag1);
         t_mag1 = wM1 ? t : t_mag1;
         const bool a1s = wA1 || (acc1_set && !(isG && gs)), m1s = wM1 || (mag1_set && !(isG && gs));
         const bool sA = isG && gs && acc1_set, sM = isG && gs && mag1_set;  // gyro shift
@@ -117,17 +125,19 @@ struct Phase3 {
             asm volatile("");  // keeps this a branch: masked 64-bit moves, not two selects per double
             pend = true;
             p_gyro = gyro; p_dt = t_gyro - prev_t;
-            p_acc0 = acc0; p_acc1 = acc1; p_an = t_gyro - t_acc0; p_ad = t_acc1 - t_acc0;
-            p_mag0 = mag0; p_mag1 = mag1; p_mn = t_gyro - t_mag0; p_md = t_mag1 - t_mag0;
+            p_acc0 = acc0; p_acc0_mean = acc0_mean; p_acc1 = acc1; p_an = t_gyro - t_acc0; p_ad = t_acc1 - t_acc0;
+            p_mag0 = mag0; p_mag0_mean = mag0_mean; p_mag1 = mag1; p_mn = t_gyro - t_mag0; p_md = t_mag1 - t_mag0;
             prev_t = t_gyro;
         }
         const bool wA0 = isA && !gs, wM0 = isM && !gs;
         const bool cA = sA || done, cM = sM || done;  // acc_0 <- acc_1 (shift or after a record)
-        acc0 = sel(wA0, V3{vx, vy, vz}, sel(cA, acc1, acc0));
+        acc0 = sel(wA0, v, sel(cA, acc1, acc0));
+        acc0_mean = acc0_mean && !wA0 && !cA;
         t_acc0 = wA0 ? t : (cA ? t_acc1 : t_acc0);
-        mag0 = sel(wM0, V3{vx, vy, vz}, sel(cM, mag1, mag0));
+        mag0 = sel(wM0, v, sel(cM, mag1, mag0));
+        mag0_mean = mag0_mean && !wM0 && !cM;
         t_mag0 = wM0 ? t : (cM ? t_mag1 : t_mag0);
-        gyro = sel(isG, F3{v4.x, v4.y, v4.z}, gyro);
+        gyro = sel(isG, v, gyro);
         t_gyro = isG ? t : t_gyro;
         gyro_set = (gs || isG) && !done;
         acc1_set = a1s && !done;
@@ -143,11 +153,10 @@ struct Phase3 {
         // division taken as one reciprocal.  Timestamps are integer ns held in doubles (exact below
         // 2^53), so t3 - t1 and t2 - t1 are the exact differences (double)t3 - (double)t1 gives.
         const double fa = p_an * recip<true>(p_ad), fm = p_mn * recip<true>(p_md);
-        const V3 a1 = p_acc1, m1 = p_mag1;
-        const V3 a = normalised({(a1.x - p_acc0.x) * fa + p_acc0.x, (a1.y - p_acc0.y) * fa + p_acc0.y,
-                                 (a1.z - p_acc0.z) * fa + p_acc0.z});
-        const V3 m = normalised({(m1.x - p_mag0.x) * fm + p_mag0.x, (m1.y - p_mag0.y) * fm + p_mag0.y,
-                                 (m1.z - p_mag0.z) * fm + p_mag0.z});
+        const V3 a0 = sel(p_acc0_mean, mean_acc, widen(p_acc0)), a1 = widen(p_acc1);
+        const V3 m0 = sel(p_mag0_mean, mean_mag, widen(p_mag0)), m1 = widen(p_mag1);
+        const V3 a = normalised({(a1.x - a0.x) * fa + a0.x, (a1.y - a0.y) * fa + a0.y, (a1.z - a0.z) * fa + a0.z});
+        const V3 m = normalised({(m1.x - m0.x) * fm + m0.x, (m1.y - m0.y) * fm + m0.y, (m1.z - m0.z) * fm + m0.z});
         lpf_mag = {alpha * m.x + beta * lpf_mag.x, alpha * m.y + beta * lpf_mag.y, alpha * m.z + beta * lpf_mag.z};
         lpf_acc = {alpha * a.x + beta * lpf_acc.x, alpha * a.y + beta * lpf_acc.y, alpha * a.z + beta * lpf_acc.z};
         if (!(p_dt >= 0.0 && p_dt < 2147483648.0)) bad |= 1;
