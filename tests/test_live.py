@@ -119,3 +119,17 @@ def test_live_reports_a_dt_past_31_bits(eng):
         eng.BatchedEKF(K).run_events(_events(K, spec))
     with pytest.raises(ValueError, match="FP64 filter on AoS"):
         eng.BatchedEKF(K, layout="soa").run_events(_events(K, spec))
+
+
+def test_live_full_batch_equals_split(eng):
+    """1,048,576 filters (16,384 generated event streams tiled x64) x 192 events: every filter's
+    final state, count and reference pair equal the split pipeline's bit for bit at full scale."""
+    K0, E, tile = 16384, 192, 64
+    ev0 = synth.generate_events(np.arange(K0), E, seed=26)
+    ev = dict(types=np.tile(ev0["types"], (1, tile)), values=np.tile(ev0["values"], (1, tile, 1)),
+              times=np.tile(ev0["times"], (1, tile)), init_acc=np.tile(ev0["init_acc"], (tile, 1)),
+              init_mag=np.tile(ev0["init_mag"], (tile, 1)), t_init=np.tile(ev0["t_init"], tile))
+    K = K0 * tile
+    fused, split = _fused(eng, ev, K), _split(eng, ev, K)
+    assert fused[2].sum() > 10 * K
+    _same(fused, split)
