@@ -26,8 +26,10 @@ namespace pekf {
 
 // Tuned on the box (scripts/ab_live.sh, profiles/r2/live/): the kernel is register-bound -- front-end
 // state, filter state and a filter step's temporaries -- so the record queue lives in LDS and the
-// launch is held to 2 waves per SIMD (256 registers; a few spills) with a 3-event ring: 5.7 ms at
-// 1M filters x 1,024 events, against 8.7 ms for 6 events and the queue in registers at 1 wave/SIMD.
+// launch is held to 2 waves per SIMD (252 registers) with a 3-event ring: 5.5 ms at 1M filters x
+// 1,024 events, against 8.7 ms for 6 events and the queue in registers at 1 wave/SIMD.  Queueing the
+// records' raw inputs instead (emit moved into the filter step, 104 B per slot, 3 deep) was slower:
+// 5.9 ms (profiles/r2/live/variants/raw_queue.log).
 #ifndef PEKF_LIVE_RING
 #define PEKF_LIVE_RING 3  // event rows in flight per lane; a filter step may run after each block of them
 #endif

@@ -42,6 +42,16 @@ __device__ __forceinline__ V3 normalised(const V3 &v) {
     return {v.x * in, v.y * in, v.z * in};
 }
 
+// A completed record's inputs, captured when the state machine completes it (its state moves on at
+// once) and turned into the record by Phase3::emit: the gyro sample, acc_0 / acc_1 / mag_0 / mag_1
+// (f32 samples; *_mean: acc_0 / mag_0 is still the phase-2 mean) and the time differences of
+// LinearInterpolationSensor and of the record's dt.
+struct RawRec {
+    F3 gyro, acc0, acc1, mag0, mag1;
+    bool acc0_mean, mag0_mean;
+    double dt, an, ad, mn, md;  // dt, acc / mag lerp num and den
+};
+
 // Samples are f32 values, so the state machine moves them as f32 (one select per component instead
 // of two, no conversions per event); they are widened only when a record is emitted.  acc_0 / mag_0
 // start as the phase-2 means (FP64, not f32 values): a flag says a slot still holds the mean.
@@ -58,18 +68,15 @@ struct Phase3 {
     V3 lpf_acc, lpf_mag;
     double alpha, beta;
 
-    // Emission is deferred: when a lane completes a record, only its inputs are copied aside
-    // (pend), and the expensive part -- two interpolations with a reciprocal, two normalisations
-    // with an rsqrt, the low-pass and the f32 packing (emit) -- runs for the whole wave once every
-    // few events instead of on every event some lane completes one (which, with 64 lanes, is nearly
-    // every event).  A lane needs at least 3 events (gyro, acc, mag) between two records, so when
-    // emit runs every 3 events it never has two pending.  Arithmetic is unchanged: the time
-    // differences are formed at emission, exactly as lerp_to would form them.
+    // Emission is deferred: when a lane completes a record, only its inputs are captured (RawRec),
+    // and the expensive part -- two interpolations with a reciprocal, two normalisations with an
+    // rsqrt, the low-pass and the f32 packing (emit) -- runs for the whole wave later, not on every
+    // event some lane completes one (which, with 64 lanes, is nearly every event).  The deferring
+    // form of event() keeps one captured record in p (pend): a lane needs at least 3 events (gyro,
+    // acc, mag) between two records, so when emit runs every 3 events it never has two pending.
+    // Arithmetic is unchanged: the time differences are formed at capture, exactly as lerp_to would.
     bool pend;
-    F3 p_gyro;
-    F3 p_acc0, p_mag0, p_acc1, p_mag1;
-    bool p_acc0_mean, p_mag0_mean;
-    double p_dt, p_an, p_ad, p_mn, p_md;  // dt, acc / mag lerp num and den
+    RawRec p;
 
     __device__ __forceinline__ void start(const double *init6, int64_t t_start, double a) {
         mean_acc = {init6[0], init6[1], init6[2]};
@@ -83,11 +90,10 @@ struct Phase3 {
         alpha = a;
         beta = 1.0 - a;
         pend = false;
-        p_gyro = {0, 0, 0};
-        p_acc0 = p_mag0 = p_acc1 = p_mag1 = {0, 0, 0};
-        p_acc0_mean = p_mag0_mean = true;
-        p_dt = p_an = p_mn = 0;
-        p_ad = p_md = 1;
+        p.gyro = p.acc0 = p.mag0 = p.acc1 = p.mag1 = {0, 0, 0};
+        p.acc0_mean = p.mag0_mean = true;
+        p.dt = p.an = p.mn = 0;
+        p.ad = p.md = 1;
     }
 
     // the filter's reference vectors: the normalised phase-2 means (Parser.cpp:48-49); call after start
@@ -103,7 +109,9 @@ struct Phase3 {
     //   before a gyro sample: acc -> acc_0, mag -> mag_0, gyro -> gyro (gyro_is_set);
     //   after it: acc -> acc_1, mag -> mag_1 (set); a new gyro replaces the gyro and shifts a set
     //   acc_1 -> acc_0 / mag_1 -> mag_0, clearing both flags.
-    __device__ __forceinline__ void event(const float4 v4) {
+    // on_done(const RawRec &) runs for a lane whose event completes a record.
+    template <typename F>
+    __device__ __forceinline__ void event(const float4 v4, F &&on_done) {
 #pragma clang fp contract(fast)
         const uint32_t word = __float_as_uint(v4.w);
         const uint32_t ty = word & 3u;
@@ -119,14 +127,15 @@ struct Phase3 {
         const bool a1s = wA1 || (acc1_set && !(isG && gs)), m1s = wM1 || (mag1_set && !(isG && gs));
         const bool sA = isG && gs && acc1_set, sM = isG && gs && mag1_set;  // gyro shift
         // ExecuteKalmanFilter (Parser.cpp:229-257) once acc_1 and mag_1 are both set: record its
-        // inputs (pending until the next emit), then acc_0 <- acc_1, mag_0 <- mag_1, flags cleared
+        // inputs, then acc_0 <- acc_1, mag_0 <- mag_1, flags cleared
         const bool done = a1s && m1s;
         if (done) {
             asm volatile("");  // keeps this a branch: masked 64-bit moves, not two selects per double
-            pend = true;
-            p_gyro = gyro; p_dt = t_gyro - prev_t;
-            p_acc0 = acc0; p_acc0_mean = acc0_mean; p_acc1 = acc1; p_an = t_gyro - t_acc0; p_ad = t_acc1 - t_acc0;
-            p_mag0 = mag0; p_mag0_mean = mag0_mean; p_mag1 = mag1; p_mn = t_gyro - t_mag0; p_md = t_mag1 - t_mag0;
+            RawRec r;
+            r.gyro = gyro; r.dt = t_gyro - prev_t;
+            r.acc0 = acc0; r.acc0_mean = acc0_mean; r.acc1 = acc1; r.an = t_gyro - t_acc0; r.ad = t_acc1 - t_acc0;
+            r.mag0 = mag0; r.mag0_mean = mag0_mean; r.mag1 = mag1; r.mn = t_gyro - t_mag0; r.md = t_mag1 - t_mag0;
+            on_done(r);
             prev_t = t_gyro;
         }
         const bool wA0 = isA && !gs, wM0 = isM && !gs;
@@ -144,25 +153,36 @@ struct Phase3 {
         mag1_set = m1s && !done;
     }
 
-    // The pending record (call only when pend): interpolation, normalisation, low-pass, f32 packing.
-    // bad |= 1 if its dt does not fit the 31-bit dt word of the stream.
+    // the deferring form: the completed record's inputs wait in p (pend) for emit(bad)
+    __device__ __forceinline__ void event(const float4 v4) {
+        event(v4, [&](const RawRec &r) {
+            pend = true;
+            p = r;
+        });
+    }
     __device__ __forceinline__ Rec emit(int &bad) {
-#pragma clang fp contract(fast)
         pend = false;
+        return emit(p, bad);
+    }
+
+    // A captured record, in the order they complete: interpolation, normalisation, low-pass, f32
+    // packing.  bad |= 1 if its dt does not fit the 31-bit dt word of the stream.
+    __device__ __forceinline__ Rec emit(const RawRec &q, int &bad) {
+#pragma clang fp contract(fast)
         // Parser::LinearInterpolationSensor (:259-267): (y2 - y1) / (t2 - t1) * (t3 - t1) + y1, the
         // division taken as one reciprocal.  Timestamps are integer ns held in doubles (exact below
         // 2^53), so t3 - t1 and t2 - t1 are the exact differences (double)t3 - (double)t1 gives.
-        const double fa = p_an * recip<true>(p_ad), fm = p_mn * recip<true>(p_md);
-        const V3 a0 = sel(p_acc0_mean, mean_acc, widen(p_acc0)), a1 = widen(p_acc1);
-        const V3 m0 = sel(p_mag0_mean, mean_mag, widen(p_mag0)), m1 = widen(p_mag1);
+        const double fa = q.an * recip<true>(q.ad), fm = q.mn * recip<true>(q.md);
+        const V3 a0 = sel(q.acc0_mean, mean_acc, widen(q.acc0)), a1 = widen(q.acc1);
+        const V3 m0 = sel(q.mag0_mean, mean_mag, widen(q.mag0)), m1 = widen(q.mag1);
         const V3 a = normalised({(a1.x - a0.x) * fa + a0.x, (a1.y - a0.y) * fa + a0.y, (a1.z - a0.z) * fa + a0.z});
         const V3 m = normalised({(m1.x - m0.x) * fm + m0.x, (m1.y - m0.y) * fm + m0.y, (m1.z - m0.z) * fm + m0.z});
         lpf_mag = {alpha * m.x + beta * lpf_mag.x, alpha * m.y + beta * lpf_mag.y, alpha * m.z + beta * lpf_mag.z};
         lpf_acc = {alpha * a.x + beta * lpf_acc.x, alpha * a.y + beta * lpf_acc.y, alpha * a.z + beta * lpf_acc.z};
-        if (!(p_dt >= 0.0 && p_dt < 2147483648.0)) bad |= 1;
+        if (!(q.dt >= 0.0 && q.dt < 2147483648.0)) bad |= 1;
         Rec r;
-        r.gd = make_float4((float)p_gyro.x, (float)p_gyro.y, (float)p_gyro.z,
-                           __uint_as_float((uint32_t)fmin(fmax(p_dt, 0.0), 2147483647.0)));
+        r.gd = make_float4((float)q.gyro.x, (float)q.gyro.y, (float)q.gyro.z,
+                           __uint_as_float((uint32_t)fmin(fmax(q.dt, 0.0), 2147483647.0)));
         r.am = make_float4((float)lpf_acc.x, (float)lpf_acc.y, (float)lpf_acc.z, (float)lpf_mag.x);
         r.my = make_float2((float)lpf_mag.y, (float)lpf_mag.z);
         return r;
