@@ -304,13 +304,23 @@ __device__ __forceinline__ void from_ref_basis(const RW &Wr, double *x, Sym4T<PT
     P = sym_rotate<false>(qw, P);
 }
 
+// Occupancy target of k_run in waves per SIMD (0: the compiler's choice)
+#ifndef PEKF_RUN_WAVES
+#define PEKF_RUN_WAVES 0
+#endif
+#if PEKF_RUN_WAVES
+#define PEKF_RUN_ATTR __attribute__((amdgpu_waves_per_eu(PEKF_RUN_WAVES)))
+#else
+#define PEKF_RUN_ATTR
+#endif
+
 // MIXED = false: every operation in FP64 (the headline path).
 // MIXED = true (opt-in, PEKF_RUN_MIXED_PRECISION): the covariance recursion (P-, S^-1, K, P)
 // in FP32 while RK4, Wahba, R->q and the X update stay FP64 (~2e-8 vs FP64).
 // COUNTS: filter b applies only its first counts[b] records of the launch (a separate
 // instantiation so the uniform-length path carries no per-step lane predicate).
 template <bool TRAJ, bool MIXED, bool SOA, bool COUNTS, bool ONE>
-__global__ __launch_bounds__(kRunBlock) void k_run(int64_t batch, int64_t n_steps, int64_t window,
+__global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run(int64_t batch, int64_t n_steps, int64_t window,
                                                    int64_t step0, const float4 *__restrict__ gd,
                                                    const float4 *__restrict__ am,
                                                    const float2 *__restrict__ my,
