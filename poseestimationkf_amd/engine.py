@@ -293,6 +293,35 @@ def frontend_init(ev, n_avg=100):
                 var_mag=st[:, 6:9], var_gyro=st[:, 9:12])
 
 
+def run_session(phase2, phase3, filters, n_avg=100, alpha=0.1):
+    """A whole client session of the server on the device (KFS/Parser.cpp:28-72): phase-2 events ->
+    initial means and start time (pekf_frontend_init_dev) -> phase-3 events -> records -> the filters'
+    state (pekf_live_dev), the phase-2 results handed over in device memory.  phase3's times continue
+    phase2's (its first gap is taken from phase2's last event, the time phase 3 starts from).
+    filters: a BatchedEKF (FP64, AoS) whose state is advanced.  Returns dict(ready (K,) bool -- a filter
+    that never finished phase 2 has NaN references and state --, counts (K,) records applied,
+    refs (K, 6))."""
+    K = filters.batch
+    p2 = synth.pack_events(phase2)
+    E2 = p2.shape[0]
+    assert p2.shape[1] == K and E2 > 0
+    t_last = np.asarray(phase2["times"], np.int64)[-1]
+    p3 = synth.pack_events(dict(phase3, t_init=t_last))
+    assert p3.shape[1] == K
+    ev2, ev3 = DeviceBuffer(p2.nbytes).upload(p2), DeviceBuffer(p3.nbytes).upload(p3)
+    tsb = DeviceBuffer(8 * K).upload(np.ascontiguousarray(phase2["t_init"], np.int64))
+    ib, tib, rb = DeviceBuffer(48 * K), DeviceBuffer(8 * K), DeviceBuffer(4 * K)
+    check(lib.pekf_frontend_init_dev(K, E2, ev2.ptr, tsb.ptr, int(n_avg), ib.ptr, tib.ptr, None, rb.ptr, None))
+    cnt, refs = DeviceBuffer(4 * K), DeviceBuffer(48 * K)
+    errb = DeviceBuffer(4).upload(np.zeros(1, np.int32))
+    filters.run_events_async(ev3, p3.shape[0], ib, tib, cnt, refs, alpha, errb)
+    check(lib.pekf_device_sync())
+    if int(errb.download((1,), np.int32)[0]) & 1:
+        raise ValueError("a record's dt does not fit the 31-bit ns field of the stream")
+    return dict(ready=rb.download((K,), np.int32).astype(bool), counts=cnt.download((K,), np.int32),
+                refs=refs.download((K, 6), np.float64))
+
+
 # ------------------------------------------------------------------ the batched filter
 
 class BatchedEKF:

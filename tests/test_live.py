@@ -133,3 +133,20 @@ def test_live_full_batch_equals_split(eng):
     fused, split = _fused(eng, ev, K), _split(eng, ev, K)
     assert fused[2].sum() > 10 * K
     _same(fused, split)
+
+
+def test_session_phase2_then_fused_phase3(eng):
+    """engine.run_session (phase 2 on the device, its means and time handed to pekf_live_dev in device
+    memory) equals frontend_init -> run_frontend -> BatchedEKF.run bit for bit."""
+    K = 320
+    ph2 = synth.generate_events(np.arange(K), 800, seed=33)
+    ph3 = synth.generate_events(np.arange(K), 500, seed=34)
+    ph3 = dict(ph3, times=ph3["times"] - ph3["t_init"][None, :] + ph2["times"][-1][None, :])
+    f = eng.BatchedEKF(K)
+    got = eng.run_session(ph2, ph3, f)
+    assert got["ready"].all()
+    ini = eng.frontend_init(ph2)
+    assert np.array_equal(ini["t_init"], ph2["times"][-1])
+    split = _split(eng, dict(ph3, t_init=ini["t_init"], init_acc=ini["init"][:, :3], init_mag=ini["init"][:, 3:]), K)
+    X, P = f.get_state()
+    _same((X, P, got["counts"], got["refs"]), split)
