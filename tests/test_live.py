@@ -150,3 +150,24 @@ def test_session_phase2_then_fused_phase3(eng):
     split = _split(eng, dict(ph3, t_init=ini["t_init"], init_acc=ini["init"][:, :3], init_mag=ini["init"][:, 3:]), K)
     X, P = f.get_state()
     _same((X, P, got["counts"], got["refs"]), split)
+
+
+def test_live_dense_jittered_streams(eng):
+    """Records every 3-6 events at lane-dependent positions (each group of three events a random
+    permutation of gyro / acc / mag): the queues fill fastest and the overflow rule decides most
+    filter steps."""
+    K, G = 448, 200
+    rng = np.random.default_rng(35)
+    perms = np.array([[0, 1, 2], [0, 2, 1], [1, 0, 2], [1, 2, 0], [2, 0, 1], [2, 1, 0]])
+    kinds = np.array([synth.EV_GYRO, synth.EV_ACC, synth.EV_MAG], np.uint32)
+    types = kinds[perms[rng.integers(0, 6, size=(G, K))]].transpose(0, 2, 1).reshape(3 * G, K)
+    E = 3 * G
+    gaps = rng.integers(1_000_000, 3_000_000, size=(E, K))
+    times = synth.T_INIT_NS + np.cumsum(gaps, axis=0)
+    vals = rng.standard_normal((E, K, 3)).astype(np.float32)
+    vals[..., 2] += np.where(types == synth.EV_ACC, 9.8, 0.0).astype(np.float32)
+    ev = dict(types=types, values=vals, times=times, init_acc=np.tile([0.1, 0.2, 9.8], (K, 1)),
+              init_mag=np.tile([20.0, 1.0, -40.0], (K, 1)), t_init=np.full(K, synth.T_INIT_NS, np.int64))
+    fused = _fused(eng, ev, K)
+    assert fused[2].min() >= G // 2 and fused[2].max() <= G
+    _same(fused, _split(eng, ev, K))
