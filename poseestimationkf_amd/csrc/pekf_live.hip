@@ -39,67 +39,15 @@ namespace pekf {
 #ifndef PEKF_LIVE_QUORUM
 #define PEKF_LIVE_QUORUM 56  // lanes of 64 with a queued record that trigger a filter step
 #endif
-#ifndef PEKF_LIVE_LDS_QUEUE
-#define PEKF_LIVE_LDS_QUEUE 1  // 0: the queue in registers (RecordQueue)
-#endif
 #ifndef PEKF_LIVE_ATTR
 #define PEKF_LIVE_ATTR __attribute__((amdgpu_waves_per_eu(2)))
 #endif
 
-// component-wise c ? a : b of a record (a struct-valued ?: would go through scratch memory)
-__device__ __forceinline__ Rec sel(bool c, const Rec &a, const Rec &b) {
-    Rec o;
-    o.gd = make_float4(c ? a.gd.x : b.gd.x, c ? a.gd.y : b.gd.y, c ? a.gd.z : b.gd.z, c ? a.gd.w : b.gd.w);
-    o.am = make_float4(c ? a.am.x : b.am.x, c ? a.am.y : b.am.y, c ? a.am.z : b.am.z, c ? a.am.w : b.am.w);
-    o.my = make_float2(c ? a.my.x : b.my.x, c ? a.my.y : b.my.y);
-    return o;
-}
-
-// A lane's records waiting for the wave's next filter step, oldest first, in registers: slots are
-// separate variables (an array, even statically indexed, was left in scratch) and a push selects
-// its slot.
-template <int Q>
-struct RecQueue;
-template <>
-struct RecQueue<0> {
-    __device__ __forceinline__ void put(int, const Rec &) {}
-    __device__ __forceinline__ void shift(Rec &) {}
-};
-template <int Q>
-struct RecQueue {
-    Rec head;
-    RecQueue<Q - 1> tail;
-    // slot i (0 = oldest) takes r
-    __device__ __forceinline__ void put(int i, const Rec &r) {
-        head = sel(i == 0, r, head);
-        tail.put(i - 1, r);
-    }
-    // every slot moves up one (slot 0 into `out`)
-    __device__ __forceinline__ void shift(Rec &out) {
-        out = head;
-        tail.shift(head);
-    }
-};
-template <int Q>
-struct RecordQueue {
-    RecQueue<Q> slots;
-    int n = 0;
-    __device__ __forceinline__ void push(const Rec &r) {
-        slots.put(n, r);
-        ++n;
-    }
-    // the oldest record (meaningful when n > 0)
-    __device__ __forceinline__ Rec pop() {
-        Rec r;
-        slots.shift(r);
-        n = n > 0 ? n - 1 : 0;
-        return r;
-    }
-};
-
-// The same queue in LDS: a ring of Q slots per lane, [slot][lane] so that a wave's accesses fall in
-// distinct banks whatever slot each lane is at.  A push or pop is a few address operations and three
-// LDS accesses instead of selects / moves over every slot, and the records' registers are free.
+// A lane's records waiting for the wave's next filter step, oldest first: a ring of Q slots per lane in
+// LDS, [slot][lane] so that a wave's accesses fall in distinct banks whatever slot each lane is at.  A
+// push or pop is a few address operations and three LDS accesses.  (Held in registers -- slots as
+// separate variables, a push selecting its slot -- the queue cost 40 selects per push and registers
+// the kernel does not have: profiles/r2/live/variants/live_ab*.log.)
 template <int Q>
 struct LdsQueue {
     float4 (*gd)[kRunBlock];
@@ -123,11 +71,10 @@ struct LdsQueue {
     }
 };
 
-__global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(int64_t batch, int64_t n_events, const float4 *__restrict__ ev,
-                                                    const double *__restrict__ init, const int64_t *__restrict__ t_init,
-                                                    double alpha, double qs, double rs, double *__restrict__ Xio,
-                                                    double *__restrict__ Pio, int32_t *__restrict__ counts,
-                                                    double *__restrict__ refs, int *__restrict__ err) {
+__global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
+    int64_t batch, int64_t n_events, const float4 *__restrict__ ev, const double *__restrict__ init,
+    const int64_t *__restrict__ t_init, double alpha, double qs, double rs, double *__restrict__ Xio,
+    double *__restrict__ Pio, int32_t *__restrict__ counts, double *__restrict__ refs, int *__restrict__ err) {
     constexpr int kRing = PEKF_LIVE_RING, kFlush = 3, kQueue = PEKF_LIVE_QUEUE, kQuorum = PEKF_LIVE_QUORUM;
     constexpr int kPush = kRing / kFlush;  // records a lane can complete within one block
     static_assert(kRing % kFlush == 0, "the ring depth must be a multiple of the emit period");
@@ -158,14 +105,10 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(int64_t batch
     }
     const StepK<double> kc = step_consts<double, true>(qs, rs);
 
-#if PEKF_LIVE_LDS_QUEUE
     __shared__ float4 q_gd[kQueue][kRunBlock], q_am[kQueue][kRunBlock];
     __shared__ float2 q_my[kQueue][kRunBlock];
     LdsQueue<kQueue> queue;
     queue.gd = q_gd; queue.am = q_am; queue.my = q_my;
-#else
-    RecordQueue<kQueue> queue;
-#endif
     int32_t applied = 0;
     int bad = 0;
     // One filter step for every lane with a queued record: its oldest, Prediction + Correction with
