@@ -113,11 +113,4 @@ int launch_run_multi(int64_t batch, int64_t n_steps, int64_t window, int64_t ste
                      const float4 *am, const float2 *my, const double *refs, double *X, double *P, double q,
                      double r, double *traj, const int32_t *counts, bool mixed, bool soa, hipStream_t stream);
 
-// Small-batch multi-record launch (pekf_run_split.hip): measurement + filter waves per 64 filters,
-// bit-identical to k_run<false, false, SOA, false, false>; run_split_wanted decides (PEKF_RUN_SPLIT).
-bool run_split_wanted(int64_t batch);
-int launch_run_split(int64_t batch, int64_t n_steps, int64_t window, int64_t step0, const float4 *gd,
-                     const float4 *am, const float2 *my, const double *refs, double *X, double *P, double q,
-                     double r, bool soa, hipStream_t stream);
-
 }  // namespace pekf

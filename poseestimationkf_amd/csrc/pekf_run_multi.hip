@@ -14,9 +14,6 @@ namespace pekf {
 int launch_run_multi(int64_t batch, int64_t n_steps, int64_t window, int64_t step0, const float4 *gd,
                      const float4 *am, const float2 *my, const double *refs, double *X, double *P, double q,
                      double r, double *traj, const int32_t *counts, bool mixed, bool soa, hipStream_t stream) {
-    // small batches: measurement and filter waves (pekf_run_split.hip), bit-identical
-    if (!traj && !counts && !mixed && run_split_wanted(batch))
-        return launch_run_split(batch, n_steps, window, step0, gd, am, my, refs, X, P, q, r, soa, stream);
     const dim3 grid(grid_for(batch, kRunBlock)), block(kRunBlock);
 #define PEKF_LAUNCH_RUN(TR, MX, SO, CN)                                                                      \
     hipLaunchKernelGGL((k_run<TR, MX, SO, CN, false>), grid, block, 0, stream, batch, n_steps, window, step0, gd, \
