@@ -493,9 +493,13 @@ PEKF_DEV void quat_to_rotm(const double *q, double *M) {
 // whatever formula we use: R' and numpy's SVD rotation differ in the last bits), and an exactly
 // identity world rotation -- the one input where it is deterministic (NaN) -- does not arise from
 // Fw R'.  The well-conditioned Q4 z value is returned instead.
-template <int F = 1, class RW, std::enable_if_t<RW::kRefBasis, int> = 0>
+struct NoPin {
+    PEKF_DEV void operator()() const {}
+};
+// pin(): called after v = Q4 z and before the fallback branch (see ekf_record_step's PEKF_PIN_SCHUR)
+template <int F = 1, class RW, class Pin = NoPin, std::enable_if_t<RW::kRefBasis, int> = 0>
 PEKF_DEV void wahba_quat_toward(const RW &W, const Frame &V, double ka, double km, const double *z, double *v,
-                                double &sc) {
+                                double &sc, const Pin &pin = Pin()) {
     const double kw = km * W.b2W, kb = km * W.b1W;
     double p = ka * W.aW * V.alpha + kb * V.beta1 + kw * V.beta2;
     double s = kw * V.beta1 - kb * V.beta2;
@@ -512,6 +516,7 @@ PEKF_DEV void wahba_quat_toward(const RW &W, const Frame &V, double ka, double k
     double nv, t0;
     q4_times(R, z, v, nv, t0);
     sc = rsqrt<F>(nv);
+    pin();
     if (PEKF_TAKEN(nv < 1.0, false)) {
         double Fw[9], Rw[9], zw[4], vw[4], qw[4];
         W.quat(qw);
@@ -528,9 +533,9 @@ PEKF_DEV void wahba_quat_toward(const RW &W, const Frame &V, double ka, double k
 }
 
 // Y = v * sc in the world basis (the per-record kernels)
-template <int F = 1>
+template <int F = 1, class Pin = NoPin>
 PEKF_DEV void wahba_quat_toward(const Frame &W, const Frame &V, double ka, double km, const double *z, double *v,
-                                double &sc) {
+                                double &sc, const Pin & = Pin()) {
     double R[9];
     wahba_rotation<true>(W, V, ka, km, R);
     rotm_to_quat_toward(R, z, v, sc);

@@ -194,7 +194,7 @@ __device__ __forceinline__ StepK<PT> step_consts(double qs, double rs) {
 // that form the products (omod, pekf_math.hpp) -- the gyro is never scaled to h = w/2, and the
 // Newton steps of the rsqrt seeds need no separate multiply by 1/2: 9 VALU fewer per record, the
 // same values bit for bit.
-template <typename PT, bool MC = false, bool LAZY = false, bool OM = false, typename Ref>
+template <typename PT, bool MC = false, bool LAZY = false, bool OM = false, bool PIN = false, typename Ref>
 __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> &P, const Ref &Wf, const StepK<PT> &k,
                                                 const double *gy, double dt_ns, bool missing,
                                                 const double *acc, const double *mag) {
@@ -246,7 +246,18 @@ __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> 
         // ka = |acc_z| >= 0, so wahba_sign(ka, km) is the sign of km = 1 - ka (never -0)
         make_frame<F>(acc, mag, Vf, 1.0 - ka);
         double v[4], sc;
-        wahba_quat_toward<F>(Wf, Vf, ka, 1.0 - ka, z, v, sc);  // Wahba.py:8-47 + the flip of :73-75: Y = v sc
+        // PIN: S^-1 depends only on the Prediction; have it computed before the rare fallback branch,
+        // in the basic block of the Wahba chain, so that the two independent chains interleave (left
+        // to itself the compiler sinks it past the branch, behind the Wahba chain).  Worth it where a
+        // SIMD has one wave and the record's dependency chain is exposed (config 2: -2.3 %); at 3 waves
+        // per SIMD (config 3) the other waves fill those gaps and the default order is 0.4 % faster
+        // (profiles/r2/ab_pin_schur/).  Scheduling only: the arithmetic is the same, bit for bit.
+        auto pin = [&] {
+            if constexpr (PIN && MC && OM)
+                asm volatile("" ::"v"(Si.a00), "v"(Si.a01), "v"(Si.a02), "v"(Si.a03), "v"(Si.a11), "v"(Si.a12),
+                             "v"(Si.a13), "v"(Si.a22), "v"(Si.a23), "v"(Si.a33));
+        };
+        wahba_quat_toward<F>(Wf, Vf, ka, 1.0 - ka, z, v, sc, pin);  // Wahba.py:8-47 + the flip of :73-75: Y = v sc
         // e = Y - z (MC: D e, whose last two components are z - Y)
         const PT e0 = (PT)fma_sub(v[0], sc, z[0]), e1 = (PT)fma_sub(v[1], sc, z[1]);
         const PT e2 = (PT)(MC ? fma_rsub(v[2], sc, z[2]) : fma_sub(v[2], sc, z[2]));
@@ -325,7 +336,8 @@ __device__ __forceinline__ void from_ref_basis(const RW &Wr, double *x, Sym4T<PT
 // in FP32 while RK4, Wahba, R->q and the X update stay FP64 (~2e-8 vs FP64).
 // COUNTS: filter b applies only its first counts[b] records of the launch (a separate
 // instantiation so the uniform-length path carries no per-step lane predicate).
-template <bool TRAJ, bool MIXED, bool SOA, bool COUNTS, bool ONE>
+// PIN: the small-batch schedule of the multi-record loop (ekf_record_step, launch_run_multi).
+template <bool TRAJ, bool MIXED, bool SOA, bool COUNTS, bool ONE, bool PIN = false>
 __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run(int64_t batch, int64_t n_steps, int64_t window,
                                                    int64_t step0, const float4 *__restrict__ gd,
                                                    const float4 *__restrict__ am,
@@ -420,7 +432,7 @@ __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run(int64_t batch, 
             const uint32_t word = __float_as_uint(cur.gd.w);
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
-            ekf_record_step<PT, MC, decltype(lazy)::value, MC && !MIXED>(
+            ekf_record_step<PT, MC, decltype(lazy)::value, MC && !MIXED, PIN>(
                 x, n2, P, ref, step_consts<PT, MC>(qs, rs), gy, (double)(word & 0x7FFFFFFFu),
                 (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
         }
