@@ -11,25 +11,20 @@
 
 namespace pekf {
 
-// True where the launch leaves a SIMD fewer than 2 waves (config 2: 1,024 waves on 1,024 SIMDs): there
-// the record's dependency chain is exposed and the PIN schedule of ekf_record_step is faster
-// (profiles/r2/ab_pin_schur/).  PEKF_RUN_PIN=0 / 1 forces the choice (A/B runs, tests).
-static bool small_batch_schedule(int64_t batch) {
+// The PIN schedule of ekf_record_step (the Schur inverse in the Wahba chain's basic block) for the
+// FP64 multi-record launch without trajectories or counts: config 2 (one wave per SIMD, the record's
+// dependency chain exposed) -2.3 %, config 3 unchanged within noise in an order-balanced A/B
+// (profiles/r2/ab_pin_schur/).  PEKF_RUN_PIN=0 selects the compiler's default order (A/B runs, tests).
+static bool pin_schedule() {
     const char *e = getenv("PEKF_RUN_PIN");
-    if (e && e[0] == '0') return false;
-    if (e && e[0] == '1') return true;
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-        return false;
-    return (batch + kWave - 1) / kWave < 2 * 4 * (int64_t)cus;
+    return !(e && e[0] == '0');
 }
 
 int launch_run_multi(int64_t batch, int64_t n_steps, int64_t window, int64_t step0, const float4 *gd,
                      const float4 *am, const float2 *my, const double *refs, double *X, double *P, double q,
                      double r, double *traj, const int32_t *counts, bool mixed, bool soa, hipStream_t stream) {
     const dim3 grid(grid_for(batch, kRunBlock)), block(kRunBlock);
-    if (!traj && !mixed && !counts && small_batch_schedule(batch)) {
+    if (!traj && !mixed && !counts && pin_schedule()) {
         if (soa)
             hipLaunchKernelGGL((k_run<false, false, true, false, false, true>), grid, block, 0, stream, batch, n_steps,
                                window, step0, gd, am, my, refs, X, P, q, r, traj, counts);

@@ -249,8 +249,8 @@ __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> 
         // PIN: S^-1 depends only on the Prediction; have it computed before the rare fallback branch,
         // in the basic block of the Wahba chain, so that the two independent chains interleave (left
         // to itself the compiler sinks it past the branch, behind the Wahba chain).  Worth it where a
-        // SIMD has one wave and the record's dependency chain is exposed (config 2: -2.3 %); at 3 waves
-        // per SIMD (config 3) the other waves fill those gaps and the default order is 0.4 % faster
+        // SIMD has one wave and the record's dependency chain is exposed (config 2: -2.3 %); neutral at
+        // 3 waves per SIMD (config 3), where the other waves fill those gaps anyway
         // (profiles/r2/ab_pin_schur/).  Scheduling only: the arithmetic is the same, bit for bit.
         auto pin = [&] {
             if constexpr (PIN && MC && OM)
@@ -336,7 +336,7 @@ __device__ __forceinline__ void from_ref_basis(const RW &Wr, double *x, Sym4T<PT
 // in FP32 while RK4, Wahba, R->q and the X update stay FP64 (~2e-8 vs FP64).
 // COUNTS: filter b applies only its first counts[b] records of the launch (a separate
 // instantiation so the uniform-length path carries no per-step lane predicate).
-// PIN: the small-batch schedule of the multi-record loop (ekf_record_step, launch_run_multi).
+// PIN: the Schur-inverse-first schedule of the multi-record loop (ekf_record_step, launch_run_multi).
 template <bool TRAJ, bool MIXED, bool SOA, bool COUNTS, bool ONE, bool PIN = false>
 __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run(int64_t batch, int64_t n_steps, int64_t window,
                                                    int64_t step0, const float4 *__restrict__ gd,

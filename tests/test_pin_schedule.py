@@ -1,7 +1,7 @@
-"""The small-batch schedule of the multi-record kernel (k_run<..., PIN = true>: the Schur inverse
-computed in the basic block of the Wahba chain, csrc/pekf_step.hpp) against the default schedule,
-bit for bit, and against the oracle.  PEKF_RUN_PIN forces the choice (0: default schedule, 1: PIN;
-unset: PIN below 2 waves per SIMD, i.e. config 2 and smaller)."""
+"""The PIN schedule of the multi-record kernel (k_run<..., PIN = true>: the Schur inverse computed in
+the basic block of the Wahba chain, csrc/pekf_step.hpp; the default for FP64 launches without
+trajectories or counts) against the compiler's own order (PEKF_RUN_PIN=0), bit for bit, and against
+the oracle."""
 import numpy as np
 import pytest
 
@@ -98,7 +98,7 @@ def test_pin_non_unit_state_and_chunks(eng, monkeypatch):
 
 
 def test_pin_config2_sampled(eng, monkeypatch, oracle_c):
-    """Config 2's batch (65,536 filters: the auto choice takes the PIN schedule) over a 64-row
+    """Config 2's batch (65,536 filters, the default PIN schedule) over a 64-row
     window, 200 records: bit-identical to the default schedule, sampled filters against the oracle."""
     K, W, N = 65536, 64, 200
     win = eng.IMUWindow(K, W).synthesize(seed=synth.DEFAULT_SEED, missing=True)
