@@ -1,20 +1,27 @@
 #!/usr/bin/env python3
 """Headline benchmark: EKF steps/s (predict + Wahba + update) at batch = 1M filters per GPU.
 
-One bench "step" = one fused launch (pekf_run_dev) that advances every filter of this
-rank's shard by --records IMU records (config 3 of BASELINE.json: 1,048,576 filters,
-10,000 records).  Inputs are a resident window of --window records per filter (40 B per
-filter-record, 43 GB at config 3 -- far beyond the 256 MB Infinity Cache), generated on
-the device by the Philox generator before timing and replayed cyclically, so every
-record is read from HBM.  For N > 1 ranks (torchrun, one process per GPU) each rank owns
-an equal contiguous shard of filters (weak scaling), and each step ends with ONE gather of
-the final quaternions to rank 0 over RCCL.
+One bench "step" = one fused launch (pekf_run_dev) per GPU that advances every filter of that
+GPU's shard by --records IMU records (config 3 of BASELINE.json: 1,048,576 filters, 10,000
+records), followed, when more than one GPU takes part, by ONE RCCL gather of the final
+quaternions to the root.  Inputs are a resident window of --window records per filter (40 B per
+filter-record, 43 GB at config 3 -- far beyond the 256 MB Infinity Cache), generated on the device
+by the Philox generator before timing and replayed cyclically, so every record is read from HBM.
 
-Prints ONE JSON line on rank 0.  `value` = filter-steps/s over all ranks (max-over-ranks
-wall clock).  `roofline` is the fused kernel's achieved algorithmic HBM read rate
-(40 B x filters x records / kernel time, HIP events on the launch stream) against the
-8 TB/s peak; `cpu_baseline` times the NumPy restatement of the reference loop on the
-host cores (rank 0, N = 1 only, bounded sample).
+`--gpus N` measures N GPUs by itself, with no PyTorch anywhere in the process:
+  * launched by torchrun (or any launcher that sets RANK / WORLD_SIZE / LOCAL_RANK): one process
+    per GPU; rank 0's RCCL id goes through a file on the node (shard.FileRendezvous), and the
+    barriers and the max-over-ranks time are RCCL all-reduces through libpekf;
+  * launched plainly: one process drives GPUs 0..N-1 (shard.MultiDeviceEKF: ncclCommInitAll,
+    per-device streams, one grouped gather).
+Either way each GPU owns an equal contiguous shard of filters (weak scaling), and the run exits
+non-zero when fewer than N GPUs are visible.
+
+Prints ONE JSON line on rank 0.  `value` = filter-steps/s over all GPUs (the slowest rank's wall
+clock, gather included).  `roofline` is the fused kernel's achieved algorithmic HBM read rate per
+GPU (40 B x filters x records / kernel time, HIP events on the launch stream) against the 8 TB/s
+peak; `valu_roofline` is the resource that binds it, FP64 VALU issue; `cpu_baseline` times the
+NumPy restatement of the reference loop on the host cores (rank 0, N = 1 only, bounded sample).
 """
 from __future__ import annotations
 
@@ -30,6 +37,18 @@ sys.path.insert(0, ROOT)
 REC_BYTES = 40          # algorithmic bytes per filter-record
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level table)
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (spec)
+# FP64 VALU issue ceiling: 256 CUs x 4 SIMDs, a wave64 FP64 instruction occupies a 16-lane SIMD for
+# 4 cycles, at the 2.4 GHz peak engine clock -> 614.4 G wave-instructions/s (= 78.6 TFLOP/s of FMA)
+SIMDS, CYCLES_PER_WAVE_INSTR, PEAK_CLOCK_GHZ = 1024, 4, 2.4
+VALU_PEAK_GWIPS = SIMDS * PEAK_CLOCK_GHZ / CYCLES_PER_WAVE_INSTR
+
+
+class BenchError(SystemExit):
+    """A refused configuration: message on stderr, exit status 2."""
+
+    def __init__(self, msg):
+        print("[bench] error: " + msg, file=sys.stderr, flush=True)
+        super().__init__(2)
 
 
 def log(msg):
@@ -53,6 +72,51 @@ class StdoutForTheResult:
         os.dup2(2, 1)
 
 
+# ----------------------------------------------------------------------------------- launch plan
+def launch_plan(gpus, environ, shard_of=None, one_process=False):
+    """How this process takes part: dict(mode, rank, world, devices, first_shard).
+
+    mode "ranks":  a launcher set RANK and WORLD_SIZE (torchrun): this process is one rank, on
+                   device LOCAL_RANK; WORLD_SIZE must equal --gpus.
+    mode "single": --gpus 1, no launcher: GPU 0.
+    mode "multi":  --gpus N > 1, no launcher: this process drives GPUs 0..N-1.
+    shard_of (R, W): a one-GPU run of rank R's shard of a W-way job (its filters keep their global
+    ids, so any rank's workload can be rehearsed on one GPU).
+    one_process: mode "multi" even for --gpus 1 (the plain --gpus N code path, rehearsed on one GPU)."""
+    if gpus < 1:
+        raise BenchError("--gpus must be >= 1")
+    if "RANK" in environ and "WORLD_SIZE" in environ:
+        rank, world = int(environ["RANK"]), int(environ["WORLD_SIZE"])
+        if world != gpus:
+            raise BenchError("WORLD_SIZE=%d from the launcher but --gpus %d" % (world, gpus))
+        if shard_of is not None:
+            raise BenchError("--shard-of is a one-process rehearsal; not under a launcher")
+        local = int(environ.get("LOCAL_RANK", rank))
+        return dict(mode="ranks", rank=rank, world=world, devices=[local], first_shard=rank)
+    if shard_of is not None:
+        r, w = shard_of
+        if gpus != 1 or not 0 <= r < w:
+            raise BenchError("--shard-of R/W needs --gpus 1 and 0 <= R < W")
+        return dict(mode="single", rank=0, world=1, devices=[0], first_shard=r)
+    if gpus == 1 and not one_process:
+        return dict(mode="single", rank=0, world=1, devices=[0], first_shard=0)
+    return dict(mode="multi", rank=0, world=gpus, devices=list(range(gpus)), first_shard=0)
+
+
+def shard_plan(batch_per_gpu, world):
+    """[(first_filter, count)] of every GPU's shard (shard.shard_range over the global batch)."""
+    from poseestimationkf_amd import shard
+    return [shard.shard_range(batch_per_gpu * world, r, world) for r in range(world)]
+
+
+def parse_shard_of(s):
+    try:
+        r, w = (int(v) for v in s.split("/"))
+    except ValueError:
+        raise argparse.ArgumentTypeError("expected R/W, e.g. 7/8")
+    return r, w
+
+
 # ----------------------------------------------------------------------------------- CPU baseline
 def _cpu_worker(args):
     """Runs in a forked child (before any GPU initialisation): NumPy restatement of main_file.py's loop."""
@@ -71,10 +135,19 @@ def _cpu_worker(args):
     return len(ids) * n_rec, time.perf_counter() - t0
 
 
+def cpu_share(environ=os.environ):
+    """(processes to use, cores visible): the host cores this job may use.  On the GPU box the job's
+    CPU share is given by OMP_NUM_THREADS (16 per GPU) while sched_getaffinity shows the whole
+    machine; elsewhere all visible cores."""
+    cores = len(os.sched_getaffinity(0))
+    cap = environ.get("OMP_NUM_THREADS")
+    use = min(cores, int(cap)) if cap and cap.isdigit() and int(cap) > 0 else cores
+    return max(1, use), cores
+
+
 def cpu_baseline(seed, missing, filters_per_core=160, n_rec=1500):
     import multiprocessing as mp
-    cores = len(os.sched_getaffinity(0))
-    workers = max(1, min(16, cores))
+    workers, cores = cpu_share()
     ctx = mp.get_context("fork")
     mgr = ctx.Manager()
     barrier = mgr.Barrier(workers)
@@ -85,9 +158,11 @@ def cpu_baseline(seed, missing, filters_per_core=160, n_rec=1500):
     steps = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
     return {"value": steps / wall, "unit": "EKF steps/s", "cores": workers, "kind": "port",
+            "per_core": steps / wall / workers, "cores_visible": cores,
             "sample": "NumPy restatement of main_file.py's per-record loop (oracle/ekf_numpy.py, bit-identical "
-                      "to the reference), %d processes x %d filters x %d records of the same synthetic stream; "
-                      "%d host cores visible" % (workers, filters_per_core, n_rec, cores),
+                      "to the reference), %d processes (one per core of this job's CPU share, OMP_NUM_THREADS; "
+                      "%d cores visible on the host) x %d filters x %d records of the same synthetic stream"
+                      % (workers, cores, filters_per_core, n_rec),
             "seconds": wall}
 
 
@@ -100,12 +175,164 @@ def c_oracle_rate(seed, missing, n_filters=64, n_rec=1000):
     t0 = time.perf_counter()
     oracle_c.run(rec)
     dt = time.perf_counter() - t0
-    return {"value": n_filters * n_rec / dt, "threads": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count())),
+    return {"value": n_filters * n_rec / dt, "threads": cpu_share()[0],
             "what": "C FP64 restatement (oracle/ekf_oracle.c, Jacobi SVD), OpenMP over filters"}
 
 
+# ----------------------------------------------------------------------------------- the runs
+class RankRun:
+    """One process = one GPU (modes "single" and "ranks"): this rank's shard as an IMUWindow +
+    BatchedEKF on device `dev`; with a communicator, each step ends with the RCCL gather to rank 0."""
+
+    def __init__(self, args, plan):
+        import numpy as np
+
+        from poseestimationkf_amd import engine, shard
+        self.np, self.engine, self.shard = np, engine, shard
+        self.rank, self.world = plan["rank"], plan["world"]
+        engine.set_device(plan["devices"][0])
+        self.B = args.batch
+        self.first = plan["first_shard"] * self.B
+        self.own_stream = engine.Stream()
+        self.stream = self.own_stream.handle
+        self.comm = None
+        if self.world > 1 or args.dist:
+            self.comm = shard.connect(self.rank, self.world)
+            log("rank %d/%d: RCCL %d communicator on device %d" % (self.rank, self.world, shard.rccl_version(),
+                                                                  self.comm.device))
+        log("rank %d/%d: synthesizing filters [%d, %d) x %d records (%.1f GB resident)" %
+            (self.rank, self.world, self.first, self.first + self.B, args.window,
+             self.B * args.window * REC_BYTES / 1e9))
+        self.win = engine.IMUWindow(self.B, args.window).synthesize(
+            seed=args.seed, first_filter=self.first, missing=args.missing, stream=self.stream)
+        self.filt = engine.BatchedEKF(self.B, q=1.0, r=0.1, precision=args.precision)
+        self.recv = engine.DeviceBuffer(32 * self.B * self.world) if (self.comm and self.rank == 0) else None
+        self.sync()
+        self.ev = []
+
+    def prepare(self, n_steps):
+        self.ev = [(self.engine.Event(), self.engine.Event()) for _ in range(n_steps)]
+
+    def sync(self):
+        self.engine.check(self.engine.lib.pekf_stream_sync(self.stream))
+
+    def barrier(self):
+        if self.comm is not None:
+            self.comm.barrier(self.stream)
+
+    def step(self, k, n_rec, row0):
+        e0, e1 = self.ev[k]
+        e0.record(self.stream)
+        self.filt.run_async(self.win, n_rec, row0, self.stream)
+        e1.record(self.stream)
+        if self.comm is not None:  # ONE RCCL gather of the final quaternions to rank 0 (pekf_gather_dev)
+            self.shard.gather_quaternions(self.comm, self.filt.X.ptr, self.B, self.recv, 0, self.stream)
+
+    def kernel_ms(self, k):
+        return self.ev[k][0].elapsed_ms(self.ev[k][1])
+
+    def slowest(self, elapsed):
+        return self.comm.max_over_ranks(elapsed, self.stream) if self.comm is not None else elapsed
+
+    def final_rows(self):
+        """(global first filter id, X rows) available on this rank: every filter's final X on rank 0
+        after the gather, this shard's otherwise."""
+        np = self.np
+        if self.comm is not None and self.rank == 0:
+            got = self.recv.download((self.world * self.B, 4), np.float64)
+            Xr, _ = self.filt.get_state()
+            if not np.array_equal(got[:self.B], Xr):
+                raise AssertionError("RCCL gather: rank 0's rows differ from its shard's state")
+            return 0 if self.world > 1 else self.first, got
+        X, _ = self.filt.get_state()
+        return self.first, X
+
+    def close(self):
+        if self.comm is not None:
+            self.comm.close()
+
+
+class MultiRun:
+    """One process drives GPUs 0..N-1 (mode "multi"): shard.MultiDeviceEKF, one grouped RCCL gather
+    per step.  Kernel times are per-device HIP events on each device's own stream."""
+
+    def __init__(self, args, plan):
+        from poseestimationkf_amd import engine, shard
+        self.engine = engine
+        self.rank, self.world, self.devices = 0, plan["world"], plan["devices"]
+        self.B = args.batch
+        log("single process over devices %s: %d filters each, %d records resident (%.1f GB per GPU)" %
+            (self.devices, self.B, args.window, self.B * args.window * REC_BYTES / 1e9))
+        self.m = shard.MultiDeviceEKF(self.devices, self.B, args.window, precision=args.precision)
+        log("RCCL %d: %d communicators (ncclCommInitAll)" % (shard.rccl_version(), len(self.devices)))
+        self.m.synthesize(seed=args.seed, missing=args.missing)
+        self.ev = []
+
+    def prepare(self, n_steps):
+        """HIP events are per device: ev[k][i] = (start, end) of step k on device i."""
+        self.ev = []
+        for _ in range(n_steps):
+            pairs = []
+            for d in self.devices:
+                self.engine.set_device(d)
+                pairs.append((self.engine.Event(), self.engine.Event()))
+            self.ev.append(pairs)
+        self.engine.set_device(self.devices[0])
+
+    def sync(self):
+        self.m.sync()
+
+    def barrier(self):
+        self.m.sync()
+
+    def step(self, k, n_rec, row0):
+        for i, d in enumerate(self.devices):
+            self.engine.set_device(d)
+            e0, e1 = self.ev[k][i]
+            s = self.m.streams[i].handle
+            e0.record(s)
+            self.m.filts[i].run_async(self.m.wins[i], n_rec, row0, s)
+            e1.record(s)
+        self.engine.set_device(self.devices[0])
+        self.m.gather_async()
+
+    def kernel_ms(self, k, device_index=None):
+        """The slowest device's kernel time of step k (or one device's)."""
+        t = [e0.elapsed_ms(e1) for e0, e1 in self.ev[k]]
+        return max(t) if device_index is None else t[device_index]
+
+    def slowest(self, elapsed):
+        return elapsed
+
+    def final_rows(self):
+        return 0, self.m.gathered()
+
+    def close(self):
+        self.m.close()
+
+
+def parity_check(first, rows, n_samples, n_records, args):
+    """Re-run sampled filters (spread over every GPU's shard when rows hold them all) with the C
+    oracle from the host mirror of the generator; max |dq| against the device's final X."""
+    import numpy as np
+
+    from oracle import oracle_c
+    from poseestimationkf_amd import synth
+    n = rows.shape[0]
+    cols = np.unique(np.linspace(0, n - 1, max(1, n_samples)).astype(np.int64))
+    rec = synth.generate(cols + first, args.window, seed=args.seed, missing=args.missing)
+    Xo, _, _ = oracle_c.run(rec, n_steps=n_records)
+    err = float(np.abs(rows[cols] - Xo).max())
+    shards = sorted({int((c + first) // args.batch) for c in cols})
+    return {"filters": int(len(cols)), "records": int(n_records), "max_abs_err_vs_oracle": err,
+            "tolerance": 1e-5, "ok": bool(err < 1e-5), "global_filter_ids": [int(cols[0] + first), int(cols[-1] + first)],
+            "shards_covered": shards,
+            "unit_norm_all": bool(np.isfinite(rows).all() and np.allclose(np.linalg.norm(rows, axis=1), 1.0,
+                                                                          atol=1e-12))}
+
+
 # ----------------------------------------------------------------------------------- main
-def main():
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -116,18 +343,20 @@ def main():
     ap.add_argument("--missing", action="store_true", help="config 5: 30%% magnetometer-missing records")
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--cpu-baseline", choices=["port", "none"], default="port")
-    ap.add_argument("--parity-samples", type=int, default=16)
+    ap.add_argument("--parity-samples", type=int, default=16,
+                    help="filters re-run by the C oracle (at least 4 per GPU when N > 1)")
     ap.add_argument("--precision", choices=["f64", "mixed"], default="f64",
                     help="f64 (default, as the reference) or mixed (covariance recursion in f32)")
     ap.add_argument("--dist", action="store_true",
                     help="use the RCCL path (pekf_gather_dev) even at world size 1 (exercises the gather)")
-    args = ap.parse_args()
+    ap.add_argument("--shard-of", type=parse_shard_of, default=None, metavar="R/W",
+                    help="rehearse rank R's shard of a W-way job on one GPU (e.g. 7/8 at config 4)")
+    ap.add_argument("--one-process", action="store_true",
+                    help="drive the GPUs from one process (MultiDeviceEKF) even for --gpus 1")
+    args = ap.parse_args(argv)
+    plan = launch_plan(args.gpus, os.environ, args.shard_of, args.one_process)
+    rank, world = plan["rank"], plan["world"]
     out_fd = StdoutForTheResult()
-
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
-    assert world == args.gpus or "RANK" not in os.environ, "WORLD_SIZE and --gpus disagree"
 
     # CPU baseline first, in forked workers, before anything touches the GPU.
     cpu = None
@@ -140,188 +369,158 @@ def main():
             cpu["c_oracle"] = {"error": str(e)}
         log("cpu baseline: %.0f steps/s on %d cores" % (cpu["value"], cpu["cores"]))
 
-    dist = None
-    use_dist = world > 1 or args.dist
-    if use_dist:
-        # torch.distributed only for the rendezvous (gloo, CPU): the RCCL id broadcast and the
-        # host barrier.  The data-path collectives are RCCL through libpekf (shard.Communicator).
-        # torch is imported before libpekf so that the process has ONE HIP runtime and ONE RCCL
-        # (the ones PyTorch-ROCm bundles; libpekf binds them by SONAME).
-        import torch  # noqa: F401
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29517")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+    from poseestimationkf_amd import _lib
+    visible = _lib.device_count()
+    need = max(plan["devices"]) + 1
+    if visible < need:
+        raise BenchError("--gpus %d (%s) needs %d visible GPU(s), %d visible" %
+                         (args.gpus, plan["mode"], need, visible))
 
-    import numpy as np
-
-    from poseestimationkf_amd import engine, shard, synth
-    engine.set_device(local)
-    first, B = shard.shard_range(args.batch * world, rank, world)
+    run = MultiRun(args, plan) if plan["mode"] == "multi" else RankRun(args, plan)
     N, W = args.records, args.window
-
-    own_stream = engine.Stream()  # keep the object alive for the whole run
-    stream = own_stream.handle
-    comm = shard.Communicator(shard.exchange_unique_id(rank, world), world, rank) if use_dist else None
-    if comm is not None:
-        log("rank %d/%d: RCCL %d communicator on device %d" % (rank, world, shard.rccl_version(), comm.device))
-
-    def sync():
-        engine.check(engine.lib.pekf_stream_sync(stream))
-
-    def barrier():
-        if use_dist:
-            dist.barrier()
-
-    log("rank %d/%d: synthesizing %d filters x %d records (%.1f GB resident)" %
-        (rank, world, B, W, synth.window_bytes(B, W) / 1e9))
-    win = engine.IMUWindow(B, W).synthesize(seed=args.seed, first_filter=first, missing=args.missing,
-                                            stream=stream)
-    filt = engine.BatchedEKF(B, q=1.0, r=0.1, precision=args.precision)
-    recv = engine.DeviceBuffer(32 * B * world) if (use_dist and rank == 0) else None
-    sync()
-
     total = args.warmup + args.steps
-    ev = [(engine.Event(), engine.Event()) for _ in range(total)]
-
-    def bench_step(k):
-        e0, e1 = ev[k]
-        e0.record(stream)
-        filt.run_async(win, N, (k * N) % W, stream)
-        e1.record(stream)
-        if use_dist:  # ONE RCCL gather of the final quaternions to rank 0 (pekf_gather_dev)
-            shard.gather_quaternions(comm, filt.X.ptr, B, recv, 0, stream)
+    run.prepare(total)
 
     for k in range(args.warmup):
-        bench_step(k)
-        sync()
-        log("warmup %d: kernel %.1f ms" % (k, ev[k][0].elapsed_ms(ev[k][1])))
+        run.step(k, N, (k * N) % W)
+        run.sync()
+        log("warmup %d: kernel %.1f ms" % (k, run.kernel_ms(k)))
 
-    sync()
-    barrier()
+    run.sync()
+    run.barrier()
     t0 = time.perf_counter()
     for k in range(args.warmup, total):
-        bench_step(k)
-    sync()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if use_dist:  # the slowest rank's time (RCCL max all-reduce)
-        tb = engine.DeviceBuffer(8).upload(np.array([elapsed], np.float64), stream)
-        comm.allreduce_max(tb.ptr, 1, stream)
-        elapsed = float(tb.download((1,), np.float64, stream)[0])
-        sync()
-    kms = [ev[k][0].elapsed_ms(ev[k][1]) for k in range(args.warmup, total)]
-    log("timed: %.3f s for %d steps; kernel ms %s" % (elapsed, args.steps, ", ".join("%.1f" % v for v in kms)))
+        run.step(k, N, (k * N) % W)
+    run.sync()
+    run.barrier()
+    elapsed = run.slowest(time.perf_counter() - t0)
+    kms = [run.kernel_ms(k) for k in range(args.warmup, total)]
+    log("timed: %.3f s for %d steps on %d GPU(s); kernel ms %s" %
+        (elapsed, args.steps, world, ", ".join("%.1f" % v for v in kms)))
 
-    # parity at scale: sampled filters re-run on the host by the C oracle
+    # final quaternions of every GPU's filters on rank 0 (the gathered rows), then all ranks part
+    rows = run.final_rows() if rank == 0 and args.parity_samples > 0 else None
+    run.barrier()
     parity = None
-    if args.parity_samples > 0:
-        from oracle import oracle_c
-        X, _ = filt.get_state()
-        cols = np.linspace(0, B - 1, args.parity_samples).astype(np.int64)
-        rec = synth.generate(cols + first, W, seed=args.seed, missing=args.missing)
-        Xo, _, _ = oracle_c.run(rec, n_steps=total * N)
-        err = float(np.abs(X[cols] - Xo).max())
-        parity = {"filters": int(args.parity_samples), "records": total * N, "max_abs_err_vs_oracle": err,
-                  "tolerance": 1e-5, "ok": bool(err < 1e-5)}
-        log("parity: max |dq| = %.3e over %d sampled filters" % (err, args.parity_samples))
+    if rows is not None:
+        samples = max(args.parity_samples, 4 * world)
+        parity = parity_check(rows[0], rows[1], samples, total * N, args)
+        log("parity: max |dq| = %.3e over %d sampled filters of shards %s" %
+            (parity["max_abs_err_vs_oracle"], parity["filters"], parity["shards_covered"]))
 
     if rank == 0:
-        steps_total = world * B * N * args.steps
-        value = steps_total / elapsed
-        k_s = float(np.mean(kms)) / 1e3
-        achieved = B * N * REC_BYTES / k_s / 1e9
-        flop = ISA_COUNTS[args.precision]["flop"]
-        valu = ISA_COUNTS[args.precision]["valu_instr"]
-        # the committed PMC pass is of the FP64 command without missing records
-        traffic, tsrc = measured_traffic(B, N) if args.precision == "f64" and not args.missing else (None, None)
-        clk = tsrc[1].get("effective_clock_ghz") if tsrc else None
-        issue_frac = (4.0 * (B / 64.0) * N * valu / (1024 * clk * 1e9 * k_s)) if clk else None
-        out = {
-            "metric": "EKF steps/sec (predict+Wahba+update) at batch=1M; HBM-roofline %",
-            "value": value,
-            "unit": "EKF filter-steps/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64" if args.precision == "f64" else "f64 quaternion path + f32 covariance (P, S^-1)",
-            "data": "synthetic (on-device Philox IMU generator, bit-identical host mirror; 40 B records, "
-                    "%d-record resident window replayed cyclically)" % W,
-            "config": {"workload": workload_name(B, N, args.missing),
-                       "filters_per_gpu": B, "global_filters": B * world, "records_per_step": N,
-                       "window_records": W, "parallelism": "dp%d (filter-batch shards, 1 RCCL gather via pekf_gather_dev)" % world},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": (os.path.relpath(tsrc[0], ROOT) + " (2 x FETCH_SIZE, separate "
-                                            "rocprofv3 --pmc pass of this command)") if tsrc else None,
-                         "kernel": "k_run<false> (pekf_run_dev)", "kernel_ms": k_s * 1e3,
-                         "bytes_per_launch": B * N * REC_BYTES},
-            "fp64_valu": {"flop_per_step": flop, "fp64_instr_per_step": ISA_COUNTS[args.precision]["fp64_instr"],
-                          "valu_instr_per_step": valu,
-                          "achieved_tflops": B * N * flop / k_s / 1e12, "peak_tflops": FP64_PEAK_TFLOPS,
-                          "frac": B * N * flop / k_s / 1e12 / FP64_PEAK_TFLOPS,
-                          "valu_busy_pmc": tsrc[1].get("valu_busy") if tsrc else None,
-                          "issue_frac": issue_frac,
-                          "clock_ghz_pmc": clk,
-                          "note": "the kernel is VALU-issue-bound at a power-limited clock: issue_frac = 4 cycles x "
-                                  "wave-instructions / (1024 SIMDs x PMC effective clock x kernel time); the same "
-                                  "launch with cache-resident records runs at 2.11 GHz instead of 1.80 "
-                                  "(profiles/r1/power_probe); HBM frac is capped by it"},
-            "cpu_baseline": cpu,
-            "parity": parity,
-        }
+        out = result_line(args, plan, elapsed, kms, cpu, parity)
         out_fd.emit(json.dumps(out))
-    if use_dist:
-        if rank == 0:  # the gathered quaternions are the filters' final X, rank 0's shard first
-            Xr, _ = filt.get_state()
-            got = recv.download((world * B, 4), np.float64)
-            assert np.array_equal(got[:B], Xr), "gather mismatch on rank 0"
-            assert np.isfinite(got).all() and np.allclose(np.linalg.norm(got, axis=1), 1.0, atol=1e-12), \
-                "gathered quaternions of other ranks are not unit"
-            log("gather: %d quaternions on rank 0 (RCCL via pekf_gather_dev) match rank 0's shard" % got.shape[0])
-        comm.close()
-        dist.destroy_process_group()
+    run.close()
+    if parity is not None and not (parity["ok"] and parity["unit_norm_all"]):
+        raise SystemExit("parity failed: %r" % parity)
 
-# FP64 work per filter-step of the fused kernel, counted from its gfx950 ISA hot loop by
-# scripts/isa_count.py (DESIGN.md "FP64 budget"): FP64 VALU instructions, and the FLOP of
-# the arithmetic ones with an FMA counted as 2.
+
+def result_line(args, plan, elapsed, kms, cpu, parity):
+    import numpy as np
+    world, B, N = plan["world"], args.batch, args.records
+    steps_total = world * B * N * args.steps
+    value = steps_total / elapsed
+    k_s = float(np.mean(kms)) / 1e3   # per-GPU kernel time (multi: the slowest device per step)
+    achieved = B * N * REC_BYTES / k_s / 1e9
+    counts = ISA_COUNTS[args.precision]
+    valu = counts["valu_instr"]
+    wave_instr = (B / 64.0) * N * valu
+    cited = cited_profile(B, N) if args.precision == "f64" and not args.missing else None
+    launch = {"ranks": "one process per GPU (launcher ranks; RCCL id through shard.FileRendezvous)",
+              "single": "one process, one GPU",
+              "multi": "one process over GPUs %s (ncclCommInitAll, grouped gather)" % plan["devices"]}[plan["mode"]]
+    return {
+        "metric": "EKF steps/sec (predict+Wahba+update) at batch=1M; HBM-roofline %",
+        "value": value,
+        "unit": "EKF filter-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64" if args.precision == "f64" else "f64 quaternion path + f32 covariance (P, S^-1)",
+        "data": "synthetic (on-device Philox IMU generator, bit-identical host mirror; 40 B records, "
+                "%d-record resident window replayed cyclically)" % args.window,
+        "config": {"workload": workload_name(B, N, args.missing, world),
+                   "filters_per_gpu": B, "global_filters": B * world, "records_per_step": N,
+                   "window_records": args.window,
+                   "first_filter": plan["first_shard"] * B if plan["mode"] == "single" else 0,
+                   "parallelism": "dp%d (filter-batch shards%s)" % (
+                       world, ", 1 RCCL gather of final quaternions per step"
+                       if world > 1 or args.dist or plan["mode"] == "multi" else ""),
+                   "launch": launch},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": cited["hbm_traffic_bytes"] if cited else None,
+                     "traffic_source": ("cited, not measured in this run: %s (2 x FETCH_SIZE of a separate "
+                                        "rocprofv3 --pmc pass of this command on an earlier box)" % cited["path"])
+                                       if cited else None,
+                     "per": "one GPU's launch", "kernel": "k_run<false> (pekf_run_dev)", "kernel_ms": k_s * 1e3,
+                     "bytes_per_launch": B * N * REC_BYTES,
+                     "binding_resource": "FP64 VALU issue, not HBM: see valu_roofline"},
+        "valu_roofline": {"bound": "fp64-valu-issue", "achieved": wave_instr / k_s / 1e9, "peak": VALU_PEAK_GWIPS,
+                          "unit": "G wave-instr/s", "frac": wave_instr / k_s / 1e9 / VALU_PEAK_GWIPS,
+                          "valu_per_filter_step": valu,
+                          "valu_source": "static count of the hot loop's executed blocks (scripts/loop_blocks.py, "
+                                         "DESIGN.md §4.2); the PMC pass counts %s per wave-step" %
+                                         ("%.1f" % cited["valu_insts_per_wave_step"] if cited else "the same"),
+                          "peak_note": "1024 SIMDs x 2.4 GHz / 4 cycles per wave64 FP64 instruction "
+                                       "(= the 78.6 TFLOP/s FP64 vector peak); the clock under this load is "
+                                       "power-limited below 2.4 GHz",
+                          "flop_per_step": counts["flop"], "fp64_instr_per_step": counts["fp64_instr"],
+                          "achieved_tflops": B * N * counts["flop"] / k_s / 1e12, "peak_tflops": FP64_PEAK_TFLOPS},
+        "cited_profile": ({"path": cited["path"], "valu_busy": cited.get("valu_busy"),
+                           "clock_ghz": cited.get("effective_clock_ghz"),
+                           "note": "from the committed rocprofv3 PMC passes of this command, not this run"}
+                          if cited else None),
+        "cpu_baseline": cpu,
+        "parity": parity,
+    }
+
+
 # per filter-step: the VALU instructions of the basic blocks a tracked lane executes in k_run's hot
 # loop (scripts/loop_blocks.py on the hipcc -S listing: the fallback bodies sit behind
-# s_cbranch_execz); FP64 instructions and FLOP from scripts/isa_count.py on the same blocks.  The
-# PMC pass in profiles/ counts the executed total (SQ_INSTS_VALU per wave-step).
+# s_cbranch_execz); FP64 instructions and FLOP (FMA = 2) from scripts/isa_count.py on the same blocks.
+# The PMC pass in profiles/ counts the executed total (SQ_INSTS_VALU per wave-step).
 ISA_COUNTS = {"f64": {"flop": 436, "fp64_instr": 298, "valu_instr": 301},
               "mixed": {"flop": 240, "fp64_instr": 191, "valu_instr": 329}}  # mixed: + ~130 f32 instructions
 FLOP_PER_STEP = ISA_COUNTS["f64"]["flop"]
 FP64_INSTR_PER_STEP = ISA_COUNTS["f64"]["fp64_instr"]
 
 
-def workload_name(batch, records, missing):
-    """BASELINE.json's configuration this run is (configs 2, 3 and 5 are 10,000 records)."""
+def workload_name(batch, records, missing, world=1):
+    """BASELINE.json's configuration this run is (configs 2-5 are 10,000 records)."""
     if records == 10000 and batch == 1 << 20:
-        return ("config 5: batch=1,048,576/GPU, 30% missing-mag" if missing else
-                "config 3: batch=1,048,576 filters/GPU x 10,000 records")
-    if records == 10000 and batch == 65536 and not missing:
+        if missing:
+            return "config 5: batch=1,048,576/GPU, 30% missing-mag" + (" x %d GPUs" % world if world > 1 else "")
+        if world == 8:
+            return "config 4: batch=8,388,608 filters sharded 8-way x 10,000 records"
+        if world > 1:
+            return "config 3 per GPU x %d GPUs: batch=%d filters x 10,000 records" % (world, batch * world)
+        return "config 3: batch=1,048,576 filters/GPU x 10,000 records"
+    if records == 10000 and batch == 65536 and not missing and world == 1:
         return "config 2: batch=65,536 filters/GPU x 10,000 records"
-    return "custom: batch=%d filters/GPU x %d records%s" % (batch, records, ", 30% missing-mag" if missing else "")
+    return "custom: batch=%d filters/GPU x %d records x %d GPU(s)%s" % (
+        batch, records, world, ", 30% missing-mag" if missing else "")
 
 
-def measured_traffic(batch, records):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of the current build
-    (profiles/HEADLINE_PMC names it; scripts/refresh.sh produces it), if its config matches."""
+def cited_profile(batch, records):
+    """The committed rocprofv3 PMC summary of the current build (profiles/HEADLINE_PMC names it;
+    scripts/refresh.sh produces it), if its config matches; its numbers are cited, not measured."""
     try:
         with open(os.path.join(ROOT, "profiles", "HEADLINE_PMC")) as fh:
-            path = os.path.join(ROOT, fh.read().strip())
-        with open(path) as fh:
+            rel = fh.read().strip()
+        with open(os.path.join(ROOT, rel)) as fh:
             s = json.load(fh)
     except OSError:
-        return None, None
+        return None
     if s.get("config") != {"batch": batch, "records": records}:
-        return None, None
-    return s["hbm_traffic_bytes"], (path, s)
+        return None
+    return dict(s, path=rel)
+
 
 if __name__ == "__main__":
     main()

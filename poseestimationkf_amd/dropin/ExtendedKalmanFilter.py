@@ -7,6 +7,7 @@ inputs (main_file.py:39-44 keeps the returned X in a list).  The arithmetic runs
 per-call gfx950 kernels of libpekf.so (k_predict, k_correct, k_rk4, ...); the two per-record
 methods go through the CPython binding ``_fastcall`` (same C entry points, less call overhead).  For many
 filters at once use ``poseestimationkf_amd.engine.BatchedEKF`` (the fused kernel).
+``predict`` / ``update`` are aliases of ``Prediction`` / ``Correction`` (the north_star's names).
 """
 import numpy as np
 from _bootstrap import engine as _eng
@@ -49,3 +50,8 @@ class KalmanFilter:
 
     def Correction(self, Mag, Acc, z_k, P_k, K_k):       # :70-80
         return _fc.correct(Mag, Acc, z_k, P_k, K_k, self.wahba.w_initial_acc, self.wahba.w_initial_mag)
+
+    # the north_star's call surface (BASELINE.json): predict()/update() are the same methods as the
+    # reference's Prediction (:58) / Correction (:70) -- aliases, not wrappers, so they are the same code
+    predict = Prediction
+    update = Correction

@@ -8,21 +8,26 @@ collective is ONE gather of the final quaternions to the root, an RCCL gather ov
 issued through libpekf's C ABI (pekf_gather_dev, include/pekf.h) -- no PyTorch on the data
 path.  Two ways to drive it:
 
-* one process per GPU (torchrun): `Communicator(exchange_unique_id(rank, world), world, rank)`;
-  the 128-byte RCCL id travels over any CPU channel -- here torch.distributed's gloo group,
-  which is used for the rendezvous only;
+* one process per GPU (torchrun or any launcher that sets RANK / WORLD_SIZE):
+  `Communicator(FileRendezvous(rank, world).share_id(Communicator.unique_id), world, rank)`;
+  the 128-byte RCCL id travels through a file on the node (no PyTorch in the process), and
+  once the communicator exists its barrier and max all-reduce are RCCL too;
 * one process for several GPUs: `MultiDeviceEKF(devices, ...)` (ncclCommInitAll, one host
-  thread, the gather as one RCCL group).
+  thread, the gather as one RCCL group) -- no out-of-band exchange at all.
 """
 from __future__ import annotations
 
 import ctypes
+import os
+import tempfile
+import time
 
 import numpy as np
 
 from ._lib import check, lib
 
 COMM_ID_BYTES = 128
+_RDZV_MAGIC = b"PEKFRDZV1"
 
 
 def shard_range(global_batch, rank, world):
@@ -76,6 +81,18 @@ class Communicator:
     def allreduce_max(self, buf_ptr, count, stream=None):
         check(lib.pekf_allreduce_max_dev(self.handle, buf_ptr, int(count), stream))
 
+    def max_over_ranks(self, value, stream=None):
+        """max of a host float over all ranks (one RCCL all-reduce of 8 bytes, then a stream sync)."""
+        from .engine import DeviceBuffer
+
+        b = DeviceBuffer(8).upload(np.array([value], np.float64), stream)
+        self.allreduce_max(b.ptr, 1, stream)
+        return float(b.download((1,), np.float64, stream)[0])
+
+    def barrier(self, stream=None):
+        """Every rank has reached this point (and its stream has drained up to it)."""
+        self.max_over_ranks(0.0, stream)
+
     def close(self):
         if getattr(self, "handle", None):
             h, self.handle = self.handle, None
@@ -88,19 +105,85 @@ class Communicator:
             pass
 
 
-def exchange_unique_id(rank, world, make_id=Communicator.unique_id):
-    """Rank 0's RCCL id on every rank, over torch.distributed's (CPU, gloo) default group.
+def _proc_start_ticks(pid):
+    """Start time of a process in clock ticks since boot (/proc/<pid>/stat field 22), or 0."""
+    try:
+        with open("/proc/%d/stat" % pid, "rb") as fh:
+            return int(fh.read().rsplit(b")", 1)[1].split()[19])
+    except (OSError, IndexError, ValueError):
+        return 0
 
-    This is rendezvous plumbing only: 128 bytes once per job; the collective itself is RCCL."""
-    import torch.distributed as dist
 
-    obj = [make_id() if rank == 0 else None]
-    if world > 1:
-        dist.broadcast_object_list(obj, src=0)
-    uid = obj[0]
-    if not isinstance(uid, (bytes, bytearray)) or len(uid) != COMM_ID_BYTES:
-        raise RuntimeError("bad RCCL unique id from rank 0")
-    return bytes(uid)
+class FileRendezvous:
+    """Torch-free out-of-band channel for rank 0's 128-byte RCCL id, through a file on the node.
+
+    A launcher such as torchrun starts every local rank as a child of one process, so the job's
+    key is (MASTER_ADDR, MASTER_PORT, the parent's pid and start time): unique among the jobs that
+    ever ran on the node, so a file left behind by another job is never read.  Rank 0 writes the id
+    atomically (temp file + rename); the others poll for it.  `key` / PEKF_RDZV_KEY override the key
+    for launchers whose ranks do not share a parent; PEKF_RDZV_DIR names the directory (it must be
+    shared by every rank, e.g. a network file system when ranks span nodes).
+    RCCL's communicator creation is itself collective, so after it returns on rank 0 every rank
+    has read the file and `done()` removes it."""
+
+    def __init__(self, rank, world, key=None, directory=None, timeout=600.0):
+        self.rank, self.world, self.timeout = int(rank), int(world), float(timeout)
+        if not 0 <= self.rank < self.world:
+            raise ValueError("need 0 <= rank < world")
+        if key is None:
+            key = os.environ.get("PEKF_RDZV_KEY")
+        if key is None:
+            ppid = os.getppid()
+            key = "%s_%s_%d_%d" % (os.environ.get("MASTER_ADDR", "local"), os.environ.get("MASTER_PORT", "0"),
+                                   ppid, _proc_start_ticks(ppid))
+        key = "".join(c if c.isalnum() or c in "-_." else "_" for c in str(key))
+        directory = directory or os.environ.get("PEKF_RDZV_DIR") or tempfile.gettempdir()
+        self.path = os.path.join(directory, "pekf-rdzv-%s.id" % key)
+
+    def share_id(self, make_id=None):
+        """Rank 0 creates the id (make_id(), default a new RCCL id) and publishes it; every rank returns it."""
+        if make_id is None:
+            make_id = Communicator.unique_id
+        if self.rank == 0:
+            uid = bytes(make_id())
+            if len(uid) != COMM_ID_BYTES:
+                raise RuntimeError("an RCCL unique id is %d bytes" % COMM_ID_BYTES)
+            if self.world > 1:
+                tmp = "%s.%d.tmp" % (self.path, os.getpid())
+                with open(tmp, "wb") as fh:
+                    fh.write(_RDZV_MAGIC + uid)
+                os.replace(tmp, self.path)
+            return uid
+        deadline = time.monotonic() + self.timeout
+        while True:
+            try:
+                with open(self.path, "rb") as fh:
+                    blob = fh.read()
+                if blob.startswith(_RDZV_MAGIC) and len(blob) == len(_RDZV_MAGIC) + COMM_ID_BYTES:
+                    return blob[len(_RDZV_MAGIC):]
+            except FileNotFoundError:
+                pass
+            if time.monotonic() > deadline:
+                raise TimeoutError("rank %d: no RCCL id from rank 0 at %s after %.0f s"
+                                   % (self.rank, self.path, self.timeout))
+            time.sleep(0.01)
+
+    def done(self):
+        """Rank 0 removes the published id (call after the communicator exists on rank 0)."""
+        if self.rank == 0:
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass
+
+
+def connect(rank, world, rendezvous=None):
+    """The RCCL communicator of this process's rank on the current device: rank 0's id shared through
+    `rendezvous` (default FileRendezvous(rank, world)), then ncclCommInitRank (collective)."""
+    rdzv = rendezvous or FileRendezvous(rank, world)
+    comm = Communicator(rdzv.share_id(), world, rank)
+    rdzv.done()
+    return comm
 
 
 def gather_quaternions(comm: Communicator, x_dev_ptr, batch_local, recv=None, root=0, stream=None):

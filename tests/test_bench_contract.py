@@ -14,13 +14,75 @@ from .conftest import ROOT
 def test_headline_pmc_summary_is_committed_and_matches_config3():
     sys.path.insert(0, ROOT)
     import bench
-    traffic, src = bench.measured_traffic(1 << 20, 10000)
-    assert traffic is not None, "profiles/HEADLINE_PMC must name a committed config-3 PMC summary"
-    path, summary = src
-    assert os.path.exists(path)
-    assert summary["config"] == {"batch": 1 << 20, "records": 10000}
-    assert 0.99 < traffic / (40 * (1 << 20) * 10000) < 1.05   # HBM bytes ~ the 40 B/record algorithmic bytes
+    cited = bench.cited_profile(1 << 20, 10000)
+    assert cited is not None, "profiles/HEADLINE_PMC must name a committed config-3 PMC summary"
+    assert os.path.exists(os.path.join(ROOT, cited["path"]))
+    assert cited["config"] == {"batch": 1 << 20, "records": 10000}
+    # HBM bytes ~ the 40 B/record algorithmic bytes
+    assert 0.99 < cited["hbm_traffic_bytes"] / (40 * (1 << 20) * 10000) < 1.05
     assert bench.workload_name(1 << 20, 10000, False).startswith("config 3")
+    assert bench.workload_name(1 << 20, 10000, False, world=8).startswith("config 4")
+
+
+def _bench():
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench
+
+
+def test_launch_plan_modes():
+    bench = _bench()
+    assert bench.launch_plan(1, {}) == dict(mode="single", rank=0, world=1, devices=[0], first_shard=0)
+    p = bench.launch_plan(8, {})
+    assert p["mode"] == "multi" and p["devices"] == list(range(8)) and p["world"] == 8
+    env = {"RANK": "3", "WORLD_SIZE": "8", "LOCAL_RANK": "3", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29500"}
+    p = bench.launch_plan(8, env)
+    assert p == dict(mode="ranks", rank=3, world=8, devices=[3], first_shard=3)
+    assert bench.launch_plan(1, {}, one_process=True)["mode"] == "multi"
+    p = bench.launch_plan(1, {}, shard_of=(7, 8))
+    assert p["mode"] == "single" and p["first_shard"] == 7 and p["world"] == 1
+    for bad in [lambda: bench.launch_plan(4, env),            # WORLD_SIZE disagrees with --gpus
+                lambda: bench.launch_plan(0, {}),
+                lambda: bench.launch_plan(2, {}, shard_of=(1, 2)),
+                lambda: bench.launch_plan(1, {}, shard_of=(8, 8)),
+                lambda: bench.launch_plan(8, env, shard_of=(1, 8))]:
+        with pytest.raises(SystemExit) as e:
+            bad()
+        assert e.value.code == 2
+
+
+def test_config4_shard_plan_covers_8m_filters():
+    bench = _bench()
+    plan = bench.shard_plan(1 << 20, 8)
+    assert len(plan) == 8 and sum(c for _, c in plan) == 8_388_608
+    assert [f for f, _ in plan] == [r << 20 for r in range(8)]
+    assert all(c == 1 << 20 for _, c in plan)
+    assert plan[7] == (7 << 20, 1 << 20)
+
+
+def test_cpu_share_follows_the_job_share():
+    bench = _bench()
+    use, cores = bench.cpu_share({"OMP_NUM_THREADS": "1"})
+    assert use == 1 and cores >= 1
+    use, cores = bench.cpu_share({})
+    assert use == cores
+
+
+def test_more_gpus_than_visible_exits_nonzero():
+    """--gpus N with fewer than N visible GPUs refuses (status 2, a message), instead of benching fewer."""
+    from poseestimationkf_amd._lib import device_count
+    n = device_count() + 1
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--cpu-baseline", "none"],
+                         capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
+    assert out.returncode == 2, (out.returncode, out.stderr[-2000:])
+    assert "needs %d visible GPU" % n in out.stderr
+    assert out.stdout.strip() == ""
+    # a launcher whose WORLD_SIZE disagrees with --gpus is refused the same way, before any GPU work
+    env.update(RANK="0", WORLD_SIZE="2", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--cpu-baseline", "none"],
+                         capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
+    assert out.returncode == 2 and "WORLD_SIZE=2" in out.stderr
 
 
 @pytest.mark.gpu
@@ -37,4 +99,51 @@ def test_small_bench_run_prints_one_json_line():
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["value"] > 0 and d["dtype"] == "f64"
     assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
+    assert d["valu_roofline"]["bound"] == "fp64-valu-issue" and 0 < d["valu_roofline"]["frac"] < 1
     assert d["parity"]["ok"] and d["parity"]["max_abs_err_vs_oracle"] < 1e-9
+
+
+def _run_bench(*extra, env=None, timeout=110):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--batch", "4096", "--records", "64", "--window", "32",
+           "--steps", "2", "--warmup", "1", "--cpu-baseline", "none", "--parity-samples", "4"] + list(extra)
+    e = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    e.update(env or {})
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=e)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0]), out.stderr
+
+
+@pytest.mark.gpu
+def test_one_process_multi_device_path_on_one_gpu():
+    """The plain `bench.py --gpus N` code path (one process, MultiDeviceEKF, ncclCommInitAll, grouped
+    gather) at N = 1: one JSON line, n_gpus = the devices used, parity of the gathered rows."""
+    d, err = _run_bench("--one-process")
+    assert d["n_gpus"] == 1 and "ncclCommInitAll" in d["config"]["launch"]
+    assert d["parity"]["ok"] and d["parity"]["max_abs_err_vs_oracle"] < 1e-9 and d["parity"]["unit_norm_all"]
+    assert "ncclCommInitAll" in err
+
+
+@pytest.mark.gpu
+def test_launcher_rank_path_world1():
+    """The torchrun code path (RANK / WORLD_SIZE / LOCAL_RANK set; FileRendezvous; RCCL barrier, gather
+    and max-over-ranks time through libpekf) at world size 1, with no PyTorch imported."""
+    d, err = _run_bench("--dist", env={"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0",
+                                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29561"})
+    assert d["n_gpus"] == 1 and d["config"]["launch"].startswith("one process per GPU")
+    assert d["parity"]["ok"] and d["parity"]["max_abs_err_vs_oracle"] < 1e-9
+
+
+@pytest.mark.gpu
+def test_config4_rank7_shard_on_one_gpu():
+    """Config 4's rank-7 workload on the one GPU: filters [7*2^20, 8*2^20) (Philox keyed by their
+    global ids), 10,000 records over the 1,024-record window, through bench.py's rank path with the
+    world-1 RCCL gather; 64 sampled filters re-run by the C oracle (main_file.py:38-47's loop)."""
+    d, err = _run_bench("--batch", str(1 << 20), "--records", "10000", "--window", "1024", "--steps", "1",
+                        "--warmup", "0", "--parity-samples", "64", "--shard-of", "7/8", "--dist", timeout=600)
+    assert d["config"]["first_filter"] == 7 << 20 and d["config"]["filters_per_gpu"] == 1 << 20
+    p = d["parity"]
+    assert p["records"] == 10000 and p["filters"] == 64 and p["shards_covered"] == [7]
+    assert p["global_filter_ids"][0] == 7 << 20 and p["global_filter_ids"][1] == (8 << 20) - 1
+    assert p["max_abs_err_vs_oracle"] < 1e-9 and p["unit_norm_all"]

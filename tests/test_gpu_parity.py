@@ -376,6 +376,41 @@ def test_dropin_returns_fresh_arrays_and_keeps_inputs(eng, monkeypatch):
     assert X1 is not z and P1 is not Pm
 
 
+def test_dropin_north_star_aliases_equal_real_names(eng, monkeypatch):
+    """KalmanFilter.predict / update and Wahba.solve (the north_star's call surface) are the
+    reference's Prediction / Correction / getQuarternion (ExtendedKalmanFilter.py:58,70, Wahba.py:49):
+    bit for bit the same results, and previousT advances the same way."""
+    monkeypatch.syspath_prepend(os.path.join(ROOT, "poseestimationkf_amd", "dropin"))
+    for m in ("ExtendedKalmanFilter", "Wahba", "UtilityFunctions", "_bootstrap"):
+        sys.modules.pop(m, None)
+    from ExtendedKalmanFilter import KalmanFilter
+    from Wahba import Wahba
+    assert KalmanFilter.predict is KalmanFilter.Prediction and KalmanFilter.update is KalmanFilter.Correction
+    assert Wahba.solve is Wahba.getQuarternion
+    acc0, mag0 = [0.0, 0.1, 0.99], [0.5, 0.0, -0.86]
+    k1, k2 = KalmanFilter(0.0, mag0, acc0, 0.5), KalmanFilter(0.0, mag0, acc0, 0.5)
+    for k in (k1, k2):
+        k.setQ(1)
+        k.setR(0.1)
+    rng = np.random.default_rng(11)
+    X1 = X2 = np.asarray([1., 0., 0., 0.])
+    P1 = P2 = np.identity(4)
+    for i in range(20):
+        g, a, m = rng.normal(0, 0.3, 3), rng.normal([0, 0.1, 0.99], 0.02), rng.normal([0.5, 0, -0.86], 0.02)
+        t = 1e7 * (i + 1)
+        z1, Pm1, K1 = k1.Prediction(g, t, X1, P1)
+        z2, Pm2, K2 = k2.predict(g, t, X2, P2)
+        assert np.array_equal(z1, z2) and np.array_equal(Pm1, Pm2) and np.array_equal(K1, K2)
+        assert k1.previousT == k2.previousT == t
+        X1, P1 = k1.Correction(m, a, z1, Pm1, K1)
+        X2, P2 = k2.update(m, a, z2, Pm2, K2)
+        assert np.array_equal(X1, X2) and np.array_equal(P1, P2)
+        w = Wahba(acc0, mag0)
+        assert np.array_equal(w.solve(a, m, 0.5, 0.5), w.getQuarternion(a, m, 0.5, 0.5))
+    want = npo.correct(m, a, z1, Pm1, K1, acc0, mag0)
+    assert _maxerr(X2, want[0]) < 1e-13
+
+
 @pytest.mark.gpu
 def test_fused_measurement_far_from_prediction(eng):
     """Filters started at random attitudes, so early Wahba measurements Y lie anywhere relative to

@@ -1,16 +1,23 @@
-"""N > 1 path on CPU: world_size-2 gloo ranks rendezvous exactly as bench.py does (rank 0's
-128-byte RCCL id broadcast by shard.exchange_unique_id over the gloo group), each takes a
-contiguous filter shard and runs it (the C oracle stands in for the device here -- test only),
-and the shards' final quaternions, concatenated in rank order as pekf_gather_dev lays them out on
-the root, equal a single-process run.  The RCCL gather itself needs GPUs: tests/test_gpu_parity.py
-runs it through libpekf at world size 1 (and bench.py --dist on the box)."""
+"""N > 1 path on CPU.
+
+* Torch-free rendezvous (shard.FileRendezvous, what bench.py uses under torchrun): two processes
+  children of one parent -- as torchrun's ranks are -- share rank 0's 128-byte RCCL id through a file,
+  with no PyTorch imported; a file from another job (another key) or a torn / foreign file is never
+  taken for the id.
+* world_size-2 gloo ranks: each takes its contiguous filter shard, runs it (the C oracle stands in
+  for the device here -- test only), and the shards' final quaternions, concatenated in rank order
+  as pekf_gather_dev lays them out on the root, equal a single-process run.  gloo only stands in
+  for the RCCL gather (which needs GPUs: tests/test_gpu_comm.py and bench.py on the box)."""
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
 
 from poseestimationkf_amd import shard, synth
+
+ID = bytes(range(128))
 
 
 def _free_port():
@@ -21,19 +28,84 @@ def _free_port():
     return port
 
 
-def _rank_main(rank, world, port, global_batch, window, q):
+def _shard_rows(rank, world, global_batch, window):
+    from oracle import oracle_c
+    first, count = shard.shard_range(global_batch, rank, world)
+    X, _, _ = oracle_c.run(synth.generate(np.arange(first, first + count), window))
+    return X
+
+
+def _rdzv_rank(rank, world, port, directory, global_batch, window, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    uid = shard.FileRendezvous(rank, world, directory=directory, timeout=60).share_id(make_id=lambda: ID)
+    rows = _shard_rows(rank, world, global_batch, window)
+    q.put((rank, uid, rows, "torch" in sys.modules))
+
+
+def test_file_rendezvous_two_processes_torch_free(tmp_path):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rdzv_rank, args=(r, 2, port, str(tmp_path), 16, 24, q)) for r in (1, 0)]
+    for p in procs:
+        p.start()
+    got = dict((r, (uid, rows, torch)) for r, uid, rows, torch in (q.get(timeout=240) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0][0] == ID and got[1][0] == ID            # rank 1 read rank 0's id
+    assert not got[0][2] and not got[1][2]                # no PyTorch in either rank
+    X, _, _ = __import__("oracle.oracle_c", fromlist=["run"]).run(synth.generate(np.arange(16), 24))
+    assert np.array_equal(np.concatenate([got[0][1], got[1][1]]), X)
+
+
+def test_file_rendezvous_key_isolation_and_cleanup(tmp_path):
+    r0 = shard.FileRendezvous(0, 2, key="jobA", directory=str(tmp_path))
+    assert r0.share_id(make_id=lambda: ID) == ID
+    assert os.path.exists(r0.path)
+    # another job's file (other key) is never read
+    with pytest.raises(TimeoutError):
+        shard.FileRendezvous(1, 2, key="jobB", directory=str(tmp_path), timeout=0.2).share_id()
+    assert shard.FileRendezvous(1, 2, key="jobA", directory=str(tmp_path), timeout=5).share_id() == ID
+    # a foreign or torn file is not taken for the id
+    bad = shard.FileRendezvous(1, 2, key="jobC", directory=str(tmp_path), timeout=0.2)
+    with open(bad.path, "wb") as fh:
+        fh.write(b"PEKFRDZV1" + ID[:100])
+    with pytest.raises(TimeoutError):
+        bad.share_id()
+    r0.done()
+    assert not os.path.exists(r0.path)
+    # world 1 needs no file at all; a bad id size is refused
+    solo = shard.FileRendezvous(0, 1, key="solo", directory=str(tmp_path))
+    assert solo.share_id(make_id=lambda: ID) == ID and not os.path.exists(solo.path)
+    with pytest.raises(RuntimeError):
+        shard.FileRendezvous(0, 2, key="short", directory=str(tmp_path)).share_id(make_id=lambda: b"x")
+    with pytest.raises(ValueError):
+        shard.FileRendezvous(2, 2)
+
+
+def test_default_key_is_shared_by_siblings_only(monkeypatch):
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", "29999")
+    monkeypatch.delenv("PEKF_RDZV_KEY", raising=False)
+    a, b = shard.FileRendezvous(0, 2), shard.FileRendezvous(1, 2)
+    assert a.path == b.path and str(os.getppid()) in a.path
+    monkeypatch.setenv("MASTER_PORT", "29998")
+    assert shard.FileRendezvous(1, 2).path != a.path
+    monkeypatch.setenv("PEKF_RDZV_KEY", "k/../x")
+    assert os.path.basename(shard.FileRendezvous(1, 2).path) == "pekf-rdzv-k_.._x.id"
+
+
+def _gloo_rank(rank, world, port, directory, global_batch, window, q):
     import torch
     import torch.distributed as dist
 
-    from oracle import oracle_c
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    uid = shard.FileRendezvous(rank, world, directory=directory, timeout=60).share_id(make_id=lambda: ID)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        uid = shard.exchange_unique_id(rank, world, make_id=lambda: bytes(range(128)))
-        assert uid == bytes(range(128))  # every rank holds rank 0's id (a failure fails the exit code)
-        first, count = shard.shard_range(global_batch, rank, world)
-        rec = synth.generate(np.arange(first, first + count), window)
-        X, _, _ = oracle_c.run(rec)
+        X = _shard_rows(rank, world, global_batch, window)
         bufs = [torch.empty_like(torch.from_numpy(X)) for _ in range(world)] if rank == 0 else None
         dist.gather(torch.from_numpy(X), gather_list=bufs, dst=0)  # stands in for RCCL (test only)
         if rank == 0:
@@ -46,18 +118,20 @@ def test_shard_ranges_cover_batch_exactly():
     ranges = [shard.shard_range(1 << 20, r, 8) for r in range(8)]
     assert ranges[0] == (0, 1 << 17) and ranges[-1] == (7 << 17, 1 << 17)
     assert sum(c for _, c in ranges) == 1 << 20
+    c4 = [shard.shard_range(8 << 20, r, 8) for r in range(8)]
+    assert c4[7] == (7 << 20, 1 << 20) and sum(c for _, c in c4) == 8_388_608
     with pytest.raises(ValueError):
         shard.shard_range(10, 0, 3)
 
 
-def test_two_rank_gather_equals_single_process():
+def test_two_rank_gloo_gather_equals_single_process(tmp_path):
     import multiprocessing as mp
 
     from oracle import oracle_c
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, 16, 24, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gloo_rank, args=(r, 2, port, str(tmp_path), 16, 24, q)) for r in range(2)]
     for p in procs:
         p.start()
     uid, got = q.get(timeout=240)
@@ -65,6 +139,6 @@ def test_two_rank_gather_equals_single_process():
         p.join(timeout=60)
         assert p.exitcode == 0
     X, _, _ = oracle_c.run(synth.generate(np.arange(16), 24))
-    assert uid == bytes(range(128))
+    assert uid == ID
     assert got.shape == (16, 4)
     assert np.array_equal(got, X)
