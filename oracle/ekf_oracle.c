@@ -262,11 +262,14 @@ void oracle_correct(const double mag[3], const double acc[3], const double z[4],
 /*
  * Run filters over a packed per-filter record stream (the layout of synth.Records):
  *   rec[f][t] = {gx,gy,gz, ax,ay,az, mx,my,mz} as float, dtw[f][t] = dt_ns | (missing << 31)
+ * A dt field of all ones (0x7FFFFFFF, the stream's escape) takes the record's dt from the float64
+ * side plane dtx[f][t] (may be NULL when no record is escaped): any T - previousT, as at
+ * ExtendedKalmanFilter.py:62.
  * Step t of the run reads record (step0 + t) % window.  X[f][4], P[f][16] in/out.
  * traj (optional, may be NULL): traj[f][t][4].
  */
 int oracle_run(int64_t n_filters, int64_t n_steps, int64_t window, int64_t step0,
-               const float *rec, const uint32_t *dtw, const double *acc0, const double *mag0,
+               const float *rec, const uint32_t *dtw, const double *dtx, const double *acc0, const double *mag0,
                double q, double r, double *X, double *P, double *traj)
 {
     int status = 0;
@@ -284,7 +287,8 @@ int oracle_run(int64_t n_filters, int64_t n_steps, int64_t window, int64_t step0
             const double g[3] = {rc[0], rc[1], rc[2]};
             const double a[3] = {rc[3], rc[4], rc[5]};
             const double m[3] = {rc[6], rc[7], rc[8]};
-            const double dt = (double)(word & 0x7FFFFFFFu);
+            const double dt = ((word & 0x7FFFFFFFu) == 0x7FFFFFFFu && dtx) ? dtx[f * window + row]
+                                                                            : (double)(word & 0x7FFFFFFFu);
             if (oracle_predict(g, dt, x, p, Q, R, z, pm, k)) { status |= 1; break; }
             if (word & 0x80000000u) {
                 memcpy(x, z, sizeof(x));

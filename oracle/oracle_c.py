@@ -41,7 +41,7 @@ def lib():
         L.oracle_wahba_rotation.argtypes = [_dp, _dp, _dp, _dp, ctypes.c_double, ctypes.c_double, _dp]
         L.oracle_wahba_quat.argtypes = [_dp, _dp, _dp, _dp, ctypes.c_double, ctypes.c_double, _dp]
         L.oracle_rotm_to_quat.argtypes = [_dp, _dp]
-        L.oracle_run.argtypes = [ctypes.c_int64] * 4 + [_fp, _up, _dp, _dp, ctypes.c_double,
+        L.oracle_run.argtypes = [ctypes.c_int64] * 4 + [_fp, _up, _dp, _dp, _dp, ctypes.c_double,
                                                          ctypes.c_double, _dp, _dp, _dp]
         _lib = L
     return _lib
@@ -124,12 +124,15 @@ def run(records, n_steps=None, step0=0, q=1.0, r=0.1, X=None, P=None, want_traj=
     rec[..., 3:6] = records.acc.transpose(1, 0, 2)
     rec[..., 6:9] = records.mag.transpose(1, 0, 2)
     dtw = np.ascontiguousarray(records.dtw.T, dtype=np.uint32)
+    dtx_rec = getattr(records, "dtx", None)
+    dtx = None if dtx_rec is None else np.ascontiguousarray(np.asarray(dtx_rec, np.float64).T)
     Xs = np.tile(np.array([1.0, 0, 0, 0]), (K, 1)) if X is None else np.array(X, np.float64, copy=True)
     Ps = np.tile(np.eye(4), (K, 1, 1)) if P is None else np.array(P, np.float64, copy=True)
     traj = np.empty((K, n_steps, 4)) if want_traj else None
     acc0 = _d(records.acc0)
     mag0 = _d(records.mag0)
     st = lib().oracle_run(K, n_steps, W, step0, rec.ctypes.data_as(_fp), dtw.ctypes.data_as(_up),
+                          _p(dtx) if dtx is not None else None,
                           _p(acc0), _p(mag0), float(q), float(r), _p(Xs), _p(Ps),
                           _p(traj) if want_traj else None)
     if st:

@@ -23,6 +23,8 @@ PEKF_ERR_COMM = 6
 MISSING_MAG_BIT = 0x80000000
 RUN_MIXED_PRECISION = 0x1
 RUN_STATE_SOA = 0x2
+DT_ESCAPE = 0x7FFFFFFF
+EV_TIME_EVENTS = 0x1
 
 
 class PekfError(RuntimeError):
@@ -78,6 +80,8 @@ SIGNATURES = {
     "pekf_wahba_quaternion": [_i64] + [_vp] * 7,
     "pekf_rotmat_to_quat": [_i64, _vp, _vp],
     "pekf_run_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp, _u32, _vp],
+    "pekf_run_ext_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp, _u32,
+                         _vp],
     "pekf_reset_state_dev": [_i64, _vp, _vp, _vp],
     "pekf_state_layout_dev": [_i64, _vp, _vp, _vp, _vp, _int, _vp],
     "pekf_filter_create": [_i64, _vp, _vp, _dbl, _dbl, _vp, _u32, ctypes.POINTER(_vp)],
@@ -90,14 +94,18 @@ SIGNATURES = {
     "pekf_filter_update": [_vp] * 7,
     "pekf_filter_update_dev": [_vp] * 8,
     "pekf_filter_run": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "pekf_filter_run_ext": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "pekf_gyro_chain_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "pekf_wahba_stream_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp],
     "pekf_quat_to_rpy": [_i64, _vp, _vp],
     "pekf_frontend_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "pekf_frontend_ext_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp],
     "pekf_frontend_init_dev": [_i64, _i64, _vp, _vp, _int, _vp, _vp, _vp, _vp, _vp],
     "pekf_live_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _vp, _vp, _dbl, _dbl, _vp, _vp, _vp, _vp],
+    "pekf_live_ext_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _vp, _vp, _dbl, _dbl, _vp, _vp, _u32, _vp, _vp],
     "pekf_log_scan": [ctypes.c_char_p, ctypes.POINTER(_i64)],
     "pekf_log_read": [ctypes.c_char_p, _i64, _vp, _vp, _vp, _vp, _dp, _dp, _dp],
+    "pekf_log_read_ext": [ctypes.c_char_p, _i64, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_i64), _dp, _dp, _dp],
     "pekf_quat_to_rpy_dev": [_i64, _vp, _vp, _vp],
     "pekf_synth_dev": [_i64, _i64, _i64, _u32, _int, _dp, _dbl, _vp, _vp, _vp, _vp, _vp],
     "pekf_comm_version": [_ip],

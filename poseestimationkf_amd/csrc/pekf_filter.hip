@@ -275,9 +275,16 @@ int pekf_filter_update(pekf_filter *f, const double *gyro, const int64_t *t_ns, 
 int pekf_filter_run(pekf_filter *f, int64_t n_steps, int64_t window, int64_t step0, const void *plane_gd,
                     const void *plane_am, const void *plane_my, double *traj, const int32_t *counts,
                     void *stream) {
+    return pekf_filter_run_ext(f, n_steps, window, step0, plane_gd, plane_am, plane_my, nullptr, traj, counts,
+                               stream);
+}
+
+int pekf_filter_run_ext(pekf_filter *f, int64_t n_steps, int64_t window, int64_t step0, const void *plane_gd,
+                        const void *plane_am, const void *plane_my, const double *dt_ext, double *traj,
+                        const int32_t *counts, void *stream) {
     if (int st = check_handle(f)) return st;
-    return pekf_run_dev(f->batch, n_steps, window, step0, plane_gd, plane_am, plane_my, f->refs, f->X, f->P, f->q,
-                        f->r, traj, counts, f->flags, stream);
+    return pekf_run_ext_dev(f->batch, n_steps, window, step0, plane_gd, plane_am, plane_my, dt_ext, f->refs, f->X,
+                            f->P, f->q, f->r, traj, counts, f->flags, stream);
 }
 
 }  // extern "C"

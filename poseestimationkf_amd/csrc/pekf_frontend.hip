@@ -18,12 +18,16 @@ constexpr int kFeBlock = 256;
 #define PEKF_FE_RING 9
 #endif
 
+// TE: the event planes may hold time events (Phase3::event).  dtx (may be null): the window's dt side
+// plane [r_max][batch]; an escaped record's float64 dt goes there (err bit 4), else err bit 1.
+template <bool TE>
 __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_events,
                                                        const float4 *__restrict__ ev,
                                                        const double *__restrict__ init,
                                                        const int64_t *__restrict__ t_init, double alpha,
                                                        int64_t r_max, float4 *__restrict__ gd,
                                                        float4 *__restrict__ am, float2 *__restrict__ my,
+                                                       double *__restrict__ dtx,
                                                        int32_t *__restrict__ counts, double *__restrict__ refs,
                                                        int *__restrict__ err) {
     const int64_t b = (int64_t)blockIdx.x * kFeBlock + threadIdx.x;
@@ -42,12 +46,15 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
     constexpr int kFlush = 3;
     auto flush = [&]() {
         if (!fe.pend) return;
-        const Rec rc = fe.emit(bad);
+        bool esc;
+        const Rec rc = fe.emit(esc);
+        if (esc) bad |= dtx ? 4 : 1;
         if (r < r_max) {
             const int64_t o = r * batch + b;
             gd[o] = rc.gd;
             am[o] = rc.am;
             my[o] = rc.my;
+            if (esc && dtx) dtx[o] = fe.p.dt;
         } else {
             bad |= 2;  // more records than the output window holds
         }
@@ -74,7 +81,7 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
                 if (e0 + k >= n_events) break;  // uniform
                 const float4 v4 = ring[k];
                 ring[k] = load(e0 + k + kRing);
-                fe.event(v4);
+                fe.event<TE>(v4);
                 if ((k + 1) % kFlush == 0) flush();
             }
         }
@@ -121,6 +128,10 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend_init(int64_t batch, int64
             const float4 v4 = r[k];
             const uint32_t word = __float_as_uint(v4.w);
             const int ty = (int)(word & 3u);
+            if (word == PEKF_EV_TIME) {  // a time event: the clock moves, nothing else happens
+                t += (int64_t)time_step(v4);
+                continue;
+            }
             t += (int64_t)(word >> 2);
             if (!(done[0] && done[1] && done[2])) {
                 if (ty <= 2) {
@@ -205,18 +216,34 @@ extern "C" int pekf_frontend_init_dev(int64_t batch, int64_t n_events, const voi
     return PEKF_OK;
 }
 
-extern "C" int pekf_frontend_dev(int64_t batch, int64_t n_events, const void *ev_planes, const double *init,
-                                 const int64_t *t_init, double alpha, int64_t r_max, void *plane_gd, void *plane_am, void *plane_my, int32_t *counts, double *refs,
-                                 int *dev_error, void *stream) {
+extern "C" int pekf_frontend_ext_dev(int64_t batch, int64_t n_events, const void *ev_planes, const double *init,
+                                     const int64_t *t_init, double alpha, int64_t r_max, void *plane_gd,
+                                     void *plane_am, void *plane_my, double *dt_ext, int32_t *counts, double *refs,
+                                     uint32_t flags, int *dev_error, void *stream) {
     PEKF_CHECK_ARG(batch >= 0 && n_events >= 0 && r_max >= 0, "negative size");
+    PEKF_CHECK_ARG((flags & ~PEKF_EV_TIME_EVENTS) == 0, "unknown flags");
     if (batch == 0) return PEKF_OK;
     PEKF_CHECK_ARG(ev_planes && init && t_init && plane_gd && plane_am && plane_my && counts && refs,
                    "null pointer");
-    hipLaunchKernelGGL(k_frontend, dim3(grid_for(batch, kFeBlock)), dim3(kFeBlock), 0, as_stream(stream), batch,
-                       n_events, static_cast<const float4 *>(ev_planes), init, t_init, alpha, r_max,
-                       static_cast<float4 *>(plane_gd), static_cast<float4 *>(plane_am),
-                       static_cast<float2 *>(plane_my), counts, refs, dev_error);
+    const auto *ev = static_cast<const float4 *>(ev_planes);
+    auto *gd = static_cast<float4 *>(plane_gd);
+    auto *am = static_cast<float4 *>(plane_am);
+    auto *my = static_cast<float2 *>(plane_my);
+    const dim3 grid(grid_for(batch, kFeBlock)), block(kFeBlock);
+    if (flags & PEKF_EV_TIME_EVENTS)
+        hipLaunchKernelGGL(k_frontend<true>, grid, block, 0, as_stream(stream), batch, n_events, ev, init, t_init,
+                           alpha, r_max, gd, am, my, dt_ext, counts, refs, dev_error);
+    else
+        hipLaunchKernelGGL(k_frontend<false>, grid, block, 0, as_stream(stream), batch, n_events, ev, init, t_init,
+                           alpha, r_max, gd, am, my, dt_ext, counts, refs, dev_error);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_frontend");
     return PEKF_OK;
+}
+
+extern "C" int pekf_frontend_dev(int64_t batch, int64_t n_events, const void *ev_planes, const double *init,
+                                 const int64_t *t_init, double alpha, int64_t r_max, void *plane_gd, void *plane_am,
+                                 void *plane_my, int32_t *counts, double *refs, int *dev_error, void *stream) {
+    return pekf_frontend_ext_dev(batch, n_events, ev_planes, init, t_init, alpha, r_max, plane_gd, plane_am, plane_my,
+                                 nullptr, counts, refs, 0u, dev_error, stream);
 }

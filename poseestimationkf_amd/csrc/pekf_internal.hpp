@@ -110,7 +110,8 @@ int launch_update(int64_t batch, const double *gyro, const int64_t *t_ns, const 
 // Multi-record fused launches (pekf_run_multi.hip, compiled with the max-ILP scheduler): every
 // k_run<TRAJ, MIXED, SOA, COUNTS, ONE = false> variant; arguments checked by pekf_run_dev.
 int launch_run_multi(int64_t batch, int64_t n_steps, int64_t window, int64_t step0, const float4 *gd,
-                     const float4 *am, const float2 *my, const double *refs, double *X, double *P, double q,
-                     double r, double *traj, const int32_t *counts, bool mixed, bool soa, hipStream_t stream);
+                     const float4 *am, const float2 *my, const double *dtx, const double *refs, double *X,
+                     double *P, double q, double r, double *traj, const int32_t *counts, bool mixed, bool soa,
+                     hipStream_t stream);
 
 }  // namespace pekf

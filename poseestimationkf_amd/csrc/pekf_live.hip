@@ -48,21 +48,29 @@ namespace pekf {
 // push or pop is a few address operations and three LDS accesses.  (Held in registers -- slots as
 // separate variables, a push selecting its slot -- the queue cost 40 selects per push and registers
 // the kernel does not have: profiles/r2/live/variants/live_ab*.log.)
+// A record whose dt does not fit its dt word (PEKF_DT_ESCAPE, a pause of 2^31 ns or more) keeps its
+// float64 dt in the slot's side entry dt[slot][lane], written and read only for such a record.
 template <int Q>
 struct LdsQueue {
     float4 (*gd)[kRunBlock];
     float4 (*am)[kRunBlock];
     float2 (*my)[kRunBlock];
+    double (*dt)[kRunBlock];
     int head = 0, n = 0;
-    __device__ __forceinline__ void push(const Rec &r) {
+    __device__ __forceinline__ void push(const Rec &r, bool esc, double dtv) {
         const int slot = head + n < Q ? head + n : head + n - Q;
         gd[slot][threadIdx.x] = r.gd;
         am[slot][threadIdx.x] = r.am;
         my[slot][threadIdx.x] = r.my;
+        if (esc) dt[slot][threadIdx.x] = dtv;
         ++n;
     }
-    __device__ __forceinline__ Rec pop() {
+    // the oldest record and its dt in ns
+    __device__ __forceinline__ Rec pop(double &dtv) {
         const Rec r = {gd[head][threadIdx.x], am[head][threadIdx.x], my[head][threadIdx.x]};
+        const uint32_t word = __float_as_uint(r.gd.w) & PEKF_DT_MASK;
+        dtv = (double)word;
+        if (word == PEKF_DT_ESCAPE) dtv = dt[head][threadIdx.x];
         if (n > 0) {
             head = head + 1 < Q ? head + 1 : 0;
             --n;
@@ -71,10 +79,12 @@ struct LdsQueue {
     }
 };
 
+// TE: the event planes may hold time events (Phase3::event).
+template <bool TE>
 __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
     int64_t batch, int64_t n_events, const float4 *__restrict__ ev, const double *__restrict__ init,
     const int64_t *__restrict__ t_init, double alpha, double qs, double rs, double *__restrict__ Xio,
-    double *__restrict__ Pio, int32_t *__restrict__ counts, double *__restrict__ refs, int *__restrict__ err) {
+    double *__restrict__ Pio, int32_t *__restrict__ counts, double *__restrict__ refs) {
     constexpr int kRing = PEKF_LIVE_RING, kFlush = 3, kQueue = PEKF_LIVE_QUEUE, kQuorum = PEKF_LIVE_QUORUM;
     constexpr int kPush = kRing / kFlush;  // records a lane can complete within one block
     static_assert(kRing % kFlush == 0, "the ring depth must be a multiple of the emit period");
@@ -107,21 +117,21 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
 
     __shared__ float4 q_gd[kQueue][kRunBlock], q_am[kQueue][kRunBlock];
     __shared__ float2 q_my[kQueue][kRunBlock];
+    __shared__ double q_dt[kQueue][kRunBlock];
     LdsQueue<kQueue> queue;
-    queue.gd = q_gd; queue.am = q_am; queue.my = q_my;
+    queue.gd = q_gd; queue.am = q_am; queue.my = q_my; queue.dt = q_dt;
     int32_t applied = 0;
-    int bad = 0;
     // One filter step for every lane with a queued record: its oldest, Prediction + Correction with
     // the multi-record kernel's arithmetic (the first record of the launch from the loaded |X|^2,
     // every later one lazy; front-end records always carry a magnetometer sample).
     auto filter_step = [&]() {
         const bool has = queue.n > 0;
-        const Rec cur = queue.pop();
+        double dt;
+        const Rec cur = queue.pop(dt);
         OmodMode mode;
         mode.enter();
         if (has) {
             const double gy[3] = {cur.gd.x, cur.gd.y, cur.gd.z};
-            const double dt = (double)(__float_as_uint(cur.gd.w) & 0x7FFFFFFFu);
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
             if (applied == 0)
@@ -133,7 +143,11 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
         mode.leave();
     };
     auto flush = [&]() {
-        if (fe.pend) queue.push(fe.emit(bad));
+        if (fe.pend) {
+            bool esc;
+            const Rec rc = fe.emit(esc);
+            queue.push(rc, esc, fe.p.dt);
+        }
     };
 
     // Events stream through a register ring of kRing rows loaded kRing events ahead (the loop is
@@ -153,7 +167,7 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
                 if (e0 + k >= n_events) break;  // uniform
                 const float4 v4 = ring[k];
                 ring[k] = load(e0 + k + kRing);
-                fe.event(v4);
+                fe.event<TE>(v4);
                 if ((k + 1) % kFlush == 0) flush();
             }
             flush();  // a record completed in a trailing partial block (nothing pending after a full one)
@@ -169,7 +183,6 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
         }
     }
     counts[b] = applied;
-    if (bad && err) atomicOr(err, bad);
     if (applied == 0) return;  // no record: the state is left as it was (as pekf_run_dev with counts)
     from_ref_basis(Wr, x, P, rs);
     store_state<false>(Xio, Pio, b, batch, x, P);
@@ -179,19 +192,33 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
 
 using namespace pekf;
 
-extern "C" int pekf_live_dev(int64_t batch, int64_t n_events, const void *ev_planes, const double *init,
-                             const int64_t *t_init, double alpha, double *X, double *P, double q, double r,
-                             int32_t *counts, double *refs, int *dev_error, void *stream) {
+extern "C" int pekf_live_ext_dev(int64_t batch, int64_t n_events, const void *ev_planes, const double *init,
+                                 const int64_t *t_init, double alpha, double *X, double *P, double q, double r,
+                                 int32_t *counts, double *refs, uint32_t flags, int *dev_error, void *stream) {
     PEKF_CHECK_ARG(batch >= 0 && n_events >= 0, "negative size");
+    PEKF_CHECK_ARG((flags & ~PEKF_EV_TIME_EVENTS) == 0, "unknown flags");
     if (batch == 0) return PEKF_OK;
     PEKF_CHECK_ARG(batch < ((int64_t)1 << 28), "batch must be < 2^28 filters per launch");
     PEKF_CHECK_ARG(ev_planes && init && t_init && X && P && counts && refs, "null pointer");
     PEKF_CHECK_ARG((uintptr_t)ev_planes % 16 == 0, "misaligned event planes");
     PEKF_CHECK_ARG(r > 0.0, "r must be > 0 (S = P- + rI must be SPD)");
-    hipLaunchKernelGGL(k_live, dim3(grid_for(batch, kRunBlock)), dim3(kRunBlock), 0, as_stream(stream), batch,
-                       n_events, static_cast<const float4 *>(ev_planes), init, t_init, alpha, q, r, X, P, counts,
-                       refs, dev_error);
+    (void)dev_error;  // every record's dt is applied (escaped ones from the queue's side entries)
+    const auto *ev = static_cast<const float4 *>(ev_planes);
+    const dim3 grid(grid_for(batch, kRunBlock)), block(kRunBlock);
+    if (flags & PEKF_EV_TIME_EVENTS)
+        hipLaunchKernelGGL(k_live<true>, grid, block, 0, as_stream(stream), batch, n_events, ev, init, t_init, alpha, q,
+                           r, X, P, counts, refs);
+    else
+        hipLaunchKernelGGL(k_live<false>, grid, block, 0, as_stream(stream), batch, n_events, ev, init, t_init, alpha,
+                           q, r, X, P, counts, refs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_live");
     return PEKF_OK;
+}
+
+extern "C" int pekf_live_dev(int64_t batch, int64_t n_events, const void *ev_planes, const double *init,
+                             const int64_t *t_init, double alpha, double *X, double *P, double q, double r,
+                             int32_t *counts, double *refs, int *dev_error, void *stream) {
+    return pekf_live_ext_dev(batch, n_events, ev_planes, init, t_init, alpha, X, P, q, r, counts, refs, 0u, dev_error,
+                             stream);
 }

@@ -113,8 +113,8 @@ int pekf_log_scan(const char *path, int64_t *n_records) {
     return validate(path, c, n_records);
 }
 
-int pekf_log_read(const char *path, int64_t n_records, float *gyro, float *acc, float *mag, uint32_t *dtw,
-                  double *acc0, double *mag0, double *t0) {
+int pekf_log_read_ext(const char *path, int64_t n_records, float *gyro, float *acc, float *mag, uint32_t *dtw,
+                      double *dt_ext, int64_t *n_escaped, double *acc0, double *mag0, double *t0) {
     if (!path || !gyro || !acc || !mag || !dtw || !acc0 || !mag0)
         return pekf::set_error(PEKF_ERR_INVALID, "null pointer");
     LogColumns c;
@@ -129,21 +129,36 @@ int pekf_log_read(const char *path, int64_t n_records, float *gyro, float *acc, 
         mag0[k] = c.mag0[k];
     }
     if (t0) *t0 = c.T[0];
+    int64_t escaped = 0;
     for (int64_t i = 0; i < n_records; ++i) {
         for (int k = 0; k < 3; ++k) {
             gyro[3 * i + k] = (float)c.gyro[3 * i + k];
             acc[3 * i + k] = (float)c.acc1[3 * i + k];
             mag[3 * i + k] = (float)c.mag1[3 * i + k];
         }
+        // T - previousT exactly as the reference forms it (ExtendedKalmanFilter.py:62): float64 difference
         const double dt = c.T[i + 1] - c.T[i];
-        if (!(dt >= 0.0 && dt < 2147483648.0 && dt == std::floor(dt)))
+        const bool fits = dt >= 0.0 && dt < (double)PEKF_DT_ESCAPE && dt == std::floor(dt);
+        if (dt_ext) dt_ext[i] = fits ? 0.0 : dt;
+        if (fits) {
+            dtw[i] = (uint32_t)dt;
+        } else if (dt_ext) {
+            dtw[i] = PEKF_DT_ESCAPE;  // the record's dt is dt_ext[i]
+            ++escaped;
+        } else {
             return pekf::set_error(PEKF_ERR_INVALID,
-                                   "%s: record %lld has dt = %.17g ns, not an integer in [0, 2^31) "
-                                   "(the 40 B record carries dt as a 31-bit ns count)",
+                                   "%s: record %lld has dt = %.17g ns, not an integer in [0, 2^31 - 1) "
+                                   "(use pekf_log_read_ext: the dt side plane takes any gap)",
                                    path, (long long)i, dt);
-        dtw[i] = (uint32_t)dt;
+        }
     }
+    if (n_escaped) *n_escaped = escaped;
     return PEKF_OK;
+}
+
+int pekf_log_read(const char *path, int64_t n_records, float *gyro, float *acc, float *mag, uint32_t *dtw,
+                  double *acc0, double *mag0, double *t0) {
+    return pekf_log_read_ext(path, n_records, gyro, acc, mag, dtw, nullptr, nullptr, acc0, mag0, t0);
 }
 
 }  // extern "C"

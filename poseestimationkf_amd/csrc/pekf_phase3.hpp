@@ -20,6 +20,12 @@ namespace pekf {
 
 enum : uint32_t { kEvAcc = 0, kEvGyro = 1, kEvMag = 2 };
 
+// The clock step of a time event (word == PEKF_EV_TIME): an integer ns count held as a float64 whose low
+// and high halves are the event's x and y bits.
+__device__ __forceinline__ double time_step(const float4 v4) {
+    return __hiloint2double(__float_as_int(v4.y), __float_as_int(v4.x));
+}
+
 struct V3 {
     double x, y, z;
 };
@@ -110,12 +116,18 @@ struct Phase3 {
     //   after it: acc -> acc_1, mag -> mag_1 (set); a new gyro replaces the gyro and shifts a set
     //   acc_1 -> acc_0 / mag_1 -> mag_0, clearing both flags.
     // on_done(const RawRec &) runs for a lane whose event completes a record.
-    template <typename F>
+    // TE: the stream may hold time events (word == PEKF_EV_TIME: no sample, the clock moves by the
+    // float64 in the x / y bits -- a pause of 2^30 ns or more, or a clock stepping back); without TE
+    // such an event moves nothing.  Either way type 3 matches no sensor, so the state machine skips it.
+    template <bool TE = false, typename F>
     __device__ __forceinline__ void event(const float4 v4, F &&on_done) {
 #pragma clang fp contract(fast)
         const uint32_t word = __float_as_uint(v4.w);
         const uint32_t ty = word & 3u;
-        t += (double)(word >> 2);
+        if constexpr (TE)
+            t += word == PEKF_EV_TIME ? time_step(v4) : (double)(word >> 2);
+        else
+            t += (double)(word >> 2);
         const bool isA = ty == kEvAcc, isM = ty == kEvMag, isG = ty == kEvGyro;
         const bool gs = gyro_set;
         const F3 v = {v4.x, v4.y, v4.z};
@@ -153,21 +165,24 @@ struct Phase3 {
         mag1_set = m1s && !done;
     }
 
-    // the deferring form: the completed record's inputs wait in p (pend) for emit(bad)
+    // the deferring form: the completed record's inputs wait in p (pend) for emit(esc)
+    template <bool TE = false>
     __device__ __forceinline__ void event(const float4 v4) {
-        event(v4, [&](const RawRec &r) {
+        event<TE>(v4, [&](const RawRec &r) {
             pend = true;
             p = r;
         });
     }
-    __device__ __forceinline__ Rec emit(int &bad) {
+    // the pending record; its dt stays in p.dt (the float64 an escaped record needs)
+    __device__ __forceinline__ Rec emit(bool &esc) {
         pend = false;
-        return emit(p, bad);
+        return emit(p, esc);
     }
 
     // A captured record, in the order they complete: interpolation, normalisation, low-pass, f32
-    // packing.  bad |= 1 if its dt does not fit the 31-bit dt word of the stream.
-    __device__ __forceinline__ Rec emit(const RawRec &q, int &bad) {
+    // packing.  esc: its dt does not fit the dt word (not in [0, 2^31 - 1) ns): the word is
+    // PEKF_DT_ESCAPE and the caller keeps q.dt beside the record (pekf.h).
+    __device__ __forceinline__ Rec emit(const RawRec &q, bool &esc) {
 #pragma clang fp contract(fast)
         // Parser::LinearInterpolationSensor (:259-267): (y2 - y1) / (t2 - t1) * (t3 - t1) + y1, the
         // division taken as one reciprocal.  Timestamps are integer ns held in doubles (exact below
@@ -179,10 +194,10 @@ struct Phase3 {
         const V3 m = normalised({(m1.x - m0.x) * fm + m0.x, (m1.y - m0.y) * fm + m0.y, (m1.z - m0.z) * fm + m0.z});
         lpf_mag = {alpha * m.x + beta * lpf_mag.x, alpha * m.y + beta * lpf_mag.y, alpha * m.z + beta * lpf_mag.z};
         lpf_acc = {alpha * a.x + beta * lpf_acc.x, alpha * a.y + beta * lpf_acc.y, alpha * a.z + beta * lpf_acc.z};
-        if (!(q.dt >= 0.0 && q.dt < 2147483648.0)) bad |= 1;
+        esc = !(q.dt >= 0.0 && q.dt < (double)PEKF_DT_ESCAPE);
         Rec r;
         r.gd = make_float4((float)q.gyro.x, (float)q.gyro.y, (float)q.gyro.z,
-                           __uint_as_float((uint32_t)fmin(fmax(q.dt, 0.0), 2147483647.0)));
+                           __uint_as_float(esc ? PEKF_DT_ESCAPE : (uint32_t)q.dt));
         r.am = make_float4((float)lpf_acc.x, (float)lpf_acc.y, (float)lpf_acc.z, (float)lpf_mag.x);
         r.my = make_float2((float)lpf_mag.y, (float)lpf_mag.z);
         return r;

@@ -134,10 +134,10 @@ using namespace pekf;
 
 extern "C" {
 
-int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
-                 const void *plane_gd, const void *plane_am, const void *plane_my,
-                 const double *refs, double *X, double *P, double q, double r, double *traj,
-                 const int32_t *counts, uint32_t flags, void *stream) {
+int pekf_run_ext_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
+                     const void *plane_gd, const void *plane_am, const void *plane_my, const double *dt_ext,
+                     const double *refs, double *X, double *P, double q, double r, double *traj,
+                     const int32_t *counts, uint32_t flags, void *stream) {
     PEKF_CHECK_ARG(batch >= 0 && n_steps >= 0, "negative size");
     PEKF_CHECK_ARG((flags & ~(uint32_t)(PEKF_RUN_MIXED_PRECISION | PEKF_RUN_STATE_SOA)) == 0, "unknown flags");
     if (batch == 0 || n_steps == 0) return PEKF_OK;
@@ -146,7 +146,8 @@ int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
     PEKF_CHECK_ARG(n_steps < ((int64_t)1 << 31), "n_steps must be < 2^31 records per launch");
     PEKF_CHECK_ARG(plane_gd && plane_am && plane_my && refs && X && P, "null pointer");
     PEKF_CHECK_ARG(((uintptr_t)plane_gd % 16 == 0) && ((uintptr_t)plane_am % 16 == 0) &&
-                       ((uintptr_t)plane_my % 8 == 0) && ((uintptr_t)traj % 16 == 0),
+                       ((uintptr_t)plane_my % 8 == 0) && ((uintptr_t)traj % 16 == 0) &&
+                       ((uintptr_t)dt_ext % 8 == 0),
                    "misaligned plane / traj pointer");
     PEKF_CHECK_ARG(r > 0.0, "r must be > 0 (S = P- + rI must be SPD)");
     const dim3 grid(grid_for(batch, kRunBlock)), block(kRunBlock);
@@ -155,14 +156,16 @@ int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
     const auto *my = static_cast<const float2 *>(plane_my);
     const bool mixed = flags & PEKF_RUN_MIXED_PRECISION, soa = flags & PEKF_RUN_STATE_SOA;
     if (n_steps > 1)  // the multi-record kernels live in pekf_run_multi.hip (its own scheduling strategy)
-        return launch_run_multi(batch, n_steps, window, step0, gd, am, my, refs, X, P, q, r, traj, counts, mixed,
-                                soa, as_stream(stream));
+        return launch_run_multi(batch, n_steps, window, step0, gd, am, my, dt_ext, refs, X, P, q, r, traj, counts,
+                                mixed, soa, as_stream(stream));
     // one-record launch (online serving)
-#define PEKF_LAUNCH_ONE(TR, MX, SO, CN)                                                                      \
-    hipLaunchKernelGGL((k_run<TR, MX, SO, CN, true>), grid, block, 0, as_stream(stream), batch, n_steps, window, \
-                       step0, gd, am, my, refs, X, P, q, r, traj, counts)
+#define PEKF_LAUNCH_ONE(TR, MX, SO, CN, LD)                                                                   \
+    hipLaunchKernelGGL((k_run<TR, MX, SO, CN, true, false, LD>), grid, block, 0, as_stream(stream), batch, n_steps, \
+                       window, step0, gd, am, my, refs, X, P, q, r, traj, counts, dt_ext)
+#define PEKF_LAUNCH_ONE0(TR, MX, SO, CN) \
+    do { if (dt_ext) PEKF_LAUNCH_ONE(TR, MX, SO, CN, true); else PEKF_LAUNCH_ONE(TR, MX, SO, CN, false); } while (0)
 #define PEKF_LAUNCH_ONE1(TR, MX, SO) \
-    do { if (counts) PEKF_LAUNCH_ONE(TR, MX, SO, true); else PEKF_LAUNCH_ONE(TR, MX, SO, false); } while (0)
+    do { if (counts) PEKF_LAUNCH_ONE0(TR, MX, SO, true); else PEKF_LAUNCH_ONE0(TR, MX, SO, false); } while (0)
 #define PEKF_LAUNCH_ONE2(TR, MX) \
     do { if (soa) PEKF_LAUNCH_ONE1(TR, MX, true); else PEKF_LAUNCH_ONE1(TR, MX, false); } while (0)
     if (traj) {
@@ -172,10 +175,19 @@ int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
     }
 #undef PEKF_LAUNCH_ONE2
 #undef PEKF_LAUNCH_ONE1
+#undef PEKF_LAUNCH_ONE0
 #undef PEKF_LAUNCH_ONE
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_run");
     return PEKF_OK;
+}
+
+int pekf_run_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
+                 const void *plane_gd, const void *plane_am, const void *plane_my,
+                 const double *refs, double *X, double *P, double q, double r, double *traj,
+                 const int32_t *counts, uint32_t flags, void *stream) {
+    return pekf_run_ext_dev(batch, n_steps, window, step0, plane_gd, plane_am, plane_my, nullptr, refs, X, P, q, r,
+                            traj, counts, flags, stream);
 }
 
 int pekf_reset_state_dev(int64_t batch, double *X, double *P, void *stream) {

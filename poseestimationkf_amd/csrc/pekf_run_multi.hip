@@ -21,25 +21,28 @@ static bool pin_schedule() {
 }
 
 int launch_run_multi(int64_t batch, int64_t n_steps, int64_t window, int64_t step0, const float4 *gd,
-                     const float4 *am, const float2 *my, const double *refs, double *X, double *P, double q,
-                     double r, double *traj, const int32_t *counts, bool mixed, bool soa, hipStream_t stream) {
+                     const float4 *am, const float2 *my, const double *dtx, const double *refs, double *X,
+                     double *P, double q, double r, double *traj, const int32_t *counts, bool mixed, bool soa,
+                     hipStream_t stream) {
     const dim3 grid(grid_for(batch, kRunBlock)), block(kRunBlock);
-    if (!traj && !mixed && !counts && pin_schedule()) {
+    if (!traj && !mixed && !counts && !dtx && pin_schedule()) {
         if (soa)
             hipLaunchKernelGGL((k_run<false, false, true, false, false, true>), grid, block, 0, stream, batch, n_steps,
-                               window, step0, gd, am, my, refs, X, P, q, r, traj, counts);
+                               window, step0, gd, am, my, refs, X, P, q, r, traj, counts, dtx);
         else
             hipLaunchKernelGGL((k_run<false, false, false, false, false, true>), grid, block, 0, stream, batch, n_steps,
-                               window, step0, gd, am, my, refs, X, P, q, r, traj, counts);
+                               window, step0, gd, am, my, refs, X, P, q, r, traj, counts, dtx);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "k_run");
         return PEKF_OK;
     }
-#define PEKF_LAUNCH_RUN(TR, MX, SO, CN)                                                                      \
-    hipLaunchKernelGGL((k_run<TR, MX, SO, CN, false>), grid, block, 0, stream, batch, n_steps, window, step0, gd, \
-                       am, my, refs, X, P, q, r, traj, counts)
+#define PEKF_LAUNCH_RUN(TR, MX, SO, CN, LD)                                                                    \
+    hipLaunchKernelGGL((k_run<TR, MX, SO, CN, false, false, LD>), grid, block, 0, stream, batch, n_steps, window, \
+                       step0, gd, am, my, refs, X, P, q, r, traj, counts, dtx)
+#define PEKF_LAUNCH_RUN0(TR, MX, SO, CN) \
+    do { if (dtx) PEKF_LAUNCH_RUN(TR, MX, SO, CN, true); else PEKF_LAUNCH_RUN(TR, MX, SO, CN, false); } while (0)
 #define PEKF_LAUNCH_RUN1(TR, MX, SO) \
-    do { if (counts) PEKF_LAUNCH_RUN(TR, MX, SO, true); else PEKF_LAUNCH_RUN(TR, MX, SO, false); } while (0)
+    do { if (counts) PEKF_LAUNCH_RUN0(TR, MX, SO, true); else PEKF_LAUNCH_RUN0(TR, MX, SO, false); } while (0)
 #define PEKF_LAUNCH_RUN2(TR, MX) \
     do { if (soa) PEKF_LAUNCH_RUN1(TR, MX, true); else PEKF_LAUNCH_RUN1(TR, MX, false); } while (0)
     if (traj) {
@@ -49,6 +52,7 @@ int launch_run_multi(int64_t batch, int64_t n_steps, int64_t window, int64_t ste
     }
 #undef PEKF_LAUNCH_RUN2
 #undef PEKF_LAUNCH_RUN1
+#undef PEKF_LAUNCH_RUN0
 #undef PEKF_LAUNCH_RUN
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_run");

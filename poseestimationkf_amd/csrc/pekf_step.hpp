@@ -337,7 +337,11 @@ __device__ __forceinline__ void from_ref_basis(const RW &Wr, double *x, Sym4T<PT
 // COUNTS: filter b applies only its first counts[b] records of the launch (a separate
 // instantiation so the uniform-length path carries no per-step lane predicate).
 // PIN: the Schur-inverse-first schedule of the multi-record loop (ekf_record_step, launch_run_multi).
-template <bool TRAJ, bool MIXED, bool SOA, bool COUNTS, bool ONE, bool PIN = false>
+// LONGDT: the window has a dt side plane dtx[window][batch] (float64 ns): a record whose dt word is
+// PEKF_DT_ESCAPE takes its dt from there -- gaps of 2^31 ns or more, negative or fractional ones, any
+// T - previousT the reference accepts (ExtendedKalmanFilter.py:62).  A separate instantiation, so the
+// windows without escapes (every synthetic and front-end stream but the rare long pause) pay nothing.
+template <bool TRAJ, bool MIXED, bool SOA, bool COUNTS, bool ONE, bool PIN = false, bool LONGDT = false>
 __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run(int64_t batch, int64_t n_steps, int64_t window,
                                                    int64_t step0, const float4 *__restrict__ gd,
                                                    const float4 *__restrict__ am,
@@ -345,7 +349,8 @@ __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run(int64_t batch, 
                                                    const double *__restrict__ refs,
                                                    double *__restrict__ Xio, double *__restrict__ Pio,
                                                    double qs, double rs, double *__restrict__ traj,
-                                                   const int32_t *__restrict__ counts) {
+                                                   const int32_t *__restrict__ counts,
+                                                   const double *__restrict__ dtx) {
     using PT = typename std::conditional<MIXED, float, double>::type;
     if constexpr (ONE) {
         // one-record launch (online serving): the state and the reference pair are most of the
@@ -383,8 +388,12 @@ __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run(int64_t batch, 
             const uint32_t word = __float_as_uint(cur.gd.w);
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
-            ekf_record_step<PT>(x, state_norm2(x), P, Wf, step_consts<PT, false>(qs, rs), gy,
-                                (double)(word & 0x7FFFFFFFu), (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
+            double dtn = (double)(word & PEKF_DT_MASK);
+            if constexpr (LONGDT) {
+                if ((word & PEKF_DT_MASK) == PEKF_DT_ESCAPE) dtn = (dtx + base)[lane];
+            }
+            ekf_record_step<PT>(x, state_norm2(x), P, Wf, step_consts<PT, false>(qs, rs), gy, dtn,
+                                (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
         }
         if (TRAJ && act) {
             double2 *o = reinterpret_cast<double2 *>(traj) + 2 * (int64_t)lane;
@@ -432,9 +441,12 @@ __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run(int64_t batch, 
             const uint32_t word = __float_as_uint(cur.gd.w);
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
+            double dtn = (double)(word & PEKF_DT_MASK);
+            if constexpr (LONGDT) {  // the escaped record's row, (step0 + t) % window (rare: off the fast path)
+                if ((word & PEKF_DT_MASK) == PEKF_DT_ESCAPE) dtn = dtx[((step0 + t) % window) * batch + b];
+            }
             ekf_record_step<PT, MC, decltype(lazy)::value, MC && !MIXED, PIN>(
-                x, n2, P, ref, step_consts<PT, MC>(qs, rs), gy, (double)(word & 0x7FFFFFFFu),
-                (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
+                x, n2, P, ref, step_consts<PT, MC>(qs, rs), gy, dtn, (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
         }
         if (TRAJ) {
             double xo[4] = {x[0], x[1], x[2], x[3]};

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 from . import synth
-from ._lib import RUN_MIXED_PRECISION, RUN_STATE_SOA, check, dptr, f64, lib
+from ._lib import EV_TIME_EVENTS, RUN_MIXED_PRECISION, RUN_STATE_SOA, check, dptr, f64, lib
 
 
 # ------------------------------------------------------------------ device plumbing
@@ -128,10 +128,13 @@ def read_log_records(path):
     n = n.value
     gyro, acc, mag = (np.empty((n, 1, 3), np.float32) for _ in range(3))
     dtw = np.empty((n, 1), np.uint32)
-    acc0, mag0, t0 = np.empty((1, 3)), np.empty((1, 3)), ctypes.c_double()
-    check(lib.pekf_log_read(bpath, n, gyro.ctypes.data, acc.ctypes.data, mag.ctypes.data, dtw.ctypes.data,
-                            dptr(acc0), dptr(mag0), ctypes.byref(t0)))
-    return synth.Records(gyro, acc, mag, dtw, acc0, mag0)
+    dtx = np.empty((n, 1), np.float64)
+    acc0, mag0, t0, n_esc = np.empty((1, 3)), np.empty((1, 3)), ctypes.c_double(), ctypes.c_int64()
+    check(lib.pekf_log_read_ext(bpath, n, gyro.ctypes.data, acc.ctypes.data, mag.ctypes.data, dtw.ctypes.data,
+                                dtx.ctypes.data, ctypes.byref(n_esc), dptr(acc0), dptr(mag0), ctypes.byref(t0)))
+    # records whose T - previousT does not fit the dt word (a pause >= 2^31 ns, a negative or fractional
+    # difference) carry it in the float64 side plane
+    return synth.Records(gyro, acc, mag, dtw, acc0, mag0, dtx if n_esc.value else None)
 
 
 # ------------------------------------------------------------------ resident IMU window
@@ -152,6 +155,7 @@ class IMUWindow:
         self.my = DeviceBuffer(8 * n)
         self.refs = DeviceBuffer(48 * self.batch)
         self.counts = None  # per-filter valid record counts when filters are ragged (logs, front-end)
+        self.dtx = None     # dt side plane [window][batch] float64 when some record's dt is escaped (pekf.h)
 
     @property
     def nbytes(self):
@@ -166,16 +170,20 @@ class IMUWindow:
         win.am.upload(am)
         win.my.upload(my)
         win.refs.upload(synth.refs_array(rec.acc0, rec.mag0))
+        if rec.dtx is not None:
+            win.dtx = DeviceBuffer(8 * W * K).upload(np.ascontiguousarray(rec.dtx, np.float64))
         return win
 
     @classmethod
-    def from_planes(cls, gd, am, my, acc0, mag0):
+    def from_planes(cls, gd, am, my, acc0, mag0, dtx=None):
         W, K = gd.shape[:2]
         win = cls(K, W)
         win.gd.upload(np.ascontiguousarray(gd, np.float32))
         win.am.upload(np.ascontiguousarray(am, np.float32))
         win.my.upload(np.ascontiguousarray(my, np.float32))
         win.refs.upload(synth.refs_array(acc0, mag0))
+        if dtx is not None:
+            win.dtx = DeviceBuffer(8 * W * K).upload(np.ascontiguousarray(dtx, np.float64))
         return win
 
     @classmethod
@@ -198,8 +206,13 @@ class IMUWindow:
                 pad[:m] = a[:m]
                 out.append(pad)
             return np.concatenate(out, axis=1)
+        escaped = any(r.dtx is not None for r in recs)
+        for r in recs:
+            if escaped and r.dtx is None:
+                r.dtx = np.zeros(r.dtw.shape, np.float64)
         rec = synth.Records(cat("gyro"), cat("acc"), cat("mag"), cat("dtw"),
-                            np.concatenate([r.acc0 for r in recs]), np.concatenate([r.mag0 for r in recs]))
+                            np.concatenate([r.acc0 for r in recs]), np.concatenate([r.mag0 for r in recs]),
+                            cat("dtx") if escaped else None)
         win = cls.from_records(rec)
         win.counts = np.minimum(lens, n).astype(np.int32)
         return win
@@ -243,34 +256,47 @@ class IMUWindow:
         am = self.am.download((self.window, self.batch, 4), np.float32)[:, cols]
         my = self.my.download((self.window, self.batch, 2), np.float32)[:, cols]
         refs = self.refs.download((self.batch, 6), np.float64)[cols]
-        return synth.unpack_planes(gd, am, my, refs[:, :3], refs[:, 3:])
+        dtx = None if self.dtx is None else self.dtx.download((self.window, self.batch), np.float64)[:, cols]
+        return synth.unpack_planes(gd, am, my, refs[:, :3], refs[:, 3:], dtx)
 
 
 # ------------------------------------------------------------------ server front-end (raw events)
 
+def _event_planes(ev):
+    """(device event planes, n_events, flags): synth.pack_events (time events inserted for gaps the
+    30-bit field cannot hold), uploaded; flags = PEKF_EV_TIME_EVENTS when the planes hold any."""
+    planes = synth.pack_events(ev)
+    return (DeviceBuffer(planes.nbytes).upload(planes), planes.shape[0],
+            EV_TIME_EVENTS if synth.has_time_events(planes) else 0)
+
+
 def run_frontend(ev, alpha=0.1, r_max=None):
     """Raw phone events (synth.generate_events layout) -> (IMUWindow of records, counts (K,) int32).
 
-    Runs pekf_frontend_dev.  Every record needs a gyro, an accelerometer and a
-    magnetometer event, so r_max defaults to n_events // 3 + 1.  Raises if a dt does not fit the
-    31-bit record field or a filter overflows r_max."""
-    planes = synth.pack_events(ev)
-    E, K = planes.shape[:2]
-    r_max = E // 3 + 1 if r_max is None else int(r_max)
-    evb = DeviceBuffer(planes.nbytes).upload(planes)
+    Runs pekf_frontend_ext_dev.  Every record needs a gyro, an accelerometer and a
+    magnetometer event, so r_max defaults to n_events // 3 + 1.  Event gaps of any size go through
+    time events, and records whose dt does not fit the dt word through the window's dt side plane
+    (win.dtx, kept only if some record needed it).  Raises if a filter overflows r_max."""
+    K = np.asarray(ev["types"]).shape[1]
+    E0 = np.asarray(ev["types"]).shape[0]
+    evb, E, flags = _event_planes(ev)
+    r_max = E0 // 3 + 1 if r_max is None else int(r_max)
     init = DeviceBuffer(48 * K).upload(np.concatenate([ev["init_acc"], ev["init_mag"]], axis=1).astype(np.float64))
     tib = DeviceBuffer(8 * K).upload(np.ascontiguousarray(ev["t_init"], np.int64))
     win = IMUWindow(K, max(1, r_max))
+    dtx = DeviceBuffer(8 * K * max(1, r_max))
     cnt = DeviceBuffer(4 * K)
     errb = DeviceBuffer(4).upload(np.zeros(1, np.int32))
-    check(lib.pekf_frontend_dev(K, E, evb.ptr, init.ptr, tib.ptr, float(alpha), r_max, win.gd.ptr,
-                                win.am.ptr, win.my.ptr, cnt.ptr, win.refs.ptr, errb.ptr, None))
+    check(lib.pekf_frontend_ext_dev(K, E, evb.ptr, init.ptr, tib.ptr, float(alpha), r_max, win.gd.ptr,
+                                    win.am.ptr, win.my.ptr, dtx.ptr, cnt.ptr, win.refs.ptr, flags, errb.ptr, None))
     check(lib.pekf_device_sync())
     err = int(errb.download((1,), np.int32)[0])
     if err & 1:
         raise ValueError("a record's dt does not fit the 31-bit ns field of the stream")
     if err & 2:
         raise ValueError("more than r_max=%d records for some filter" % r_max)
+    if err & 4:
+        win.dtx = dtx
     win.counts = cnt.download((K,), np.int32)
     return win, win.counts
 
@@ -280,9 +306,8 @@ def frontend_init(ev, n_avg=100):
     dict(init (K, 6) raw {acc, mag} means, t_init (K,) int64, ready (K,) bool, gyro_mean (K, 3),
     var_acc / var_mag / var_gyro (K, 3)) by pekf_frontend_init_dev: the inputs run_frontend needs
     for phase 3 (KFS/Parser.cpp:36-58,84-140, KFS/InitialValues.cpp)."""
-    planes = synth.pack_events(ev)
-    E, K = planes.shape[:2]
-    evb = DeviceBuffer(planes.nbytes).upload(planes)
+    K = np.asarray(ev["types"]).shape[1]
+    evb, E, _ = _event_planes(ev)   # phase 2 always honours time events
     tsb = DeviceBuffer(8 * K).upload(np.ascontiguousarray(ev["t_init"], np.int64))
     ib, tib, sb, rb = DeviceBuffer(48 * K), DeviceBuffer(8 * K), DeviceBuffer(96 * K), DeviceBuffer(4 * K)
     check(lib.pekf_frontend_init_dev(K, E, evb.ptr, tsb.ptr, int(n_avg), ib.ptr, tib.ptr, sb.ptr, rb.ptr, None))
@@ -302,22 +327,17 @@ def run_session(phase2, phase3, filters, n_avg=100, alpha=0.1):
     that never finished phase 2 has NaN references and state --, counts (K,) records applied,
     refs (K, 6))."""
     K = filters.batch
-    p2 = synth.pack_events(phase2)
-    E2 = p2.shape[0]
-    assert p2.shape[1] == K and E2 > 0
+    assert np.asarray(phase2["types"]).shape[1] == K and np.asarray(phase2["types"]).shape[0] > 0
+    assert np.asarray(phase3["types"]).shape[1] == K
     t_last = np.asarray(phase2["times"], np.int64)[-1]
-    p3 = synth.pack_events(dict(phase3, t_init=t_last))
-    assert p3.shape[1] == K
-    ev2, ev3 = DeviceBuffer(p2.nbytes).upload(p2), DeviceBuffer(p3.nbytes).upload(p3)
+    ev2, E2, _ = _event_planes(phase2)
+    ev3, E3, flags3 = _event_planes(dict(phase3, t_init=t_last))
     tsb = DeviceBuffer(8 * K).upload(np.ascontiguousarray(phase2["t_init"], np.int64))
     ib, tib, rb = DeviceBuffer(48 * K), DeviceBuffer(8 * K), DeviceBuffer(4 * K)
     check(lib.pekf_frontend_init_dev(K, E2, ev2.ptr, tsb.ptr, int(n_avg), ib.ptr, tib.ptr, None, rb.ptr, None))
     cnt, refs = DeviceBuffer(4 * K), DeviceBuffer(48 * K)
-    errb = DeviceBuffer(4).upload(np.zeros(1, np.int32))
-    filters.run_events_async(ev3, p3.shape[0], ib, tib, cnt, refs, alpha, errb)
+    filters.run_events_async(ev3, E3, ib, tib, cnt, refs, alpha, flags=flags3)
     check(lib.pekf_device_sync())
-    if int(errb.download((1,), np.int32)[0]) & 1:
-        raise ValueError("a record's dt does not fit the 31-bit ns field of the stream")
     return dict(ready=rb.download((K,), np.int32).astype(bool), counts=cnt.download((K,), np.int32),
                 refs=refs.download((K, 6), np.float64))
 
@@ -383,12 +403,18 @@ class BatchedEKF:
 
     def run_async(self, win: IMUWindow, n_steps, step0=0, stream=None, traj=None, counts=None):
         """Enqueue one fused launch; traj: optional DeviceBuffer of n_steps*batch*32 bytes;
-        counts: optional DeviceBuffer of batch int32 (filter b applies its first counts[b] records)."""
+        counts: optional DeviceBuffer of batch int32 (filter b applies its first counts[b] records).
+        A window with a dt side plane (escaped records) runs pekf_run_ext_dev with it."""
         assert win.batch == self.batch
-        check(lib.pekf_run_dev(self.batch, int(n_steps), win.window, int(step0), win.gd.ptr,
-                               win.am.ptr, win.my.ptr, win.refs.ptr, self.X.ptr, self.P.ptr,
-                               self.q, self.r, traj.ptr if traj is not None else None,
-                               counts.ptr if counts is not None else None, self.flags, stream))
+        tr, cn = traj.ptr if traj is not None else None, counts.ptr if counts is not None else None
+        if win.dtx is None:
+            check(lib.pekf_run_dev(self.batch, int(n_steps), win.window, int(step0), win.gd.ptr, win.am.ptr,
+                                   win.my.ptr, win.refs.ptr, self.X.ptr, self.P.ptr, self.q, self.r, tr, cn,
+                                   self.flags, stream))
+        else:
+            check(lib.pekf_run_ext_dev(self.batch, int(n_steps), win.window, int(step0), win.gd.ptr, win.am.ptr,
+                                       win.my.ptr, win.dtx.ptr, win.refs.ptr, self.X.ptr, self.P.ptr, self.q,
+                                       self.r, tr, cn, self.flags, stream))
 
     def run(self, win: IMUWindow, n_steps=None, step0=0, want_traj=False, counts=None):
         """Advance every filter n_steps records (default: the whole window) from row step0.
@@ -409,31 +435,28 @@ class BatchedEKF:
             return tb.download((n_steps, self.batch, 4), np.float64)
         return None
 
-    def run_events_async(self, ev_planes, n_events, init, t_init, counts, refs, alpha=0.1, err=None, stream=None):
-        """Enqueue pekf_live_dev: device event planes [n_events][batch][4] f32 (synth.pack_events), init
-        (batch, 6), t_init (batch,) int64; counts (batch,) int32 and refs (batch, 6) outputs -- DeviceBuffers."""
+    def run_events_async(self, ev_planes, n_events, init, t_init, counts, refs, alpha=0.1, stream=None, flags=0):
+        """Enqueue pekf_live_ext_dev: device event planes [n_events][batch][4] f32 (synth.pack_events), init
+        (batch, 6), t_init (batch,) int64; counts (batch,) int32 and refs (batch, 6) outputs -- DeviceBuffers;
+        flags: EV_TIME_EVENTS if the planes hold time events."""
         if self.layout != "aos" or self.flags & RUN_MIXED_PRECISION:
             raise ValueError("the fused front-end + filter kernel runs the FP64 filter on AoS state")
-        check(lib.pekf_live_dev(self.batch, int(n_events), ev_planes.ptr, init.ptr, t_init.ptr, float(alpha), self.X.ptr,
-                                self.P.ptr, self.q, self.r, counts.ptr, refs.ptr,
-                                err.ptr if err is not None else None, stream))
+        check(lib.pekf_live_ext_dev(self.batch, int(n_events), ev_planes.ptr, init.ptr, t_init.ptr, float(alpha),
+                                    self.X.ptr, self.P.ptr, self.q, self.r, counts.ptr, refs.ptr, int(flags), None,
+                                    stream))
 
     def run_events(self, ev, alpha=0.1):
         """Raw phone events (synth.generate_events layout) -> front-end -> filter, fused in one launch
-        (pekf_live_dev).  Returns (counts (batch,) int32 records applied, refs (batch, 6)
-        the filters' acc0 / mag0).  Raises if a record dt does not fit the 31-bit field."""
-        planes = synth.pack_events(ev)
-        assert planes.shape[1] == self.batch
-        evb = DeviceBuffer(planes.nbytes).upload(planes)
+        (pekf_live_ext_dev).  Returns (counts (batch,) int32 records applied, refs (batch, 6)
+        the filters' acc0 / mag0).  Any event gap and any record dt is applied (time events, escapes)."""
+        assert np.asarray(ev["types"]).shape[1] == self.batch
+        evb, E, flags = _event_planes(ev)
         init = DeviceBuffer(48 * self.batch).upload(
             np.concatenate([ev["init_acc"], ev["init_mag"]], axis=1).astype(np.float64))
         tib = DeviceBuffer(8 * self.batch).upload(np.ascontiguousarray(ev["t_init"], np.int64))
         cnt, refs = DeviceBuffer(4 * self.batch), DeviceBuffer(48 * self.batch)
-        errb = DeviceBuffer(4).upload(np.zeros(1, np.int32))
-        self.run_events_async(evb, planes.shape[0], init, tib, cnt, refs, alpha, errb)
+        self.run_events_async(evb, E, init, tib, cnt, refs, alpha, flags=flags)
         check(lib.pekf_device_sync())
-        if int(errb.download((1,), np.int32)[0]) & 1:
-            raise ValueError("a record's dt does not fit the 31-bit ns field of the stream")
         return cnt.download((self.batch,), np.int32), refs.download((self.batch, 6), np.float64)
 
 
@@ -481,8 +504,9 @@ class FilterHandle:
         if counts is not None:
             c = np.ascontiguousarray(counts, dtype=np.int32).reshape(self.batch)
             cb = DeviceBuffer(c.nbytes).upload(c)
-        check(lib.pekf_filter_run(self.h, n_steps, win.window, int(step0), win.gd.ptr, win.am.ptr, win.my.ptr,
-                                  tb.ptr if tb is not None else None, cb.ptr if cb is not None else None, None))
+        check(lib.pekf_filter_run_ext(self.h, n_steps, win.window, int(step0), win.gd.ptr, win.am.ptr, win.my.ptr,
+                                      win.dtx.ptr if win.dtx is not None else None,
+                                      tb.ptr if tb is not None else None, cb.ptr if cb is not None else None, None))
         check(lib.pekf_device_sync())
         return tb.download((n_steps, self.batch, 4), np.float64) if want_traj else None
 

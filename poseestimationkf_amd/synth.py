@@ -40,6 +40,7 @@ DT_SPAN_NS = 16_000_001       # dt_ns = DT_MIN_NS + x % DT_SPAN_NS  -> [4e6, 2e7
 MISS_THRESH = 5_033_165       # (x >> 8) < 0.3 * 2^24
 MISSING_BIT = 0x80000000
 DT_MASK = 0x7FFFFFFF
+DT_ESCAPE = 0x7FFFFFFF        # dt field of all ones: the record's dt is in the float64 side plane (dtx)
 
 SQRT3 = 1.7320508075688772    # correctly rounded sqrt(3)
 SIN60 = 0.8660254037844386    # correctly rounded sqrt(3)/2
@@ -136,10 +137,16 @@ class Records:
     dtw: np.ndarray    # (W,K)   uint32: dt_ns | MISSING_BIT
     acc0: np.ndarray   # (K,3)   float64
     mag0: np.ndarray   # (K,3)   float64
+    dtx: np.ndarray = None  # (W,K) float64 dt side plane, or None: the dt of records whose dt field is DT_ESCAPE
 
     @property
     def dt_ns(self):
-        return (self.dtw & DT_MASK).astype(np.float64)
+        """(W,K) float64 T - previousT of every record (the side plane's value for an escaped one)."""
+        field = self.dtw & DT_MASK
+        dt = field.astype(np.float64)
+        if self.dtx is not None:
+            dt = np.where(field == DT_ESCAPE, self.dtx, dt)
+        return dt
 
     @property
     def missing(self):
@@ -219,13 +226,14 @@ def pack_planes(rec: Records):
     return gd, am, my
 
 
-def unpack_planes(gd, am, my, acc0, mag0):
+def unpack_planes(gd, am, my, acc0, mag0, dtx=None):
     """Inverse of pack_planes (used to pull sampled filters back off the device)."""
     gyro = np.ascontiguousarray(gd[..., :3])
     dtw = np.ascontiguousarray(gd[..., 3]).view(np.uint32)
     acc = np.ascontiguousarray(am[..., :3])
     mag = np.concatenate([am[..., 3:4], my], axis=-1)
-    return Records(gyro, acc, mag, dtw, np.asarray(acc0, np.float64), np.asarray(mag0, np.float64))
+    return Records(gyro, acc, mag, dtw, np.asarray(acc0, np.float64), np.asarray(mag0, np.float64),
+                   None if dtx is None else np.asarray(dtx, np.float64))
 
 
 def refs_array(acc0, mag0):
@@ -295,24 +303,46 @@ def generate_events(ids, n_events, seed=DEFAULT_SEED, params=SynthParams()):
 
 
 EV_DT_BITS = 30  # event word = (ns since the previous event << 2) | type
+EV_TIME = 3      # a time event: word == 3, x / y = the float64 clock step (include/pekf.h PEKF_EV_TIME)
 
 
 def pack_events(ev):
-    """generate_events dict -> EV float4 plane (E,K,4) f32 {x, y, z, bits(word)}.
+    """generate_events dict -> EV float4 plane (E',K,4) f32 {x, y, z, bits(word)}.
 
     16 B per event: the word carries the 2-bit type and the ns gap to the filter's previous
-    event (the first one: to t_init), which must be in [0, 2^30)."""
+    event (the first one: to t_init).  A gap the 30-bit field cannot hold (a pause of 2^30 ns or
+    more, or a clock that steps back) becomes a time event -- word 3, the gap as a float64 in the
+    x / y bits -- followed by the event itself with gap 0; every filter's stream is then padded to
+    the longest with zero-step time events (E' = E + the most time events any filter needs)."""
     E, K = ev["types"].shape
     times = np.asarray(ev["times"], np.int64)
     prev = np.concatenate([np.asarray(ev["t_init"], np.int64)[None, :], times[:-1]], axis=0)
     gap = times - prev
-    if E and (gap.min() < 0 or gap.max() >= (1 << EV_DT_BITS)):
-        raise ValueError("event gaps must be in [0, 2^%d) ns" % EV_DT_BITS)
-    word = ((gap.astype(np.uint64) << np.uint64(2)) | np.asarray(ev["types"], np.uint64)).astype(np.uint32)
-    planes = np.empty((E, K, 4), np.float32)
-    planes[..., :3] = ev["values"]
-    planes[..., 3] = word.view(np.float32)
+    long_gap = (gap < 0) | (gap >= (1 << EV_DT_BITS))
+    gap_field = np.where(long_gap, 0, gap)
+    word = ((gap_field.astype(np.uint64) << np.uint64(2)) | np.asarray(ev["types"], np.uint64)).astype(np.uint32)
+    if not long_gap.any():
+        planes = np.empty((E, K, 4), np.float32)
+        planes[..., :3] = ev["values"]
+        planes[..., 3] = word.view(np.float32)
+        return planes
+    shift = np.cumsum(long_gap, axis=0)            # time events inserted up to and including event e
+    planes = np.zeros((E + int(shift[-1].max()), K, 4), np.float32)
+    planes[..., 3] = np.uint32(EV_TIME).reshape(1).view(np.float32)[0]   # padding: zero-step time events
+    cols = np.broadcast_to(np.arange(K), (E, K))
+    row = np.arange(E)[:, None] + shift            # each event's row in the packed stream
+    planes[row, cols, :3] = ev["values"]
+    planes[row, cols, 3] = word.view(np.float32)
+    e, k = np.nonzero(long_gap)
+    step = gap[e, k].astype(np.float64).view(np.uint32).reshape(-1, 2)   # float64 halves (low, high)
+    planes[row[e, k] - 1, k, 0] = step[:, 0].view(np.float32)
+    planes[row[e, k] - 1, k, 1] = step[:, 1].view(np.float32)
     return planes
+
+
+def has_time_events(planes):
+    """Whether an event plane holds time events (word == EV_TIME): the flag the phase-3 kernels need."""
+    return bool((np.ascontiguousarray(planes[..., 3]).view(np.uint32) == EV_TIME).any())
 
 
 def window_bytes(batch, window):
@@ -331,4 +361,4 @@ def c1_timestamps(dt_ns, t0_ns=1_234_567_890_123):
 
 __all__ = ["DEFAULT_SEED", "SynthParams", "Records", "philox4x32", "reference_vectors", "generate",
            "pack_planes", "unpack_planes", "refs_array", "window_bytes", "c1_timestamps",
-           "MISSING_BIT", "DT_MASK"]
+           "MISSING_BIT", "DT_MASK", "DT_ESCAPE", "pack_events", "has_time_events", "EV_TIME"]

@@ -171,7 +171,7 @@ def main():
     # (160 B per filter) read and written once
     f = engine.BatchedEKF(K)
     cnt2, refs2 = engine.DeviceBuffer(4 * K), engine.DeviceBuffer(48 * K)
-    ms = timed(lambda: f.run_events_async(evb, E, ib, tb, cnt2, refs2, 0.1, err, s), s)
+    ms = timed(lambda: f.run_events_async(evb, E, ib, tb, cnt2, refs2, 0.1, s), s)
     assert np.array_equal(cnt2.download((K,), np.int32), counts)
     byts = K * E * 16 + K * (160 + 160 + 48 + 48 + 8 + 4)
     res["live"] = {"filters": K, "events_per_filter": E, "records": recs, "kernel_ms": ms,

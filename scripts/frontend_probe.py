@@ -44,7 +44,7 @@ def main():
     for _ in range(reps):
         e0.record(s)
         if live:
-            f.run_events_async(evb, E, ib, tb, cnt, win.refs, 0.1, err, s)
+            f.run_events_async(evb, E, ib, tb, cnt, win.refs, 0.1, s)
         else:
             check(lib.pekf_frontend_dev(K, E, evb.ptr, ib.ptr, tb.ptr, 0.1, r_max, win.gd.ptr, win.am.ptr,
                                         win.my.ptr, cnt.ptr, win.refs.ptr, err.ptr, s))

@@ -111,12 +111,15 @@ def test_live_lockstep_streams(eng):
     _same(fused, _split(eng, ev, K))
 
 
-def test_live_reports_a_dt_past_31_bits(eng):
+def test_live_applies_a_dt_past_31_bits(eng):
+    """Records 3 x (2^30 - 1) ns apart (dt past the 31-bit word: escaped, the float64 dt kept in the
+    queue's side entry) apply exactly as the split pipeline's (side plane + pekf_run_ext_dev)."""
     K = 4
     g = (1 << 30) - 1
-    spec = [(synth.EV_GYRO, g), (synth.EV_GYRO, g), (synth.EV_GYRO, g), (synth.EV_ACC, 10), (synth.EV_MAG, 10)]
-    with pytest.raises(ValueError, match="31-bit"):
-        eng.BatchedEKF(K).run_events(_events(K, spec))
+    spec = [(synth.EV_GYRO, g), (synth.EV_GYRO, g), (synth.EV_GYRO, g), (synth.EV_ACC, 10), (synth.EV_MAG, 10)] * 3
+    fused, split = _fused(eng, _events(K, spec), K), _split(eng, _events(K, spec), K)
+    assert np.all(fused[2] == 3)
+    _same(fused, split)
     with pytest.raises(ValueError, match="FP64 filter on AoS"):
         eng.BatchedEKF(K, layout="soa").run_events(_events(K, spec))
 

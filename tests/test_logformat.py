@@ -59,14 +59,52 @@ def test_native_ingest_matches_python_reader(c1_log):
 
 
 def test_native_ingest_errors_are_reported(tmp_path):
+    import ctypes
+
     from poseestimationkf_amd import _lib, engine
     bad = tmp_path / "bad.txt"
     bad.write_text("mag_0 : 1,0,0\nacc_0 : 0,0,1\ngyro : 0,0,0\nT : 0\nT : 0.5\nMag_1 : 1,0,0\nAcc_1 : 0,0,1\n")
-    with pytest.raises(_lib.PekfError, match="not an integer"):
-        engine.read_log_records(str(bad))
+    # the plain reader refuses a dt the dt word cannot hold; read_log_records takes it via the side plane
+    f3, u1 = np.empty(3, np.float32), np.empty(1, np.uint32)
+    a0, m0 = np.empty(3), np.empty(3)
+    st = _lib.lib.pekf_log_read(os.fsencode(str(bad)), 1, f3.ctypes.data, f3.ctypes.data, f3.ctypes.data,
+                                u1.ctypes.data, _lib.dptr(a0), _lib.dptr(m0), None)
+    assert st == _lib.PEKF_ERR_INVALID and "not an integer" in _lib.last_error()
+    rec = engine.read_log_records(str(bad))
+    assert rec.dtw[0, 0] == synth.DT_ESCAPE and rec.dt_ns[0, 0] == 0.5
     with pytest.raises(_lib.PekfError, match="cannot open"):
         engine.read_log_records(str(tmp_path / "missing.txt"))
     short = tmp_path / "short.txt"
     short.write_text("mag_0 : 1,0,0\nacc_0 : 0,0,1\nMag_1 : 1,0,0\nAcc_1 : 0,0,1\n")
     with pytest.raises(_lib.PekfError, match="Acc_1 records"):
         engine.read_log_records(str(short))
+    assert ctypes  # (imported for the raw call above)
+
+
+def test_native_ingest_escapes_long_negative_and_fractional_gaps(tmp_path):
+    """Any float64 T - previousT the reference accepts (ExtendedKalmanFilter.py:62): a 5 s pause, a
+    clock stepping back, a fractional ns difference and the escape value itself go to the dt side
+    plane; the other records keep their dt in the word, and dt_ns equals the Python reader's."""
+    from poseestimationkf_amd import engine
+    rec = synth.generate(np.arange(1), 8)
+    g, d, a, m = rec.filter(0)
+    d = d.copy()
+    d[2] = 5e9                 # a pause past 2^31 ns
+    d[4] = -3e6                # a negative gap
+    d[5] = float(0x7FFFFFFF)   # exactly the escape value: must be escaped too
+    ts = [1_000_000_000_000.0]
+    for v in d:
+        ts.append(ts[-1] + v)
+    path = tmp_path / "gaps.txt"
+    with open(path, "w") as fh:
+        logformat.write_log(fh, ts, g, a, m, rec.acc0[0], rec.mag0[0])
+    lines = path.read_text().splitlines(keepends=True)
+    last_t = max(i for i, l in enumerate(lines) if l.startswith("T : "))
+    lines[last_t] = lines[last_t].rstrip("\n") + ".5\n"   # a fractional last gap (float64 timestamps)
+    path.write_text("".join(lines))
+    got = engine.read_log_records(str(path))
+    _, dt_py, *_ = logformat.log_to_arrays(logformat.read_log(str(path)))
+    assert np.array_equal(got.dt_ns[:, 0], dt_py)
+    esc = got.dtw[:, 0] & synth.DT_MASK
+    assert np.nonzero(esc == synth.DT_ESCAPE)[0].tolist() == [2, 4, 5, 7]
+    assert got.dtx is not None and got.dtx[2, 0] == 5e9 and got.dtx[4, 0] == -3e6

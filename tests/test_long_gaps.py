@@ -1,0 +1,208 @@
+"""Any float64 time difference the reference accepts, on every stream path (VERDICT r2 "missing" #3).
+
+The reference forms dt = T - previousT in float64 (ExtendedKalmanFilter.py:62) and takes whatever
+it gets: a pause of seconds, a clock that steps back, a fractional difference.  The 40 B record
+carries dt as a 31-bit ns count, so such a record's dt word is the escape (PEKF_DT_ESCAPE) and its
+float64 dt sits in the window's side plane (include/pekf.h); raw phone events carry a 30-bit gap,
+so a longer or negative gap is a time event (word 3, the float64 step in x / y).
+
+CPU: the packing round trips and the two oracles agree on escaped records.  GPU: the fused kernel
+(multi-record, trajectory, counts, one-record and handle launches), the front-end, the fused
+front-end + filter kernel and phase 2 against the oracles."""
+import numpy as np
+import pytest
+
+from oracle import ekf_numpy
+from oracle import frontend_numpy as fe
+from poseestimationkf_amd import synth
+
+from .test_frontend import _oracle_records
+
+ODD_DTS = [5e9, -2e7, 1e7 + 0.5, float(0x7FFFFFFF), 3.3e10, 0.0]
+
+
+def _escaped_records(K=256, W=64, seed=41):
+    """A synthetic window with odd dts at scattered (row, filter) places, escaped into dtx."""
+    rec = synth.generate(np.arange(K), W, seed=seed)
+    dt = rec.dt_ns.copy()
+    rng = np.random.default_rng(seed)
+    for i, (r, k) in enumerate(zip(rng.integers(0, W, 40), rng.integers(0, K, 40))):
+        dt[r, k] = ODD_DTS[i % len(ODD_DTS)]
+    dt[:, 5] = 5e9                                        # one filter with a pause on every record
+    return with_dts(rec, dt)
+
+
+def with_dts(rec, dt):
+    fits = (dt >= 0) & (dt < synth.DT_ESCAPE) & (dt == np.floor(dt))
+    field = np.where(fits, dt, synth.DT_ESCAPE).astype(np.uint32)
+    dtw = (rec.dtw & np.uint32(synth.MISSING_BIT)) | field
+    return synth.Records(rec.gyro, rec.acc, rec.mag, dtw, rec.acc0, rec.mag0, np.where(fits, 0.0, dt))
+
+
+def _decode_events(planes, t_init):
+    """Host decoder of an event plane: per filter, the (type, time) of its sample events."""
+    words = np.ascontiguousarray(planes[..., 3]).view(np.uint32)
+    out = []
+    for k in range(planes.shape[1]):
+        t, evs = int(t_init[k]), []
+        for e in range(planes.shape[0]):
+            w = int(words[e, k])
+            if w == synth.EV_TIME:
+                t += int(planes[e, k, :2].copy().view(np.float64)[0])
+            else:
+                t += w >> 2
+                evs.append((w & 3, t))
+        out.append(evs)
+    return out
+
+
+def test_pack_events_time_events_round_trip():
+    K, E = 6, 40
+    ev = synth.generate_events(np.arange(K), E, seed=3)
+    t = ev["times"].copy()
+    t[10:, 1] += 5_000_000_000          # a 5 s pause
+    t[20:, 3] -= 700_000_000            # the clock steps back 0.7 s
+    t[5:, 4] += 2_000_000_000           # two pauses on one filter
+    t[30:, 4] += 1 << 30
+    ev = dict(ev, times=t)
+    planes = synth.pack_events(ev)
+    assert planes.shape[0] == E + 2 and synth.has_time_events(planes)
+    got = _decode_events(planes, ev["t_init"])
+    for k in range(K):
+        assert got[k] == [(int(ev["types"][e, k]), int(t[e, k])) for e in range(E)]
+    assert not synth.has_time_events(synth.pack_events(synth.generate_events(np.arange(K), E, seed=3)))
+
+
+def test_records_dt_ns_and_oracles_agree_on_escapes(oracle_c):
+    rec = _escaped_records(K=16, W=40)
+    dt = rec.dt_ns
+    assert (rec.dtw & np.uint32(synth.DT_MASK) == synth.DT_ESCAPE).sum() > 10
+    assert dt[0, 5] == 5e9 and np.isin(ODD_DTS, dt).sum() >= 4
+    Xo, Po, _ = oracle_c.run(rec)
+    for k in (0, 5, 9):
+        g, d, a, m = rec.filter(k)
+        Xn, Pn = ekf_numpy.run_filter(g, d, a, m, rec.acc0[k], rec.mag0[k], record=False)[:2]
+        assert np.abs(Xn - Xo[k]).max() < 1e-10
+
+
+# ------------------------------------------------------------------------------------------ GPU
+@pytest.fixture(scope="module")
+def eng():
+    from poseestimationkf_amd import engine
+    from poseestimationkf_amd._lib import device_count
+    assert device_count() > 0, "GPU tests need a HIP device"
+    return engine
+
+
+def _err(a, b):
+    return float(np.abs(np.asarray(a) - np.asarray(b)).max())
+
+
+@pytest.mark.gpu
+def test_fused_run_with_escaped_dts(eng, oracle_c):
+    """Every launch shape of the fused kernel reads escaped records' dt from the side plane."""
+    rec = _escaped_records()
+    K, W = rec.dtw.shape[1], rec.dtw.shape[0]
+    win = eng.IMUWindow.from_records(rec)
+    assert win.dtx is not None
+    Xo, Po, tro = oracle_c.run(rec, n_steps=100, step0=7, want_traj=True)
+    f = eng.BatchedEKF(K)                                     # multi-record launch, wraps the window
+    f.run(win, n_steps=100, step0=7)
+    X, P = f.get_state()
+    assert _err(X, Xo) < 1e-9 and _err(P, Po) < 1e-9
+    tr = eng.BatchedEKF(K).run(win, n_steps=100, step0=7, want_traj=True)   # trajectory variant
+    assert _err(tr, tro.transpose(1, 0, 2)) < 1e-9
+    cnt = np.arange(K) % 100                                  # ragged counts
+    fc = eng.BatchedEKF(K)
+    fc.run(win, n_steps=100, step0=7, counts=cnt)
+    Xc, _ = fc.get_state()
+    for k in (1, 5, 37, 99, 200):
+        Xk, _, _ = oracle_c.run(synth.Records(*(a[:, k:k + 1] for a in (rec.gyro, rec.acc, rec.mag, rec.dtw)),
+                                              rec.acc0[k:k + 1], rec.mag0[k:k + 1], rec.dtx[:, k:k + 1]),
+                                n_steps=int(cnt[k]), step0=7)
+        assert _err(Xc[k], Xk[0]) < 1e-9
+    fo = eng.BatchedEKF(K)                                    # one-record launches (online serving)
+    for t in range(12):
+        fo.run(win, n_steps=1, step0=7 + t)
+    X1, _ = fo.get_state()
+    X1o, _, _ = oracle_c.run(rec, n_steps=12, step0=7)
+    assert _err(X1, X1o) < 1e-9
+    h = eng.FilterHandle(rec.acc0, rec.mag0)                  # the handle's stream path
+    h.run(win, n_steps=30)
+    Xh, _ = h.get_state()
+    X30, _, _ = oracle_c.run(rec, n_steps=30)
+    assert _err(Xh, X30) < 1e-9
+    fm = eng.BatchedEKF(K, precision="mixed")                 # mixed precision: same records
+    fm.run(win, n_steps=100, step0=7)
+    assert _err(fm.get_state()[0], Xo) < 1e-5
+    fs = eng.BatchedEKF(K, layout="soa")
+    fs.run(win, n_steps=100, step0=7)
+    assert np.array_equal(fs.get_state()[0], X)
+
+
+def _paused_events(K, E, seed):
+    ev = synth.generate_events(np.arange(K), E, seed=seed)
+    t = ev["times"].copy()
+    rng = np.random.default_rng(seed)
+    for k in range(K):
+        if k % 3 == 0:                          # a 5 s pause (records across it have dt > 2^31 ns)
+            t[rng.integers(1, E):, k] += 5_000_000_000
+        if k % 4 == 1:                          # the phone clock steps back 0.5 s
+            t[rng.integers(1, E):, k] -= 500_000_000
+        if k % 7 == 2:                          # a pause just under the 30-bit event field, twice
+            t[rng.integers(1, E):, k] += (1 << 30) + 12345
+    return dict(ev, times=t)
+
+
+@pytest.mark.gpu
+def test_frontend_records_across_pauses_and_clock_steps(eng):
+    K, E = 192, 900
+    ev = _paused_events(K, E, seed=51)
+    win, counts = eng.run_frontend(ev)
+    assert win.dtx is not None                                # some record needed the side plane
+    rec = win.download_filters(np.arange(K))
+    dt_dev = rec.dt_ns
+    n_esc = 0
+    for k in range(K):
+        g, dt, a, m = _oracle_records(ev, k)
+        r = len(dt)
+        assert counts[k] == r
+        assert np.array_equal(dt_dev[:r, k], dt.astype(np.float64))
+        assert np.array_equal(rec.gyro[:r, k], g.astype(np.float32))
+        n_esc += int(((rec.dtw[:r, k] & np.uint32(synth.DT_MASK)) == synth.DT_ESCAPE).sum())
+    assert n_esc >= K // 3
+
+
+@pytest.mark.gpu
+def test_live_and_split_pipelines_across_pauses(eng, oracle_c):
+    """k_live (time events + escaped records in its LDS queue) equals the split pipeline bit for bit,
+    and both match the oracle chain."""
+    from .test_live import _fused, _same, _split
+    K, E = 320, 1000
+    ev = _paused_events(K, E, seed=52)
+    fused, split = _fused(eng, ev, K), _split(eng, ev, K)
+    _same(fused, split)
+    X, _, counts, refs = fused
+    worst = 0.0
+    for k in range(0, K, 9):
+        g, dt, a, m = _oracle_records(ev, k)
+        base = synth.Records(g[:, None].astype(np.float32), a[:, None].astype(np.float32),
+                             m[:, None].astype(np.float32), np.zeros((len(dt), 1), np.uint32),
+                             refs[k:k + 1, :3], refs[k:k + 1, 3:])
+        Xo, _, _ = oracle_c.run(with_dts(base, dt[:, None].astype(np.float64)))
+        worst = max(worst, _err(X[k], Xo[0]))
+    print("events with pauses / clock steps -> filter vs oracle chain: max |dq| = %.3e" % worst)
+    assert worst < 1e-9
+
+
+@pytest.mark.gpu
+def test_phase2_with_pauses_and_clock_steps(eng):
+    K, E = 200, 700
+    ev = _paused_events(K, E, seed=53)
+    got = eng.frontend_init(ev)
+    for k in range(K):
+        o = fe.initial_values(ev["types"][:, k], ev["values"][:, k], ev["times"][:, k])
+        assert got["ready"][k] == o["ready"]
+        if o["ready"]:
+            assert got["t_init"][k] == o["t_init"]
+            assert np.array_equal(got["init"][k], np.array(o["acc"] + o["mag"]))
