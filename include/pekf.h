@@ -219,6 +219,7 @@ int pekf_log_read_ext(const char *path, int64_t n_records, float *gyro, float *a
  * word = (ns since the filter's previous event, first: since t_init[b]) << 2 | type (0 acc, 1 gyro,
  * 2 mag), so gaps must be < 2^30 ns.  init[batch*6] = raw phase-2 means {acc xyz, mag xyz}
  * (Parser.cpp:44-53); refs[batch*6] receives their normalised values (the filter's acc0 / mag0).
+ * A filter whose init is not finite (pekf_frontend_init_dev's "not ready") produces no record (counts 0).
  * *dev_error |= 1 if a record dt does not fit 31 bits, 2 if a filter had more than r_max records. */
 int pekf_frontend_dev(int64_t batch, int64_t n_events, const void *ev_planes, const double *init,
                       const int64_t *t_init, double alpha, int64_t r_max,
@@ -246,7 +247,8 @@ int pekf_frontend_ext_dev(int64_t batch, int64_t n_events, const void *ev_planes
  * written anywhere -- each is applied to the filter's state on the same lane (Prediction + Correction,
  * main_file.py:42-45) as soon as the wave runs its next filter step.  Same events, init, t_init, alpha
  * and refs as pekf_frontend_dev; X[batch*4], P[batch*16] (AoS, FP64) are the filters' state, read at
- * the start and written at the end (left untouched for a filter with no record); q, r as pekf_run_dev.
+ * the start and written at the end (left untouched for a filter with no record, as for one whose init
+ * is not finite: phase 2 never got ready); q, r as pekf_run_dev.
  * counts[b] receives the number of records filter b applied.  The final state equals pekf_frontend_dev
  * followed by pekf_run_dev with those counts, bit for bit.  A record whose dt does not fit the dt word
  * keeps its float64 dt beside it on the lane (as pekf_frontend_ext_dev + pekf_run_ext_dev would), so any

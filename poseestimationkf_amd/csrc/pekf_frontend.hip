@@ -34,6 +34,7 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
     if (b >= batch) return;
     Phase3 fe;
     fe.start(init + 6 * b, t_init[b], alpha);
+    const bool ready = init_is_finite(init + 6 * b);  // not ready (phase 2 unfinished): no records
     {
         double rf[6];
         fe.refs(rf);
@@ -48,6 +49,7 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
         if (!fe.pend) return;
         bool esc;
         const Rec rc = fe.emit(esc);
+        if (!ready) return;
         if (esc) bad |= dtx ? 4 : 1;
         if (r < r_max) {
             const int64_t o = r * batch + b;

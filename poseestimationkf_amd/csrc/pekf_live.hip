@@ -94,6 +94,9 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
 
     Phase3 fe;
     fe.start(init + 6 * b, t_init[b], alpha);
+    // a filter that never finished phase 2 (non-finite init: pekf_frontend_init_dev's "not ready")
+    // applies no record: its state is left as it was and counts[b] = 0
+    const bool ready = init_is_finite(init + 6 * b);
     double rf[6];
     fe.refs(rf);
 #pragma unroll
@@ -146,7 +149,7 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
         if (fe.pend) {
             bool esc;
             const Rec rc = fe.emit(esc);
-            queue.push(rc, esc, fe.p.dt);
+            if (ready) queue.push(rc, esc, fe.p.dt);
         }
     };
 

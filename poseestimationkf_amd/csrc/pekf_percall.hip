@@ -493,9 +493,8 @@ class Service {
         if (mode().load() != PEKF_PERCALL_SERVICE) return nullptr;
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
-        Service &s = instances()[dev];
-        s.dev_ = dev;  // this instance serves device dev (its wall-clock rate sets the idle limit)
-        return s.broken_ ? nullptr : &s;
+        Service &s = instances()[dev];  // instance dev serves device dev (set once, at construction)
+        return s.broken_.load() ? nullptr : &s;
     }
 
     // One request: n_in doubles in, n_out doubles out.  Returns PEKF_OK, or an error (the caller
@@ -523,7 +522,11 @@ class Service {
   private:
     static constexpr int kMaxDevices = 16;
     static Service *instances() {
-        static Service per_device[kMaxDevices];
+        static Service *per_device = [] {
+            static Service all[kMaxDevices];
+            for (int i = 0; i < kMaxDevices; ++i) all[i].dev_ = i;  // its wall-clock rate sets the idle limit
+            return all;
+        }();
         return per_device;
     }
 
@@ -622,7 +625,7 @@ class Service {
     int dev_ = 0;
     uint32_t seq_ = 0;
     std::atomic<bool> running_{false};  // read without the lock by quiesce_all
-    bool broken_ = false;
+    std::atomic<bool> broken_{false};  // read without the lock by get()
     std::chrono::steady_clock::time_point last_;
 };
 

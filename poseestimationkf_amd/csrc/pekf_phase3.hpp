@@ -26,6 +26,14 @@ __device__ __forceinline__ double time_step(const float4 v4) {
     return __hiloint2double(__float_as_int(v4.y), __float_as_int(v4.x));
 }
 
+// phase 2's result for a filter is usable (pekf_frontend_init_dev writes NaN for one that never got ready)
+__device__ __forceinline__ bool init_is_finite(const double *init6) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) ok = ok && isfinite(init6[k]);
+    return ok;
+}
+
 struct V3 {
     double x, y, z;
 };

@@ -324,8 +324,8 @@ def run_session(phase2, phase3, filters, n_avg=100, alpha=0.1):
     state (pekf_live_dev), the phase-2 results handed over in device memory.  phase3's times continue
     phase2's (its first gap is taken from phase2's last event, the time phase 3 starts from).
     filters: a BatchedEKF (FP64, AoS) whose state is advanced.  Returns dict(ready (K,) bool -- a filter
-    that never finished phase 2 has NaN references and state --, counts (K,) records applied,
-    refs (K, 6))."""
+    that never finished phase 2 has NaN references, applies no record and keeps its state --, counts
+    (K,) records applied, refs (K, 6))."""
     K = filters.batch
     assert np.asarray(phase2["types"]).shape[1] == K and np.asarray(phase2["types"]).shape[0] > 0
     assert np.asarray(phase3["types"]).shape[1] == K

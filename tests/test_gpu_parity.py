@@ -408,7 +408,7 @@ def test_dropin_north_star_aliases_equal_real_names(eng, monkeypatch):
         w = Wahba(acc0, mag0)
         assert np.array_equal(w.solve(a, m, 0.5, 0.5), w.getQuarternion(a, m, 0.5, 0.5))
     want = npo.correct(m, a, z1, Pm1, K1, acc0, mag0)
-    assert _maxerr(X2, want[0]) < 1e-13
+    assert _maxerr(X2, want[0]) < 1e-11   # raw samples: k_mag = 1 - |acc_z| ~ 0.01, LAPACK's bound ~ eps / k_mag
 
 
 @pytest.mark.gpu

@@ -155,6 +155,34 @@ def test_session_phase2_then_fused_phase3(eng):
     _same((X, P, got["counts"], got["refs"]), split)
 
 
+def test_session_leaves_filters_that_never_got_ready(eng):
+    """Filters whose phase 2 never completed (pekf_frontend_init_dev: not ready, NaN means) apply no
+    phase-3 record: counts 0 and their state untouched (not overwritten with NaN); the ready ones equal
+    the split pipeline run on them alone."""
+    K = 384
+    ph2 = synth.generate_events(np.arange(K), 520, seed=36)     # about a third never get ready
+    ph3 = synth.generate_events(np.arange(K), 400, seed=37)
+    ph3 = dict(ph3, times=ph3["times"] - ph3["t_init"][None, :] + ph2["times"][-1][None, :])
+    rng = np.random.default_rng(38)
+    X0 = rng.standard_normal((K, 4))
+    X0 /= np.linalg.norm(X0, axis=1, keepdims=True)
+    P0 = np.tile(np.eye(4) * 0.3, (K, 1, 1))
+    f = eng.BatchedEKF(K)
+    f.set_state(X0, P0)
+    got = eng.run_session(ph2, ph3, f)
+    ready = got["ready"]
+    assert 0 < ready.sum() < K
+    X, P = f.get_state()
+    assert np.all(got["counts"][~ready] == 0)
+    assert np.array_equal(X[~ready], X0[~ready]) and np.array_equal(P[~ready], P0[~ready])
+    assert np.all(got["counts"][ready] > 0) and np.isfinite(X[ready]).all()
+    ini = eng.frontend_init(ph2)
+    ev = dict(ph3, t_init=ini["t_init"], init_acc=ini["init"][:, :3], init_mag=ini["init"][:, 3:])
+    Xs, Ps, cs, _ = _split(eng, ev, K, X0, P0)
+    assert np.all(cs[~ready] == 0)                               # the split front-end skips them too
+    assert np.array_equal(X, Xs) and np.array_equal(P, Ps)
+
+
 def test_live_dense_jittered_streams(eng):
     """Records every 3-6 events at lane-dependent positions (each group of three events a random
     permutation of gyro / acc / mag): the queues fill fastest and the overflow rule decides most
