@@ -371,6 +371,8 @@ def main(argv=None):
 
     from poseestimationkf_amd import _lib
     visible = _lib.device_count()
+    if plan["mode"] == "ranks" and visible == 1 and plan["devices"][0] > 0:
+        plan["devices"] = [0]   # the launcher gave each rank its own GPU (HIP/CUDA_VISIBLE_DEVICES)
     need = max(plan["devices"]) + 1
     if visible < need:
         raise BenchError("--gpus %d (%s) needs %d visible GPU(s), %d visible" %

@@ -97,6 +97,22 @@ def test_default_key_is_shared_by_siblings_only(monkeypatch):
     assert os.path.basename(shard.FileRendezvous(1, 2).path) == "pekf-rdzv-k_.._x.id"
 
 
+def test_file_rendezvous_under_torchrun(tmp_path):
+    """The launcher the driver uses for N > 1 (torchrun, 3 ranks here): every rank gets rank 0's id
+    through the file channel, keyed by the torchrun agent (the ranks' common parent), torch-free."""
+    import subprocess
+    env = dict(os.environ, PEKF_RDZV_DIR=str(tmp_path))
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "PEKF_RDZV_KEY"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
+                          "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                          os.path.join(os.path.dirname(__file__), "_rdzv_probe.py")],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = sorted(l for l in out.stdout.splitlines() if l.startswith("RDZV"))
+    assert lines == ["RDZV rank=%d ok=1 torch=0" % r for r in range(3)], out.stdout
+
+
 def _gloo_rank(rank, world, port, directory, global_batch, window, q):
     import torch
     import torch.distributed as dist
