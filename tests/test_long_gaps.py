@@ -6,9 +6,13 @@ carries dt as a 31-bit ns count, so such a record's dt word is the escape (PEKF_
 float64 dt sits in the window's side plane (include/pekf.h); raw phone events carry a 30-bit gap,
 so a longer or negative gap is a time event (word 3, the float64 step in x / y).
 
-CPU: the packing round trips and the two oracles agree on escaped records.  GPU: the fused kernel
-(multi-record, trajectory, counts, one-record and handle launches), the front-end, the fused
-front-end + filter kernel and phase 2 against the oracles."""
+Pinned by tests/golden/gaps.npz, which tests/golden/make_gaps_golden.py made by running the reference's
+own KalmanFilter over streams with such differences (5 s and 33 s pauses, negative and fractional
+differences, 2^31 - 1 and 2^31 ns exactly).  CPU: the packing round trips, the NumPy restatement
+reproduces the reference bit for bit and the C oracle within 1e-10 on those records.  GPU: the fused
+kernel (multi-record, trajectory, counts, one-record and handle launches) against the reference's
+trajectories and the oracles, the front-end, the fused front-end + filter kernel and phase 2 against
+the oracles."""
 import numpy as np
 import pytest
 
@@ -85,6 +89,30 @@ def test_records_dt_ns_and_oracles_agree_on_escapes(oracle_c):
         assert np.abs(Xn - Xo[k]).max() < 1e-10
 
 
+def _golden():
+    import os
+
+    from .conftest import GOLDEN
+    with np.load(os.path.join(GOLDEN, "gaps.npz")) as z:
+        d = {k: z[k] for k in z}
+    base = synth.Records(d["gyro"], d["acc"], d["mag"], np.zeros(d["dt"].shape, np.uint32), d["acc0"], d["mag0"])
+    return with_dts(base, d["dt"]), d
+
+
+def test_golden_gaps_pin_the_oracles(oracle_c):
+    """The reference's own trajectories over odd time differences: the NumPy restatement bit for bit,
+    the C oracle (escaped records from the side plane) within 1e-10."""
+    rec, d = _golden()
+    assert (rec.dtw & np.uint32(synth.DT_MASK) == synth.DT_ESCAPE).sum() >= 300 + 5 * 12 // 2
+    assert np.array_equal(rec.dt_ns, d["dt"])
+    for k in range(rec.dtw.shape[1]):
+        g, dt, a, m = rec.filter(k)
+        _, _, tr = ekf_numpy.run_filter(g, dt, a, m, rec.acc0[k], rec.mag0[k])
+        assert np.array_equal(tr, d["traj"][:, k]), k
+    _, _, tro = oracle_c.run(rec, want_traj=True)
+    assert np.abs(tro.transpose(1, 0, 2) - d["traj"]).max() < 1e-10
+
+
 # ------------------------------------------------------------------------------------------ GPU
 @pytest.fixture(scope="module")
 def eng():
@@ -96,6 +124,24 @@ def eng():
 
 def _err(a, b):
     return float(np.abs(np.asarray(a) - np.asarray(b)).max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["aos", "soa"])
+def test_fused_escapes_match_the_reference_trajectories(eng, layout):
+    """tests/golden/gaps.npz through the fused kernel: every record's X within 1e-9 of the reference's,
+    from the multi-record launch (trajectory variant) and from one-record launches alike."""
+    rec, d = _golden()
+    K = rec.dtw.shape[1]
+    win = eng.IMUWindow.from_records(rec)
+    tr = eng.BatchedEKF(K, layout=layout).run(win, want_traj=True)
+    err = _err(tr, d["traj"])
+    f1 = eng.BatchedEKF(K, layout=layout)
+    for t in range(40):
+        f1.run(win, n_steps=1, step0=t)
+    err1 = _err(f1.get_state()[0], d["traj"][39])
+    print("escaped dts vs the reference (%s): max |dq| = %.3e (multi-record), %.3e (one-record)" % (layout, err, err1))
+    assert err < 1e-9 and err1 < 1e-9
 
 
 @pytest.mark.gpu
