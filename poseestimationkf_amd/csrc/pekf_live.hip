@@ -42,6 +42,9 @@ namespace pekf {
 #ifndef PEKF_LIVE_ATTR
 #define PEKF_LIVE_ATTR __attribute__((amdgpu_waves_per_eu(2)))
 #endif
+#ifndef PEKF_LIVE_PIN
+#define PEKF_LIVE_PIN 0  // the filter step's Schur inverse pinned into the Wahba chain's block (pekf_step.hpp)
+#endif
 
 // A lane's records waiting for the wave's next filter step, oldest first: a ring of Q slots per lane in
 // LDS, [slot][lane] so that a wave's accesses fall in distinct banks whatever slot each lane is at.  A
@@ -137,10 +140,11 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
             const double gy[3] = {cur.gd.x, cur.gd.y, cur.gd.z};
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
+            constexpr bool kPin = PEKF_LIVE_PIN != 0;
             if (applied == 0)
-                ekf_record_step<double, true, false, true>(x, state_norm2(x), P, Wr, kc, gy, dt, false, acc, mag);
+                ekf_record_step<double, true, false, true, kPin>(x, state_norm2(x), P, Wr, kc, gy, dt, false, acc, mag);
             else
-                ekf_record_step<double, true, true, true>(x, 1.0, P, Wr, kc, gy, dt, false, acc, mag);
+                ekf_record_step<double, true, true, true, kPin>(x, 1.0, P, Wr, kc, gy, dt, false, acc, mag);
             ++applied;
         }
         mode.leave();

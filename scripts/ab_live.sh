@@ -6,6 +6,6 @@ set -u
 for round in 1 2; do
   for lib in "$@"; do
     echo "== $lib round $round"
-    PEKF_LIB=$lib timeout -k 10 120 python3 scripts/frontend_probe.py 4 --live || exit $?
+    PEKF_LIB=$lib timeout -k 10 120 python3 scripts/frontend_probe.py ${REPS:-4} --live || exit $?
   done
 done
