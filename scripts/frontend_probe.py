@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """The front-end kernel alone (the bench_aux.py workload: 16K generated event streams tiled x64 ->
 1,048,576 filters x 1,024 events), for rocprofv3 PMC passes that should see only k_frontend; with
---live the fused front-end + filter kernel (pekf_live_dev) on the same events instead.
+--live the fused front-end + filter kernel (pekf_live_dev) on the same events instead, with --init
+phase 2 (pekf_frontend_init_dev, the means / variances of the first 100 samples).
 
-usage: python3 scripts/frontend_probe.py [reps] [--live]
+usage: python3 scripts/frontend_probe.py [reps] [--live | --init]
 """
 from __future__ import annotations
 
@@ -22,6 +23,7 @@ from poseestimationkf_amd._lib import check, lib  # noqa: E402
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     live = "--live" in sys.argv
+    phase2 = "--init" in sys.argv
     reps = int(args[0]) if args else 3
     st = engine.Stream()
     s = st.handle
@@ -41,9 +43,14 @@ def main():
     e0, e1 = engine.Event(), engine.Event()
     times = []
     f = engine.BatchedEKF(K) if live else None
+    if phase2:
+        ob, tob, rb = engine.DeviceBuffer(48 * K), engine.DeviceBuffer(8 * K), engine.DeviceBuffer(4 * K)
+        sb = engine.DeviceBuffer(96 * K)
     for _ in range(reps):
         e0.record(s)
-        if live:
+        if phase2:
+            check(lib.pekf_frontend_init_dev(K, E, evb.ptr, tb.ptr, 100, ob.ptr, tob.ptr, sb.ptr, rb.ptr, s))
+        elif live:
             f.run_events_async(evb, E, ib, tb, cnt, win.refs, 0.1, s)
         else:
             check(lib.pekf_frontend_dev(K, E, evb.ptr, ib.ptr, tb.ptr, 0.1, r_max, win.gd.ptr, win.am.ptr,
@@ -51,6 +58,12 @@ def main():
         e1.record(s)
         e1.sync()
         times.append(e0.elapsed_ms(e1))
+    if phase2:
+        ready = int(rb.download((K,), np.int32).sum())
+        digest = float(np.nansum(sb.download((K, 12), np.float64)))
+        print("frontend_probe --init: %d filters x %d events, %d ready, stats digest %.17g, ms %s"
+              % (K, E, ready, digest, ["%.3f" % t for t in times]))
+        return
     recs = int(cnt.download((K,), np.int32).sum())
     print("frontend_probe%s: %d filters x %d events, %d records, ms %s"
           % (" --live" if live else "", K, E, recs, ["%.3f" % t for t in times]))
