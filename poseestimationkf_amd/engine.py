@@ -284,15 +284,22 @@ def run_frontend(ev, alpha=0.1, r_max=None):
     init = DeviceBuffer(48 * K).upload(np.concatenate([ev["init_acc"], ev["init_mag"]], axis=1).astype(np.float64))
     tib = DeviceBuffer(8 * K).upload(np.ascontiguousarray(ev["t_init"], np.int64))
     win = IMUWindow(K, max(1, r_max))
-    dtx = DeviceBuffer(8 * K * max(1, r_max))
     cnt = DeviceBuffer(4 * K)
-    errb = DeviceBuffer(4).upload(np.zeros(1, np.int32))
-    check(lib.pekf_frontend_ext_dev(K, E, evb.ptr, init.ptr, tib.ptr, float(alpha), r_max, win.gd.ptr,
-                                    win.am.ptr, win.my.ptr, dtx.ptr, cnt.ptr, win.refs.ptr, flags, errb.ptr, None))
-    check(lib.pekf_device_sync())
-    err = int(errb.download((1,), np.int32)[0])
-    if err & 1:
-        raise ValueError("a record's dt does not fit the 31-bit ns field of the stream")
+    errb = DeviceBuffer(4)
+    dtx = None
+    while True:
+        # without a side plane first; only if some record's dt does not fit the dt word (err bit 1: a
+        # pause of 2^31 ns or more) run again with one (8 B per record slot, kept in win.dtx)
+        errb.upload(np.zeros(1, np.int32))
+        check(lib.pekf_frontend_ext_dev(K, E, evb.ptr, init.ptr, tib.ptr, float(alpha), r_max, win.gd.ptr,
+                                        win.am.ptr, win.my.ptr, dtx.ptr if dtx is not None else None, cnt.ptr,
+                                        win.refs.ptr, flags, errb.ptr, None))
+        check(lib.pekf_device_sync())
+        err = int(errb.download((1,), np.int32)[0])
+        if err & 1 and dtx is None:
+            dtx = DeviceBuffer(8 * K * max(1, r_max))
+            continue
+        break
     if err & 2:
         raise ValueError("more than r_max=%d records for some filter" % r_max)
     if err & 4:
