@@ -59,8 +59,6 @@ def test_native_ingest_matches_python_reader(c1_log):
 
 
 def test_native_ingest_errors_are_reported(tmp_path):
-    import ctypes
-
     from poseestimationkf_amd import _lib, engine
     bad = tmp_path / "bad.txt"
     bad.write_text("mag_0 : 1,0,0\nacc_0 : 0,0,1\ngyro : 0,0,0\nT : 0\nT : 0.5\nMag_1 : 1,0,0\nAcc_1 : 0,0,1\n")
@@ -78,7 +76,6 @@ def test_native_ingest_errors_are_reported(tmp_path):
     short.write_text("mag_0 : 1,0,0\nacc_0 : 0,0,1\nMag_1 : 1,0,0\nAcc_1 : 0,0,1\n")
     with pytest.raises(_lib.PekfError, match="Acc_1 records"):
         engine.read_log_records(str(short))
-    assert ctypes  # (imported for the raw call above)
 
 
 def test_native_ingest_escapes_long_negative_and_fractional_gaps(tmp_path):
