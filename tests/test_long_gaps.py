@@ -145,6 +145,26 @@ def test_fused_escapes_match_the_reference_trajectories(eng, layout):
 
 
 @pytest.mark.gpu
+def test_fused_escapes_with_missing_magnetometer(eng, oracle_c):
+    """Escaped dt words with the missing-magnetometer bit set (word 0xFFFFFFFF): the Wahba-skip rule and
+    the side plane's dt apply together (config 5's stream with pauses)."""
+    K, W = 512, 48
+    rec = synth.generate(np.arange(K), W, seed=43, missing=True)
+    dt = rec.dt_ns.copy()
+    dt[::5, ::3] = 7.5e9
+    dt[3::7, 1::4] = -4e6
+    rec = with_dts(rec, dt)
+    both = ((rec.dtw & np.uint32(synth.DT_MASK)) == synth.DT_ESCAPE) & rec.missing
+    assert both.sum() > 100
+    win = eng.IMUWindow.from_records(rec)
+    f = eng.BatchedEKF(K)
+    f.run(win, n_steps=90, step0=11)
+    Xo, Po, _ = oracle_c.run(rec, n_steps=90, step0=11)
+    X, P = f.get_state()
+    assert _err(X, Xo) < 1e-9 and _err(P, Po) < 1e-9
+
+
+@pytest.mark.gpu
 def test_fused_run_with_escaped_dts(eng, oracle_c):
     """Every launch shape of the fused kernel reads escaped records' dt from the side plane."""
     rec = _escaped_records()
@@ -195,8 +215,12 @@ def _paused_events(K, E, seed):
             t[rng.integers(1, E):, k] += 5_000_000_000
         if k % 4 == 1:                          # the phone clock steps back 0.5 s
             t[rng.integers(1, E):, k] -= 500_000_000
-        if k % 7 == 2:                          # a pause just under the 30-bit event field, twice
+        if k % 7 == 2:                          # a pause just over the 30-bit event field
             t[rng.integers(1, E):, k] += (1 << 30) + 12345
+        if k % 5 == 3:                          # the very first event 4 s after t_init
+            t[:, k] += 4_000_000_000
+        if k % 11 == 6:                         # the very first event before t_init
+            t[:, k] -= 30_000_000
     return dict(ev, times=t)
 
 
