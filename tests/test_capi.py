@@ -115,3 +115,29 @@ def test_product_package_never_imports_the_oracle():
             if f.endswith((".py", ".hip", ".hpp", ".cpp")):
                 src = open(os.path.join(dirpath, f)).read()
                 assert not re.search(r"^\s*(from|import)\s+oracle|ekf_oracle|oracle_c|ekf_numpy", src, re.M), f
+
+
+def test_round3_entry_points_check_their_arguments():
+    """The dt-escape / time-event entry points validate before touching a device (CPU)."""
+    from poseestimationkf_amd import _lib
+    L = _lib.lib
+    st = L.pekf_run_ext_dev(4, 2, 1, 0, None, None, None, None, None, None, None, 1.0, 0.1, None, None, 0, None)
+    assert st == _lib.PEKF_ERR_INVALID and "null" in _lib.last_error()
+    st = L.pekf_run_ext_dev(4, 2, 1, 0, 16, 16, 8, 4, 8, 8, 8, 1.0, 0.1, None, None, 0, None)  # dt_ext % 8 != 0
+    assert st == _lib.PEKF_ERR_INVALID and "misaligned" in _lib.last_error()
+    assert L.pekf_run_ext_dev(0, 5, 1, 0, None, None, None, None, None, None, None, 1.0, 0.1, None, None, 0,
+                              None) == _lib.PEKF_OK                                     # empty batch: no-op
+    st = L.pekf_frontend_ext_dev(4, 8, None, None, None, 0.1, 3, None, None, None, None, None, None, 0x2, None, None)
+    assert st == _lib.PEKF_ERR_INVALID and "flags" in _lib.last_error()
+    st = L.pekf_frontend_ext_dev(4, 8, None, None, None, 0.1, 3, None, None, None, None, None, None, 0x1, None, None)
+    assert st == _lib.PEKF_ERR_INVALID and "null" in _lib.last_error()
+    st = L.pekf_live_ext_dev(4, 8, None, None, None, 0.1, None, None, 1.0, 0.1, None, None, 0x8, None, None)
+    assert st == _lib.PEKF_ERR_INVALID and "flags" in _lib.last_error()
+    st = L.pekf_live_ext_dev(-1, 8, None, None, None, 0.1, None, None, 1.0, 0.1, None, None, 0, None, None)
+    assert st == _lib.PEKF_ERR_INVALID and "negative" in _lib.last_error()
+    st = L.pekf_log_read_ext(b"/nonexistent", 1, None, None, None, None, None, None, None, None, None)
+    assert st == _lib.PEKF_ERR_INVALID and "null" in _lib.last_error()
+    h = ctypes.c_void_p()
+    st = L.pekf_filter_run_ext(None, 2, 1, 0, None, None, None, None, None, None, None)
+    assert st == _lib.PEKF_ERR_INVALID and "handle" in _lib.last_error()
+    assert h.value is None
