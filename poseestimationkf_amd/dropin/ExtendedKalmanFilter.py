@@ -8,11 +8,20 @@ per-call gfx950 kernels of libpekf.so (k_predict, k_correct, k_rk4, ...); the tw
 methods go through the CPython binding ``_fastcall`` (same C entry points, less call overhead).  For many
 filters at once use ``poseestimationkf_amd.engine.BatchedEKF`` (the fused kernel).
 ``predict`` / ``update`` are aliases of ``Prediction`` / ``Correction`` (the north_star's names).
+
+Per-record calls are answered by a resident kernel that polls pinned host memory and leaves 5 ms
+after the last call; a device-wide synchronisation elsewhere in the process may wait for it.  To
+launch one kernel per call instead (identical results): ``PEKF_PERCALL=launch`` in the environment,
+or ``percall_mode(PERCALL_LAUNCH)`` from this module.
 """
 import numpy as np
 from _bootstrap import engine as _eng
 from _bootstrap import fastcall as _fc
 from Wahba import Wahba
+
+# the per-call service switch (include/pekf.h: pekf_set_percall_mode), re-exported for the drop-in's users
+percall_mode = _eng.percall_mode
+PERCALL_SERVICE, PERCALL_LAUNCH = _eng.PERCALL_SERVICE, _eng.PERCALL_LAUNCH
 
 
 class KalmanFilter:

@@ -23,6 +23,26 @@ def test_mode_api_rejects_unknown_modes():
     assert lib.pekf_get_percall_mode(ctypes.byref(m)) == 0 and m.value in (0, 1)
 
 
+def test_dropin_module_exposes_the_mode_switch(monkeypatch):
+    """The switch is reachable from the module main_file.py imports (no GPU needed to set the mode)."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    monkeypatch.syspath_prepend(os.path.join(root, "poseestimationkf_amd", "dropin"))
+    sys.modules.pop("ExtendedKalmanFilter", None)
+    import ExtendedKalmanFilter as ekf
+    prev = ekf.percall_mode()
+    try:
+        assert ekf.percall_mode(ekf.PERCALL_LAUNCH) == ekf.PERCALL_LAUNCH
+        m = ctypes.c_int(-1)
+        assert lib.pekf_get_percall_mode(ctypes.byref(m)) == 0 and m.value == ekf.PERCALL_LAUNCH
+        assert ekf.percall_mode(ekf.PERCALL_SERVICE) == ekf.PERCALL_SERVICE
+    finally:
+        ekf.percall_mode(prev)
+        for name in ("ExtendedKalmanFilter", "Wahba", "_bootstrap"):
+            sys.modules.pop(name, None)
+
+
 @pytest.fixture()
 def eng():
     from poseestimationkf_amd import engine
