@@ -9,7 +9,8 @@ so a longer or negative gap is a time event (word 3, the float64 step in x / y).
 Pinned by tests/golden/gaps.npz, which tests/golden/make_gaps_golden.py made by running the reference's
 own KalmanFilter over streams with such differences (5 s and 33 s pauses, negative and fractional
 differences, 2^31 - 1 and 2^31 ns exactly).  CPU: the packing round trips, the NumPy restatement
-reproduces the reference bit for bit and the C oracle within 1e-10 on those records.  GPU: the fused
+reproduces the reference bit for bit and the C oracle within 1e-10 on those records.  GPU: the
+per-record drop-in loop (the per-call kernels, dt = T - previousT) and the fused
 kernel (multi-record, trajectory, counts, one-record and handle launches) against the reference's
 trajectories and the oracles, the front-end, the fused front-end + filter kernel and phase 2 against
 the oracles."""
@@ -142,6 +143,38 @@ def test_fused_escapes_match_the_reference_trajectories(eng, layout):
     err1 = _err(f1.get_state()[0], d["traj"][39])
     print("escaped dts vs the reference (%s): max |dq| = %.3e (multi-record), %.3e (one-record)" % (layout, err, err1))
     assert err < 1e-9 and err1 < 1e-9
+
+
+@pytest.mark.gpu
+def test_dropin_loop_over_odd_time_differences(eng, monkeypatch):
+    """The per-record drop-in (main_file.py's loop through dropin/ExtendedKalmanFilter.py) on the golden
+    streams, with the absolute timestamps the reference saw: pauses, a clock stepping back, fractional
+    differences reach the per-call kernels as T - previousT, and every X matches the reference's."""
+    import os
+    import sys
+
+    from .conftest import ROOT
+    rec, d = _golden()
+    monkeypatch.syspath_prepend(os.path.join(ROOT, "poseestimationkf_amd", "dropin"))
+    for m in ("ExtendedKalmanFilter", "Wahba", "UtilityFunctions", "_bootstrap"):
+        sys.modules.pop(m, None)
+    from ExtendedKalmanFilter import KalmanFilter
+    W, K = d["dt"].shape
+    err = 0.0
+    for k in (1, 3, 5):   # filter 3 pauses 5 s before every record
+        kf = KalmanFilter(d["t0"][k], d["mag0"][k], d["acc0"][k], 0.5)
+        kf.setQ(1)
+        kf.setR(0.1)
+        X, P, T = np.asarray([1., 0., 0., 0.]), np.identity(4), d["t0"][k]
+        for i in range(W):
+            T = T + d["dt"][i, k]
+            z, Pm, Kk = kf.Prediction(d["gyro"][i, k].astype(np.float64), T, X, P)
+            X, P = kf.Correction(d["mag"][i, k].astype(np.float64), d["acc"][i, k].astype(np.float64), z, Pm, Kk)
+            err = max(err, _err(X, d["traj"][i, k]))
+    for m in ("ExtendedKalmanFilter", "Wahba", "UtilityFunctions", "_bootstrap"):
+        sys.modules.pop(m, None)
+    print("drop-in loop over odd time differences vs the reference: max |dq| = %.3e" % err)
+    assert err < 1e-11
 
 
 @pytest.mark.gpu
