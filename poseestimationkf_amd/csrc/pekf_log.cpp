@@ -55,10 +55,11 @@ bool values(const char *line, std::vector<double> &dst, int want) {
 int parse(const char *path, LogColumns &c) {
     FILE *f = std::fopen(path, "r");
     if (!f) return pekf::set_error(PEKF_ERR_INVALID, "cannot open log '%s': %s", path, std::strerror(errno));
-    char buf[4096];
+    char *buf = nullptr;  // whole lines of any length, as Python's line iteration gives them
+    size_t cap = 0;
     int64_t lineno = 0;
     int status = PEKF_OK;
-    while (std::fgets(buf, sizeof(buf), f)) {
+    while (getline(&buf, &cap, f) != -1) {
         ++lineno;
         const char *l = buf;
         bool ok = true;
@@ -87,6 +88,7 @@ int parse(const char *path, LogColumns &c) {
             break;
         }
     }
+    std::free(buf);
     std::fclose(f);
     return status;
 }

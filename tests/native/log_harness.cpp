@@ -1,0 +1,45 @@
+// Host-only harness for the native log reader (csrc/pekf_log.cpp) under AddressSanitizer and
+// UndefinedBehaviorSanitizer (tests/test_log_sanitizers.py builds and runs it; no GPU, no HIP).
+// Each argument is a log path: scan it, then read it with and without the dt side plane and with one
+// record too many.  pekf::set_error (pekf_capi.hip in the library) is replaced by a printing stub.
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <vector>
+
+#include "pekf.h"
+
+namespace pekf {
+int set_error(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    char msg[512];
+    vsnprintf(msg, sizeof msg, fmt, ap);
+    va_end(ap);
+    fprintf(stderr, "error %d: %s\n", code, msg);
+    return code;
+}
+}  // namespace pekf
+
+int main(int argc, char **argv) {
+    for (int i = 1; i < argc; ++i) {
+        int64_t n = -1;
+        int st = pekf_log_scan(argv[i], &n);
+        printf("%s scan=%d records=%lld", argv[i], st, (long long)n);
+        if (st == 0 && n > 0) {
+            std::vector<float> g(3 * n), a(3 * n), m(3 * n);
+            std::vector<uint32_t> dtw(n);
+            std::vector<double> dtx(n);
+            double acc0[3], mag0[3], t0 = 0;
+            int64_t esc = -1;
+            const int ext = pekf_log_read_ext(argv[i], n, g.data(), a.data(), m.data(), dtw.data(), dtx.data(), &esc,
+                                              acc0, mag0, &t0);
+            const int plain = pekf_log_read(argv[i], n, g.data(), a.data(), m.data(), dtw.data(), acc0, mag0, &t0);
+            const int over = pekf_log_read_ext(argv[i], n + 1, g.data(), a.data(), m.data(), dtw.data(), dtx.data(),
+                                               &esc, acc0, mag0, &t0);
+            printf(" ext=%d escaped=%lld plain=%d over=%d", ext, (long long)esc, plain, over);
+        }
+        printf("\n");
+    }
+    return 0;
+}

@@ -1,0 +1,76 @@
+"""The native log reader (csrc/pekf_log.cpp: host code that parses untrusted text) under AddressSanitizer
+and UndefinedBehaviorSanitizer: tests/native/log_harness.cpp, built here with g++ against the reader's
+source, scans and reads well-formed logs (pauses, a clock stepping back, lines of any length) and broken
+ones (truncated, a missing value, no colon, binary bytes, empty, absent) without a sanitizer report,
+with the results the library reports."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from poseestimationkf_amd import logformat, synth
+
+from .conftest import ROOT
+
+
+@pytest.fixture(scope="module")
+def harness(tmp_path_factory):
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    out = tmp_path_factory.mktemp("asan") / "log_harness"
+    cmd = ["g++", "-g", "-O1", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+           "-fno-omit-frame-pointer", "-I" + os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "tests", "native", "log_harness.cpp"),
+           os.path.join(ROOT, "poseestimationkf_amd", "csrc", "pekf_log.cpp"), "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return str(out)
+
+
+def _logs(d):
+    rng = np.random.default_rng(5)
+    n = 120
+    ts = np.cumsum(np.r_[1e12, rng.integers(4_000_000, 20_000_000, n)]).astype(np.float64)
+    ts[40:] += 5e9          # a 5 s pause
+    ts[70:] -= 3e7          # the clock steps back
+    g, a, m = rng.normal(size=(3, n, 3))
+    good = d / "good.txt"
+    logformat.write_log(str(good), ts, g, a, m, [0, 0, 1.0], [0.5, 0, -0.8])
+    lines = good.read_text().splitlines(keepends=True)
+    files = {"good": good}
+    files["trunc"] = d / "trunc.txt"
+    files["trunc"].write_text("".join(lines[:len(lines) // 2]))
+    bad = list(lines)
+    i = next(k for k, l in enumerate(bad) if l.startswith("Acc_1"))
+    bad[i] = "Acc_1 : 1.0,,2\n"
+    files["missing_value"] = d / "missing_value.txt"
+    files["missing_value"].write_text("".join(bad))
+    long = list(lines)
+    long[3] = "X_k : " + ", ".join(["1.0"] * 4000) + "\n"
+    files["long_lines"] = d / "long_lines.txt"
+    files["long_lines"].write_text("".join(long))
+    files["no_colon"] = d / "no_colon.txt"
+    files["no_colon"].write_text("gyro 1 2 3\nT\n")
+    files["binary"] = d / "binary.bin"
+    files["binary"].write_bytes(bytes(range(256)) * 40)
+    files["empty"] = d / "empty.txt"
+    files["empty"].write_text("")
+    files["absent"] = d / "absent.txt"
+    return files
+
+
+def test_log_reader_under_sanitizers(harness, tmp_path):
+    files = _logs(tmp_path)
+    r = subprocess.run([harness] + [str(p) for p in files.values()], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
+                                UBSAN_OPTIONS="print_stacktrace=1"))
+    report = r.stdout + r.stderr
+    assert r.returncode == 0 and "Sanitizer" not in report and "runtime error" not in report, report[-3000:]
+    got = dict(zip(files, r.stdout.splitlines()))
+    for name in ("good", "long_lines"):
+        assert "scan=0 records=120 ext=0 escaped=2 plain=1 over=1" in got[name], got[name]
+    assert " scan=0 " in got["trunc"] and " ext=0 " in got["trunc"]
+    for name in ("missing_value", "no_colon", "binary", "empty", "absent"):
+        assert " scan=1 " in got[name], got[name]

@@ -105,3 +105,25 @@ def test_native_ingest_escapes_long_negative_and_fractional_gaps(tmp_path):
     esc = got.dtw[:, 0] & synth.DT_MASK
     assert np.nonzero(esc == synth.DT_ESCAPE)[0].tolist() == [2, 4, 5, 7]
     assert got.dtx is not None and got.dtx[2, 0] == 5e9 and got.dtx[4, 0] == -3e6
+
+
+def test_native_ingest_takes_lines_of_any_length(tmp_path):
+    """A line is a line however long (Python's line iteration, ReadFile.py:27): a 3,000-value side
+    channel and a sample padded with 6,000 blanks parse as the Python reader parses them."""
+    from poseestimationkf_amd import engine
+    rec = synth.generate(np.arange(1), 6)
+    g, d, a, m = rec.filter(0)
+    ts = synth.c1_timestamps(d.astype(np.int64))
+    path = tmp_path / "long.txt"
+    with open(path, "w") as fh:
+        logformat.write_log(fh, ts, g, a, m, rec.acc0[0], rec.mag0[0])
+    lines = path.read_text().splitlines(keepends=True)
+    x = next(i for i, l in enumerate(lines) if l.startswith("X_k"))
+    lines[x] = "X_k : " + ", ".join(["1.0"] * 3000) + "\n"
+    gi = next(i for i, l in enumerate(lines) if l.startswith("gyro"))
+    lines[gi] = "gyro : " + " " * 6000 + "0.25, -0.5, 0.125\n"
+    path.write_text("".join(lines))
+    got = engine.read_log_records(str(path))
+    gp, dt_py, ap, mp, _, _ = logformat.log_to_arrays(logformat.read_log(str(path)))
+    assert got.dtw.shape == (6, 1) and np.array_equal(got.dt_ns[:, 0], dt_py)
+    assert np.array_equal(got.gyro[:, 0], gp.astype(np.float32)) and got.gyro[0, 0].tolist() == [0.25, -0.5, 0.125]
