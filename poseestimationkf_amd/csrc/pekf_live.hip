@@ -134,6 +134,14 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
         const bool has = queue.n > 0;
         double dt;
         const Rec cur = queue.pop(dt);
+        auto reload = [&](double *a, double *m) {  // rare: the degenerate-Wahba fallback
+            // the popped record stays in its slot (the one before head) until a later push
+            const int slot = queue.head == 0 ? kQueue - 1 : queue.head - 1;
+            const float4 va = q_am[slot][threadIdx.x];
+            const float2 vm = q_my[slot][threadIdx.x];
+            a[0] = va.x; a[1] = va.y; a[2] = va.z;
+            m[0] = va.w; m[1] = vm.x; m[2] = vm.y;
+        };
         OmodMode mode;
         mode.enter();
         if (has) {
@@ -142,9 +150,10 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
             constexpr bool kPin = PEKF_LIVE_PIN != 0;
             if (applied == 0)
-                ekf_record_step<double, true, false, true, kPin>(x, state_norm2(x), P, Wr, kc, gy, dt, false, acc, mag);
+                ekf_record_step<double, true, false, true, kPin>(x, state_norm2(x), P, Wr, kc, gy, dt, false, acc, mag,
+                                                                 reload);
             else
-                ekf_record_step<double, true, true, true, kPin>(x, 1.0, P, Wr, kc, gy, dt, false, acc, mag);
+                ekf_record_step<double, true, true, true, kPin>(x, 1.0, P, Wr, kc, gy, dt, false, acc, mag, reload);
             ++applied;
         }
         mode.leave();

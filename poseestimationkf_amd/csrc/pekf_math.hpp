@@ -330,12 +330,135 @@ PEKF_DEV bool wahba_b_finite(const double *acc0, const double *mag0, const doubl
     return ok;
 }
 
+// A frame whose pair does not span a plane to working accuracy: a zero vector (make_frame divides 0 by
+// 0: NaN), or m parallel to a, where Gram-Schmidt's remainder t = m - (m.e1) e1 is rounding noise and e2
+// = t/|t| is not orthogonal to e1 (|t| < 1e-12 |m|).  NaN inputs count as degenerate too.
+PEKF_DEV bool frame_degenerate(const Frame &F) {
+    return !(F.beta2 * F.beta2 > 1e-24 * (F.beta1 * F.beta1 + F.beta2 * F.beta2)) || !(F.e1[0] == F.e1[0]);
+}
+
+// ---- Wahba with a rank-deficient B (Wahba.py:8-17) ----
+// A zero acc or mag sample, or acc parallel to mag, in either pair makes B = ka acc0 acc^T +
+// km mag0 mag^T = w v^T.  Every rotation taking v/|v| to w/|w| attains the optimum tr(R^T B) = |w||v|,
+// and np.linalg.svd (Wahba.py:14) picks one of them by the rounding noise of B's zero singular values,
+// which no other evaluation reproduces; these take the shortest arc.  B = 0 (both samples zero) gives
+// NaN, as the reference does there: its SVD returns U = V = I and RotationMatrix2Quart of the identity
+// divides 0 by 0 (Wahba.py:41-46).  Branch-free (selects only): in the fused kernels they run inside
+// the rare fallback branch, where a nested divergent branch would hold another exec mask in scalar
+// registers across the whole loop.
+
+// the rotation taking the unit vector v to the unit vector w about v x w (Rodrigues); for w = -v half a
+// turn about a normal of v (v x the coordinate axis least aligned with v)
+template <int FAST>
+PEKF_DEV void shortest_arc(const double *v, const double *w, double *R) {
+    const double c = v[0] * w[0] + v[1] * w[1] + v[2] * w[2];
+    const double k[3] = {v[1] * w[2] - v[2] * w[1], v[2] * w[0] - v[0] * w[2], v[0] * w[1] - v[1] * w[0]};
+    const double sk = k[0] * k[0] + k[1] * k[1] + k[2] * k[2];
+    const double ax = fabs(v[0]), ay = fabs(v[1]), az = fabs(v[2]);
+    const bool j0 = ax <= ay && ax <= az, j1 = !j0 && ay <= az;
+    const double n[3] = {j0 ? 0.0 : (j1 ? -v[2] : v[1]), j0 ? v[2] : (j1 ? 0.0 : -v[0]),
+                         j0 ? -v[1] : (j1 ? v[0] : 0.0)};
+    // R = c I + [k]x + (1 - c) h h^T, k = sin(theta) h (h: k's direction, or n where k = 0)
+    const bool use_k = sk > 0.0;
+    const double ih = rsqrt<FAST>(use_k ? sk : n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    const double h[3] = {(use_k ? k[0] : n[0]) * ih, (use_k ? k[1] : n[1]) * ih, (use_k ? k[2] : n[2]) * ih};
+    const double d = 1.0 - c;
+    R[0] = c + d * h[0] * h[0];    R[1] = d * h[0] * h[1] - k[2]; R[2] = d * h[0] * h[2] + k[1];
+    R[3] = d * h[1] * h[0] + k[2]; R[4] = c + d * h[1] * h[1];    R[5] = d * h[1] * h[2] - k[0];
+    R[6] = d * h[2] * h[0] - k[1]; R[7] = d * h[2] * h[1] + k[0]; R[8] = c + d * h[2] * h[2];
+}
+
+// Any rank-deficient B (the per-call operators, where either pair may be degenerate): B is formed, its
+// longest row gives v's direction and B v the image's.
+template <int FAST = 0>
+PEKF_DEV void wahba_rank1_rotation(const double *acc0, const double *mag0, const double *acc, const double *mag,
+                                   double ka, double km, double *R) {
+    double B[9], rn[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) B[3 * i + j] = ka * (acc0[i] * acc[j]) + km * (mag0[i] * mag[j]);
+        rn[i] = B[3 * i] * B[3 * i] + B[3 * i + 1] * B[3 * i + 1] + B[3 * i + 2] * B[3 * i + 2];
+    }
+    const bool r0 = rn[0] >= rn[1] && rn[0] >= rn[2], r1 = !r0 && rn[1] >= rn[2];
+    const double iv = rsqrt<FAST>(r0 ? rn[0] : (r1 ? rn[1] : rn[2]));
+    double v[3], w[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) v[j] = (r0 ? B[j] : (r1 ? B[3 + j] : B[6 + j])) * iv;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) w[i] = B[3 * i] * v[0] + B[3 * i + 1] * v[1] + B[3 * i + 2] * v[2];
+    const double iw = rsqrt<FAST>(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    w[0] *= iw; w[1] *= iw; w[2] *= iw;
+    shortest_arc<FAST>(v, w, R);
+}
+
+// The fused kernels' case: the reference pair spans a plane (it defines the filter's frame) and the
+// current one does not.  Then v is acc's direction (mag's where acc = 0), acc = alpha v, mag = beta v and
+// w = ka alpha acc0 + km beta mag0: no B, few registers.
+template <int FAST>
+PEKF_DEV void wahba_current_rank1(const double *acc0, const double *mag0, const double *acc, const double *mag,
+                                  double ka, double km, double *R) {
+    const double sa = acc[0] * acc[0] + acc[1] * acc[1] + acc[2] * acc[2];
+    const bool ua = sa > 0.0;
+    const double u[3] = {ua ? acc[0] : mag[0], ua ? acc[1] : mag[1], ua ? acc[2] : mag[2]};
+    const double iu = rsqrt<FAST>(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+    const double v[3] = {u[0] * iu, u[1] * iu, u[2] * iu};
+    const double al = ka * (acc[0] * v[0] + acc[1] * v[1] + acc[2] * v[2]);
+    const double be = km * (mag[0] * v[0] + mag[1] * v[1] + mag[2] * v[2]);
+    double w[3] = {al * acc0[0] + be * mag0[0], al * acc0[1] + be * mag0[1], al * acc0[2] + be * mag0[2]};
+    const double iw = rsqrt<FAST>(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    w[0] *= iw; w[1] *= iw; w[2] *= iw;
+    shortest_arc<FAST>(v, w, R);
+}
+
+// wahba_current_rank1's rotation as its quaternion, for the fused kernels' fallback: the shortest arc
+// from v to w is q = normalise(1 + v.w, v x w) (w = -v: half a turn, (0, n)), in RotationMatrix2Quart's
+// convention (R(q) v = w), so no rotation matrix is formed.
+template <int FAST>
+PEKF_DEV void wahba_current_rank1_quat(const double *acc0, const double *mag0, const double *acc, const double *mag,
+                                       double ka, double km, double *q) {
+    const double sa = acc[0] * acc[0] + acc[1] * acc[1] + acc[2] * acc[2];
+    const bool ua = sa > 0.0;
+    const double u[3] = {ua ? acc[0] : mag[0], ua ? acc[1] : mag[1], ua ? acc[2] : mag[2]};
+    const double iu = rsqrt<FAST>(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+    const double v[3] = {u[0] * iu, u[1] * iu, u[2] * iu};
+    const double al = ka * (acc[0] * v[0] + acc[1] * v[1] + acc[2] * v[2]);
+    const double be = km * (mag[0] * v[0] + mag[1] * v[1] + mag[2] * v[2]);
+    const double w[3] = {al * acc0[0] + be * mag0[0], al * acc0[1] + be * mag0[1], al * acc0[2] + be * mag0[2]};
+    const double iw = rsqrt<FAST>(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    // (1 + v.w) |w| and (v x w) |w|: the scale drops out in the normalisation
+    const double c1 = fma(v[0], w[0] * iw, fma(v[1], w[1] * iw, fma(v[2], w[2] * iw, 1.0)));
+    const double k[3] = {(v[1] * w[2] - v[2] * w[1]) * iw, (v[2] * w[0] - v[0] * w[2]) * iw,
+                         (v[0] * w[1] - v[1] * w[0]) * iw};
+    const double nq = c1 * c1 + k[0] * k[0] + k[1] * k[1] + k[2] * k[2];
+    const double ax = fabs(v[0]), ay = fabs(v[1]), az = fabs(v[2]);
+    const bool j0 = ax <= ay && ax <= az, j1 = !j0 && ay <= az;
+    const double n[3] = {j0 ? 0.0 : (j1 ? -v[2] : v[1]), j0 ? v[2] : (j1 ? 0.0 : -v[0]),
+                         j0 ? -v[1] : (j1 ? v[0] : 0.0)};
+    const bool half = !(nq > 0.0) && (iw == iw);  // w = -v exactly (NaN w, i.e. B = 0, stays NaN)
+    const double t[4] = {half ? 0.0 : c1, half ? n[0] : k[0], half ? n[1] : k[1], half ? n[2] : k[2]};
+    const double it = rsqrt<FAST>(t[0] * t[0] + t[1] * t[1] + t[2] * t[2] + t[3] * t[3]);
+    q[0] = t[0] * it; q[1] = t[1] * it; q[2] = t[2] * it; q[3] = t[3] * it;
+}
+
+// the reference pair of a frame built with sg = 1: acc0 = alpha e1, mag0 = beta1 e1 + beta2 e2
+PEKF_DEV void frame_pair(const Frame &F, double *a, double *m) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        a[i] = F.alpha * F.e1[i];
+        m[i] = F.beta1 * F.e1[i] + F.beta2 * F.e2[i];
+    }
+}
+
 PEKF_DEV void wahba_rotation_vectors(const double *acc0, const double *mag0, const double *acc,
                                      const double *mag, double ka, double km, double *R) {
     Frame W, V;
     make_frame(acc0, mag0, W);
     make_frame(acc, mag, V, wahba_sign(ka, km));
-    wahba_rotation(W, V, ka, km, R);
+    if (frame_degenerate(W) || frame_degenerate(V))
+        wahba_rank1_rotation(acc0, mag0, acc, mag, ka, km, R);
+    else
+        wahba_rotation(W, V, ka, km, R);
 }
 
 // Branch-free RotationMatrix2Quart for the fused kernel: the reference's branch choice
@@ -497,9 +620,14 @@ struct NoPin {
     PEKF_DEV void operator()() const {}
 };
 // pin(): called after v = Q4 z and before the fallback branch (see ekf_record_step's PEKF_PIN_SCHUR)
-template <int F = 1, class RW, class Pin = NoPin, std::enable_if_t<RW::kRefBasis, int> = 0>
+// reload(acc, mag): the record's samples again, for a degenerate current frame only (a zero sample or acc
+// parallel to mag, rank-1 B): V is NaN there, so is nv, and the fallback branch -- taken for NaN too --
+// solves Wahba by wahba_current_rank1_quat with the reference's weights |acc_z|, 1 - |acc_z|
+// (ExtendedKalmanFilter.py:71).  The caller re-reads them (memory, LDS) instead of holding six doubles
+// in registers through the Wahba chain.
+template <int F = 1, class RW, class Reload, class Pin = NoPin, std::enable_if_t<RW::kRefBasis, int> = 0>
 PEKF_DEV void wahba_quat_toward(const RW &W, const Frame &V, double ka, double km, const double *z, double *v,
-                                double &sc, const Pin &pin = Pin()) {
+                                double &sc, const Reload &reload, const Pin &pin = Pin()) {
     const double kw = km * W.b2W, kb = km * W.b1W;
     double p = ka * W.aW * V.alpha + kb * V.beta1 + kw * V.beta2;
     double s = kw * V.beta1 - kb * V.beta2;
@@ -517,7 +645,7 @@ PEKF_DEV void wahba_quat_toward(const RW &W, const Frame &V, double ka, double k
     q4_times(R, z, v, nv, t0);
     sc = rsqrt<F>(nv);
     pin();
-    if (PEKF_TAKEN(nv < 1.0, false)) {
+    if (PEKF_TAKEN(!(nv >= 1.0), false)) {  // (nv < 1, or NaN)
         double Fw[9], Rw[9], zw[4], vw[4], qw[4];
         W.quat(qw);
         quat_to_rotm(qw, Fw);
@@ -528,17 +656,41 @@ PEKF_DEV void wahba_quat_toward(const RW &W, const Frame &V, double ka, double k
         qmul_left<false>(qw, z, zw);
         rotm_to_quat_flip_reference(Rw, zw, vw, sc);
         qmul_left<true>(qw, vw, v);
+        // NaN: a degenerate current frame.  In this basis B' = Fw^T B pairs acc, mag with the reference
+        // pair's own coordinates (aW, 0, 0), (b1W, b2W, 0); its shortest-arc attitude, flipped toward z
+        // as ExtendedKalmanFilter.py:73-75 flips, replaces the NaN one.
+        if (!(nv == nv)) {  // (it overwrites v and sc in place)
+            double acc[3], mag[3];
+            reload(acc, mag);
+            const double a0[3] = {W.aW, 0.0, 0.0}, m0[3] = {W.b1W, W.b2W, 0.0}, kr = fabs(acc[2]);
+            wahba_current_rank1_quat<1>(a0, m0, acc, mag, kr, 1.0 - kr, v);
+            sc = v[0] * z[0] + v[1] * z[1] + v[2] * z[2] + v[3] * z[3] < 0.0 ? -1.0 : 1.0;
+        }
     }
     (void)t0;
 }
 
 // Y = v * sc in the world basis (the per-record kernels)
-template <int F = 1, class Pin = NoPin>
+template <int F = 1, class Reload, class Pin = NoPin>
 PEKF_DEV void wahba_quat_toward(const Frame &W, const Frame &V, double ka, double km, const double *z, double *v,
-                                double &sc, const Pin & = Pin()) {
-    double R[9];
+                                double &sc, const Reload &reload, const Pin & = Pin()) {
+    double R[9], nv, t0;
     wahba_rotation<true>(W, V, ka, km, R);
-    rotm_to_quat_toward(R, z, v, sc);
+    q4_times(R, z, v, nv, t0);
+    sc = rsqrt<true>(nv);
+    // rotm_to_quat_toward's fallback, taken for NaN too (a degenerate current frame: rank-1 B)
+    if (PEKF_TAKEN(!(nv >= 1.0) || t0 > 4.0 - 1e-10, false)) {
+        rotm_to_quat_flip_reference(R, z, v, sc);
+        // NaN: a degenerate current frame, solved from the re-read samples (see the reference-basis form)
+        if (!(nv == nv)) {
+            double acc[3], mag[3], a0[3], m0[3];
+            reload(acc, mag);
+            frame_pair(W, a0, m0);
+            const double kr = fabs(acc[2]);
+            wahba_current_rank1_quat<1>(a0, m0, acc, mag, kr, 1.0 - kr, v);
+            sc = v[0] * z[0] + v[1] * z[1] + v[2] * z[2] + v[3] * z[3] < 0.0 ? -1.0 : 1.0;
+        }
+    }
 }
 
 // ------------------------------- fused-step forms --------------------------------------------

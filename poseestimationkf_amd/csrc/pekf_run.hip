@@ -97,7 +97,14 @@ __global__ __launch_bounds__(kRunBlock) void k_update(int64_t batch, const doubl
     tl.to_lanes(cm, m);
     Frame Wf;
     make_frame<true>(rf, rf + 3, Wf);
-    ekf_record_step<PT>(x, state_norm2(x), P, Wf, step_consts<PT, false>(qs, rs), g, dt_ns, miss, a, m);
+    auto reload = [&](double *ra, double *rm) {  // rare: the degenerate-Wahba fallback
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            ra[i] = acc[3 * b + i];
+            rm[i] = mag[3 * b + i];
+        }
+    };
+    ekf_record_step<PT>(x, state_norm2(x), P, Wf, step_consts<PT, false>(qs, rs), g, dt_ns, miss, a, m, reload);
     if (act) prev_t[b] = t;
     if constexpr (SOA) {
         if (act) store_state<true>(Xio, Pio, b, batch, x, P);

@@ -98,6 +98,12 @@ __global__ __launch_bounds__(kSideBlock) void k_wahba_stream(int64_t batch, int6
             make_frame<true>(acc, mag, Vf, sg);
             double R[9], y[4];
             wahba_rotation<true>(Wf, Vf, ka, km, R);
+            if (frame_degenerate(Vf)) {  // a zero sample or acc parallel to mag: B has rank 1 (pekf_math.hpp)
+                const double ra[3] = {a.x, a.y, a.z}, rm[3] = {a.w, m.x, m.y};  // from the f32 record again
+                double a0[3], m0[3];
+                frame_pair(Wf, a0, m0);
+                wahba_current_rank1<1>(a0, m0, ra, rm, ka, km, R);
+            }
             rotm_to_quat_fast(R, y);  // keeps the reference's branch / sign convention
             double2 *o = reinterpret_cast<double2 *>(out + t * batch * 4) + 2 * (int64_t)lane;
             o[0] = make_double2(y[0], y[1]);

@@ -194,10 +194,13 @@ __device__ __forceinline__ StepK<PT> step_consts(double qs, double rs) {
 // that form the products (omod, pekf_math.hpp) -- the gyro is never scaled to h = w/2, and the
 // Newton steps of the rsqrt seeds need no separate multiply by 1/2: 9 VALU fewer per record, the
 // same values bit for bit.
-template <typename PT, bool MC = false, bool LAZY = false, bool OM = false, bool PIN = false, typename Ref>
+// reload(acc, mag) re-reads the record's samples for the rare degenerate-Wahba fallback
+// (wahba_quat_toward); it is not called on the common path.
+template <typename PT, bool MC = false, bool LAZY = false, bool OM = false, bool PIN = false, typename Ref,
+          typename Reload>
 __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> &P, const Ref &Wf, const StepK<PT> &k,
                                                 const double *gy, double dt_ns, bool missing,
-                                                const double *acc, const double *mag) {
+                                                const double *acc, const double *mag, const Reload &reload) {
     static_assert(!OM || (MC && std::is_same<PT, double>::value), "omod form: FP64 multi-record loop only");
     constexpr int F = OM ? 2 : 1;  // rsqrt form
     // ---- Prediction (ExtendedKalmanFilter.py:58-68) ----
@@ -257,7 +260,7 @@ __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> 
                 asm volatile("" ::"v"(Si.a00), "v"(Si.a01), "v"(Si.a02), "v"(Si.a03), "v"(Si.a11), "v"(Si.a12),
                              "v"(Si.a13), "v"(Si.a22), "v"(Si.a23), "v"(Si.a33));
         };
-        wahba_quat_toward<F>(Wf, Vf, ka, 1.0 - ka, z, v, sc, pin);  // Wahba.py:8-47 + the flip of :73-75: Y = v sc
+        wahba_quat_toward<F>(Wf, Vf, ka, 1.0 - ka, z, v, sc, reload, pin);  // Wahba.py:8-47 + the flip of :73-75: Y = v sc
         // e = Y - z (MC: D e, whose last two components are z - Y)
         const PT e0 = (PT)fma_sub(v[0], sc, z[0]), e1 = (PT)fma_sub(v[1], sc, z[1]);
         const PT e2 = (PT)(MC ? fma_rsub(v[2], sc, z[2]) : fma_sub(v[2], sc, z[2]));
@@ -392,8 +395,14 @@ __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run(int64_t batch, 
             if constexpr (LONGDT) {
                 if ((word & PEKF_DT_MASK) == PEKF_DT_ESCAPE) dtn = (dtx + base)[lane];
             }
+            auto reload = [&](double *a, double *m) {  // rare: the degenerate-Wahba fallback
+                const float4 va = (am + base)[lane];
+                const float2 vm = (my + base)[lane];
+                a[0] = va.x; a[1] = va.y; a[2] = va.z;
+                m[0] = va.w; m[1] = vm.x; m[2] = vm.y;
+            };
             ekf_record_step<PT>(x, state_norm2(x), P, Wf, step_consts<PT, false>(qs, rs), gy, dtn,
-                                (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
+                                (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag, reload);
         }
         if (TRAJ && act) {
             double2 *o = reinterpret_cast<double2 *>(traj) + 2 * (int64_t)lane;
@@ -431,6 +440,12 @@ __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run(int64_t batch, 
     const uint32_t lane = (uint32_t)b;
     const uint32_t off16 = lane * 16u, off8 = lane * 8u;
     RowCursor rows(gd, am, my, batch, window);
+    // rows the cursor runs ahead of the record a step works on (the prefetch depth)
+#if PEKF_RUN_PREFETCH > 2
+    constexpr int32_t kLag = PEKF_RUN_PREFETCH - 1;
+#else
+    constexpr int32_t kLag = 1;
+#endif
     // One record: Prediction + Correction (main_file.py:42-45) on (x, P) in registers.
     auto step = [&](const Rec &cur, int32_t t, double n2, const auto &ref, auto lazy) {
         // the multi-record loop (RefW) carries N and an unnormalised X, the one-record launch
@@ -445,8 +460,21 @@ __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run(int64_t batch, 
             if constexpr (LONGDT) {  // the escaped record's row, (step0 + t) % window (rare: off the fast path)
                 if ((word & PEKF_DT_MASK) == PEKF_DT_ESCAPE) dtn = dtx[((step0 + t) % window) * batch + b];
             }
+            auto reload = [&](double *a, double *m) {  // rare: this record again; the cursor is kLag rows ahead
+                int32_t r = rows.row - kLag;
+                while (r < 0) r += rows.window;
+                // through one-row descriptors and the lane offsets the loop holds anyway (no 64-bit
+                // lane index is kept live for this)
+                const float4 va = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                    row_rsrc(rows.a + (uint64_t)r * rows.row16, rows.row16), off16, 0, 0));
+                const float2 vm = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(
+                    row_rsrc(rows.m + (uint64_t)r * rows.row8, rows.row8), off8, 0, 0));
+                a[0] = va.x; a[1] = va.y; a[2] = va.z;
+                m[0] = va.w; m[1] = vm.x; m[2] = vm.y;
+            };
             ekf_record_step<PT, MC, decltype(lazy)::value, MC && !MIXED, PIN>(
-                x, n2, P, ref, step_consts<PT, MC>(qs, rs), gy, dtn, (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag);
+                x, n2, P, ref, step_consts<PT, MC>(qs, rs), gy, dtn, (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag,
+                reload);
         }
         if (TRAJ) {
             double xo[4] = {x[0], x[1], x[2], x[3]};
