@@ -22,13 +22,14 @@
 
 #define PEKF_DEV __device__ __forceinline__
 
-// Rarely taken fallback branches of the fused step: PEKF_TAKEN(cond, c) is cond, except in the
+// Rarely taken fallback branches of the fused step: PEKF_TAKEN(cond, c) is cond, marked unlikely (the
+// fallback bodies are placed after the loop, so the common path falls straight through), except in the
 // instruction-count build (make asm-common, -DPEKF_ISA_COMMON_PATH), where it is the constant c of
 // the path a tracked lane takes, so scripts/isa_count.py counts what actually executes.
 #ifdef PEKF_ISA_COMMON_PATH
 #define PEKF_TAKEN(cond, common) (common)
 #else
-#define PEKF_TAKEN(cond, common) (cond)
+#define PEKF_TAKEN(cond, common) __builtin_expect(!!(cond), 0)
 #endif
 
 namespace pekf {
