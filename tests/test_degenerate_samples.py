@@ -179,3 +179,36 @@ def test_wahba_side_output_through_rank1_records(eng):
             a, m = rec.acc[r, k].astype(np.float64), rec.mag[r, k].astype(np.float64)
             R, B = _ref_rotation(rec.acc0[k], rec.mag0[k], a, m, 0.5, 0.5)
             assert abs(np.trace(_quat_rotm(q[r, k]).T @ B) - np.trace(R.T @ B)) < 1e-10, (k, r)
+
+
+@pytest.mark.gpu
+def test_dropin_loop_through_rank1_records(eng, monkeypatch):
+    """main_file.py's loop through the drop-in modules (per-call kernels) over the same streams: finite,
+    equal to the reference before the first rank-1 record, back on it 30 records after."""
+    import os
+    import sys
+
+    from .conftest import ROOT
+    rec, marks = _degenerate_stream()
+    monkeypatch.syspath_prepend(os.path.join(ROOT, "poseestimationkf_amd", "dropin"))
+    for m in ("ExtendedKalmanFilter", "Wahba", "UtilityFunctions", "_bootstrap"):
+        sys.modules.pop(m, None)
+    from ExtendedKalmanFilter import KalmanFilter
+    W = rec.dtw.shape[0]
+    for k in (0, 1, 3):
+        g, d, a, m = rec.filter(k)
+        _, _, want = ekf_numpy.run_filter(g, d, a, m, rec.acc0[k], rec.mag0[k])
+        kf = KalmanFilter(0.0, rec.mag0[k], rec.acc0[k], 0.5)
+        kf.setQ(1)
+        kf.setR(0.1)
+        X, P, T, got = np.asarray([1., 0., 0., 0.]), np.identity(4), 0.0, np.empty((W, 4))
+        for i in range(W):
+            T = T + d[i]
+            z, Pm, Kk = kf.Prediction(g[i], T, X, P)
+            X, P = kf.Correction(m[i], a[i], z, Pm, Kk)
+            got[i] = X
+        err = np.abs(got - want).max(axis=1)
+        assert np.isfinite(got).all(), k
+        assert err[:marks[k][0]].max() < 1e-11 and err[marks[k][-1] + 30:].max() < 1e-9, k
+    for m in ("ExtendedKalmanFilter", "Wahba", "UtilityFunctions", "_bootstrap"):
+        sys.modules.pop(m, None)
