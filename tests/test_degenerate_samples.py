@@ -212,3 +212,25 @@ def test_dropin_loop_through_rank1_records(eng, monkeypatch):
         assert err[:marks[k][0]].max() < 1e-11 and err[marks[k][-1] + 30:].max() < 1e-9, k
     for m in ("ExtendedKalmanFilter", "Wahba", "UtilityFunctions", "_bootstrap"):
         sys.modules.pop(m, None)
+
+
+@pytest.mark.gpu
+def test_degenerate_reference_pair_in_the_fused_kernels(eng):
+    """A reference pair that does not span a plane leaves the filter's frame undefined, and with it
+    every record's Wahba attitude (the reference's are its SVD's noise-chosen rotations, record after
+    record).  The fused kernels, which run each filter in that frame, return NaN for a zero vector and
+    an unspecified unit quaternion for an exactly parallel pair; the other filters
+    of the launch are untouched."""
+    rec = synth.generate(np.arange(4), 40, seed=4)
+    rec.mag0[1] = 2.0 * rec.acc0[1]      # mag0 parallel to acc0
+    rec.mag0[2] = 0.0                    # zero mag0
+    win = eng.IMUWindow.from_records(rec)
+    f = eng.BatchedEKF(4)
+    f.run(win)
+    X = f.get_state()[0]
+    assert np.isnan(X[2]).all()
+    assert np.isfinite(X[1]).all() and abs(np.linalg.norm(X[1]) - 1) < 1e-9
+    for k in (0, 3):
+        g, d, a, m = rec.filter(k)
+        Xo = ekf_numpy.run_filter(g, d, a, m, rec.acc0[k], rec.mag0[k], record=False)[0]
+        assert np.abs(X[k] - Xo).max() < 1e-9
