@@ -350,15 +350,24 @@ PEKF_DEV bool frame_degenerate(const Frame &F) {
 
 // the rotation taking the unit vector v to the unit vector w about v x w (Rodrigues); for w = -v half a
 // turn about a normal of v (v x the coordinate axis least aligned with v)
+// a normal of the unit vector v: v x the coordinate axis least aligned with v (not normalised)
+PEKF_DEV void normal_of(const double *v, double *n) {
+    const double ax = fabs(v[0]), ay = fabs(v[1]), az = fabs(v[2]);
+    const bool j0 = ax <= ay && ax <= az, j1 = !j0 && ay <= az;
+    n[0] = j0 ? 0.0 : (j1 ? -v[2] : v[1]);
+    n[1] = j0 ? v[2] : (j1 ? 0.0 : -v[0]);
+    n[2] = j0 ? -v[1] : (j1 ? v[0] : 0.0);
+}
+
+// the rotation taking the unit vector v to the unit vector w about v x w (Rodrigues); for w = -v half a
+// turn about normal_of(v)
 template <int FAST>
 PEKF_DEV void shortest_arc(const double *v, const double *w, double *R) {
     const double c = v[0] * w[0] + v[1] * w[1] + v[2] * w[2];
     const double k[3] = {v[1] * w[2] - v[2] * w[1], v[2] * w[0] - v[0] * w[2], v[0] * w[1] - v[1] * w[0]};
     const double sk = k[0] * k[0] + k[1] * k[1] + k[2] * k[2];
-    const double ax = fabs(v[0]), ay = fabs(v[1]), az = fabs(v[2]);
-    const bool j0 = ax <= ay && ax <= az, j1 = !j0 && ay <= az;
-    const double n[3] = {j0 ? 0.0 : (j1 ? -v[2] : v[1]), j0 ? v[2] : (j1 ? 0.0 : -v[0]),
-                         j0 ? -v[1] : (j1 ? v[0] : 0.0)};
+    double n[3];
+    normal_of(v, n);
     // R = c I + [k]x + (1 - c) h h^T, k = sin(theta) h (h: k's direction, or n where k = 0)
     const bool use_k = sk > 0.0;
     const double ih = rsqrt<FAST>(use_k ? sk : n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
@@ -395,48 +404,43 @@ PEKF_DEV void wahba_rank1_rotation(const double *acc0, const double *mag0, const
 
 // The fused kernels' case: the reference pair spans a plane (it defines the filter's frame) and the
 // current one does not.  Then v is acc's direction (mag's where acc = 0), acc = alpha v, mag = beta v and
-// w = ka alpha acc0 + km beta mag0: no B, few registers.
+// w = ka alpha acc0 + km beta mag0: no B, few registers.  v, w unit (NaN where B = 0).
 template <int FAST>
-PEKF_DEV void wahba_current_rank1(const double *acc0, const double *mag0, const double *acc, const double *mag,
-                                  double ka, double km, double *R) {
+PEKF_DEV void current_rank1_directions(const double *acc0, const double *mag0, const double *acc, const double *mag,
+                                       double ka, double km, double *v, double *w) {
     const double sa = acc[0] * acc[0] + acc[1] * acc[1] + acc[2] * acc[2];
     const bool ua = sa > 0.0;
     const double u[3] = {ua ? acc[0] : mag[0], ua ? acc[1] : mag[1], ua ? acc[2] : mag[2]};
     const double iu = rsqrt<FAST>(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
-    const double v[3] = {u[0] * iu, u[1] * iu, u[2] * iu};
+    v[0] = u[0] * iu; v[1] = u[1] * iu; v[2] = u[2] * iu;
     const double al = ka * (acc[0] * v[0] + acc[1] * v[1] + acc[2] * v[2]);
     const double be = km * (mag[0] * v[0] + mag[1] * v[1] + mag[2] * v[2]);
-    double w[3] = {al * acc0[0] + be * mag0[0], al * acc0[1] + be * mag0[1], al * acc0[2] + be * mag0[2]};
-    const double iw = rsqrt<FAST>(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-    w[0] *= iw; w[1] *= iw; w[2] *= iw;
+    const double x[3] = {al * acc0[0] + be * mag0[0], al * acc0[1] + be * mag0[1], al * acc0[2] + be * mag0[2]};
+    const double ix = rsqrt<FAST>(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+    w[0] = x[0] * ix; w[1] = x[1] * ix; w[2] = x[2] * ix;
+}
+
+template <int FAST>
+PEKF_DEV void wahba_current_rank1(const double *acc0, const double *mag0, const double *acc, const double *mag,
+                                  double ka, double km, double *R) {
+    double v[3], w[3];
+    current_rank1_directions<FAST>(acc0, mag0, acc, mag, ka, km, v, w);
     shortest_arc<FAST>(v, w, R);
 }
 
 // wahba_current_rank1's rotation as its quaternion, for the fused kernels' fallback: the shortest arc
-// from v to w is q = normalise(1 + v.w, v x w) (w = -v: half a turn, (0, n)), in RotationMatrix2Quart's
-// convention (R(q) v = w), so no rotation matrix is formed.
+// from v to w is q = normalise(1 + v.w, v x w) (w = -v: half a turn, (0, normal_of(v))), in
+// RotationMatrix2Quart's convention (R(q) v = w), so no rotation matrix is formed.
 template <int FAST>
 PEKF_DEV void wahba_current_rank1_quat(const double *acc0, const double *mag0, const double *acc, const double *mag,
                                        double ka, double km, double *q) {
-    const double sa = acc[0] * acc[0] + acc[1] * acc[1] + acc[2] * acc[2];
-    const bool ua = sa > 0.0;
-    const double u[3] = {ua ? acc[0] : mag[0], ua ? acc[1] : mag[1], ua ? acc[2] : mag[2]};
-    const double iu = rsqrt<FAST>(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
-    const double v[3] = {u[0] * iu, u[1] * iu, u[2] * iu};
-    const double al = ka * (acc[0] * v[0] + acc[1] * v[1] + acc[2] * v[2]);
-    const double be = km * (mag[0] * v[0] + mag[1] * v[1] + mag[2] * v[2]);
-    const double w[3] = {al * acc0[0] + be * mag0[0], al * acc0[1] + be * mag0[1], al * acc0[2] + be * mag0[2]};
-    const double iw = rsqrt<FAST>(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-    // (1 + v.w) |w| and (v x w) |w|: the scale drops out in the normalisation
-    const double c1 = fma(v[0], w[0] * iw, fma(v[1], w[1] * iw, fma(v[2], w[2] * iw, 1.0)));
-    const double k[3] = {(v[1] * w[2] - v[2] * w[1]) * iw, (v[2] * w[0] - v[0] * w[2]) * iw,
-                         (v[0] * w[1] - v[1] * w[0]) * iw};
-    const double nq = c1 * c1 + k[0] * k[0] + k[1] * k[1] + k[2] * k[2];
-    const double ax = fabs(v[0]), ay = fabs(v[1]), az = fabs(v[2]);
-    const bool j0 = ax <= ay && ax <= az, j1 = !j0 && ay <= az;
-    const double n[3] = {j0 ? 0.0 : (j1 ? -v[2] : v[1]), j0 ? v[2] : (j1 ? 0.0 : -v[0]),
-                         j0 ? -v[1] : (j1 ? v[0] : 0.0)};
-    const bool half = !(nq > 0.0) && (iw == iw);  // w = -v exactly (NaN w, i.e. B = 0, stays NaN)
+    double v[3], w[3], n[3];
+    current_rank1_directions<FAST>(acc0, mag0, acc, mag, ka, km, v, w);
+    const double c1 = fma(v[0], w[0], fma(v[1], w[1], fma(v[2], w[2], 1.0)));
+    const double k[3] = {v[1] * w[2] - v[2] * w[1], v[2] * w[0] - v[0] * w[2], v[0] * w[1] - v[1] * w[0]};
+    normal_of(v, n);
+    // w = -v exactly (a NaN w, i.e. B = 0, stays NaN)
+    const bool half = !(c1 * c1 + k[0] * k[0] + k[1] * k[1] + k[2] * k[2] > 0.0) && (w[0] == w[0]);
     const double t[4] = {half ? 0.0 : c1, half ? n[0] : k[0], half ? n[1] : k[1], half ? n[2] : k[2]};
     const double it = rsqrt<FAST>(t[0] * t[0] + t[1] * t[1] + t[2] * t[2] + t[3] * t[3]);
     q[0] = t[0] * it; q[1] = t[1] * it; q[2] = t[2] * it; q[3] = t[3] * it;
