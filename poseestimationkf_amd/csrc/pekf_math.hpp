@@ -348,8 +348,6 @@ PEKF_DEV bool frame_degenerate(const Frame &F) {
 // the rare fallback branch, where a nested divergent branch would hold another exec mask in scalar
 // registers across the whole loop.
 
-// the rotation taking the unit vector v to the unit vector w about v x w (Rodrigues); for w = -v half a
-// turn about a normal of v (v x the coordinate axis least aligned with v)
 // a normal of the unit vector v: v x the coordinate axis least aligned with v (not normalised)
 PEKF_DEV void normal_of(const double *v, double *n) {
     const double ax = fabs(v[0]), ay = fabs(v[1]), az = fabs(v[2]);
