@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""Randomised sweep of the fused front-end + filter kernel (pekf_live_ext_dev) against the split
+pipeline it replaces (pekf_frontend_ext_dev writing records, then pekf_run_ext_dev with counts), on
+the GPU box.  The two must agree bit for bit (NaN where both are NaN): same records, same filter
+arithmetic, applied in the same order (pekf_live.hip's header).
+
+Each case draws 1-700 filters and 1-400 events per filter with per-filter type mixes (balanced,
+gyro-heavy, mag-starved, or strict gyro/acc/mag triples in random order), gaps of 0 ns (duplicate
+timestamps: the interpolation divides 0 by 0 as the C++ server does), 1-4 ms, or now and then a pause
+of 2^30 ns and more or a clock stepping back (time events, escaped record dts), filters that never got
+ready (NaN phase-2 means) and a random initial state.
+
+usage: python3 scripts/fuzz_live.py [--cases N] [--seed S]   (exit status 1 on any difference)
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from poseestimationkf_amd import engine, synth  # noqa: E402
+
+KINDS = np.array([synth.EV_ACC, synth.EV_GYRO, synth.EV_MAG], np.uint32)
+
+
+def draw_case(rng):
+    K = int(rng.integers(1, 701))
+    E = int(rng.integers(1, 401))
+    mix = str(rng.choice(["balanced", "gyro", "magless", "triples"]))
+    if mix == "triples":
+        perms = np.array([[0, 1, 2], [0, 2, 1], [1, 0, 2], [1, 2, 0], [2, 0, 1], [2, 1, 0]])
+        G = (E + 2) // 3
+        types = KINDS[perms[rng.integers(0, 6, size=(G, K))]].transpose(0, 2, 1).reshape(3 * G, K)[:E]
+    else:
+        p = {"balanced": [0.4, 0.4, 0.2], "gyro": [0.2, 0.7, 0.1], "magless": [0.5, 0.48, 0.02]}[mix]
+        types = KINDS[rng.choice(3, size=(E, K), p=p)]
+    gaps = rng.integers(1_000_000, 4_000_001, size=(E, K)).astype(np.int64)
+    gaps = np.where(rng.random((E, K)) < 0.03, 0, gaps)
+    if rng.random() < 0.4:  # pauses past the event word's 30-bit gap, and a clock stepping back
+        odd = rng.random((E, K)) < 0.01
+        gaps = np.where(odd, rng.choice([1 << 30, 3_000_000_000, -5_000_000, -2_500_000_000], size=(E, K)), gaps)
+    times = synth.T_INIT_NS + np.cumsum(gaps, axis=0)
+    vals = rng.standard_normal((E, K, 3)).astype(np.float32)
+    vals[..., 2] += np.where(types == synth.EV_ACC, 9.8, 0.0).astype(np.float32)
+    init_acc = rng.normal(size=(K, 3)) + [0.0, 0.0, 9.8]
+    init_mag = rng.normal(size=(K, 3)) * 20.0
+    init_acc[rng.random(K) < 0.05] = np.nan  # never got ready: no records, state left as it was
+    ev = dict(types=types, values=vals, times=times, init_acc=init_acc, init_mag=init_mag,
+              t_init=np.full(K, synth.T_INIT_NS, np.int64))
+    X0 = P0 = None
+    if rng.random() < 0.5:
+        X0 = rng.normal(size=(K, 4))
+        X0 /= np.linalg.norm(X0, axis=1, keepdims=True)
+        A = rng.normal(scale=0.3, size=(K, 4, 4))
+        P0 = A @ A.transpose(0, 2, 1) + 0.05 * np.eye(4)
+    return dict(ev=ev, K=K, E=E, mix=mix, X0=X0, P0=P0)
+
+
+def split(case):
+    win, counts = engine.run_frontend(case["ev"])
+    f = engine.BatchedEKF(case["K"])
+    if case["X0"] is not None:
+        f.set_state(case["X0"], case["P0"])
+    if counts.max(initial=0) > 0:
+        # at least two steps, so that the launch is the multi-record kernel k_live shares its arithmetic
+        # with (a launch of one record takes the online kernel, which runs the step in the world basis
+        # and agrees with it to rounding only); the counts keep every filter to its own records
+        f.run(win, n_steps=max(2, int(counts.max())))
+    X, P = f.get_state()
+    return X, P, counts, win.refs.download((case["K"], 6), np.float64)
+
+
+def fused(case):
+    f = engine.BatchedEKF(case["K"])
+    if case["X0"] is not None:
+        f.set_state(case["X0"], case["P0"])
+    counts, refs = f.run_events(case["ev"])
+    X, P = f.get_state()
+    return X, P, counts, refs
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cases", type=int, default=100)
+    ap.add_argument("--seed", type=int, default=1)
+    a = ap.parse_args(argv)
+    rng = np.random.default_rng(a.seed)
+    fails, records, t0 = 0, 0, time.time()
+    for i in range(a.cases):
+        if i and i % 25 == 0:
+            print("%d cases, %d differ, %d records applied, %.0f s" % (i, fails, records, time.time() - t0), flush=True)
+        case = draw_case(rng)
+        u, v = fused(case), split(case)
+        records += int(u[2].sum())
+        same = all(np.array_equal(x, y, equal_nan=True) for x, y in zip(u, v))
+        if not same:
+            fails += 1
+            names = ["%s (max |d| %.3e)" % (n, float(np.nanmax(np.abs(np.asarray(x, float) - np.asarray(y, float)))))
+                     for n, x, y in zip(("X", "P", "counts", "refs"), u, v) if not np.array_equal(x, y, equal_nan=True)]
+            print("DIFFERENT case %d: %s  K=%d E=%d mix=%s X0=%s" % (i, ", ".join(names), case["K"], case["E"],
+                                                                     case["mix"], case["X0"] is not None), flush=True)
+    print("done: %d cases, %d differ, %d records applied" % (a.cases, fails, records))
+    return 1 if fails else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

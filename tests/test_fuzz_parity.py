@@ -3,7 +3,8 @@ windows of 1-48 rows wrapped, runs cut into one-record and multi-record launches
 trajectories, AoS / SoA state, FP64 / mixed precision, the batched engine and the native handle,
 random initial states, escaped dts and missing magnetometer samples.  The sweep is seeded, so a
 failure names a reproducible case; the GPU box runs longer sweeps of the same script
-(profiles/r3/fuzz/)."""
+(profiles/r3/fuzz/).  scripts/fuzz_live.py does the same for the fused front-end + filter kernel, which
+must equal the split pipeline bit for bit."""
 from __future__ import annotations
 
 import importlib.util
@@ -15,8 +16,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _fuzz():
-    spec = importlib.util.spec_from_file_location("fuzz_gpu", os.path.join(ROOT, "scripts", "fuzz_gpu.py"))
+def _fuzz(name="fuzz_gpu"):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(ROOT, "scripts", name + ".py"))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     return mod
@@ -49,3 +50,8 @@ def test_fuzz_cases_cover_the_launch_shapes(oracle_c):
 @pytest.mark.gpu
 def test_random_launch_shapes_vs_oracle(oracle_c):
     assert _fuzz().main(["--cases", "40", "--seed", "7"]) == 0
+
+
+@pytest.mark.gpu
+def test_random_event_streams_live_equals_split():
+    assert _fuzz("fuzz_live").main(["--cases", "20", "--seed", "7"]) == 0

@@ -27,8 +27,8 @@ def _split(eng, ev, K, X0=None, P0=None):
     f = eng.BatchedEKF(K)
     if X0 is not None:
         f.set_state(X0, P0)
-    if counts.max(initial=0) > 0:
-        f.run(win, n_steps=int(counts.max()))
+    if counts.max(initial=0) > 0:  # >= 2 steps: the multi-record kernel (one record takes the online kernel)
+        f.run(win, n_steps=max(2, int(counts.max())))
     X, P = f.get_state()
     return X, P, counts, win.refs.download((K, 6), np.float64)
 
