@@ -2,7 +2,9 @@
 """Randomised sweep of the fused front-end + filter kernel (pekf_live_ext_dev) against the split
 pipeline it replaces (pekf_frontend_ext_dev writing records, then pekf_run_ext_dev with counts), on
 the GPU box.  The two must agree bit for bit (NaN where both are NaN): same records, same filter
-arithmetic, applied in the same order (pekf_live.hip's header).
+arithmetic, applied in the same order (pekf_live.hip's header).  The split pipeline's records of four
+filters per case are also checked against the front-end restatement (oracle/frontend_numpy.py): the
+same count, gyro samples and dt exactly, acc / mag within 1 f32 ulp (the kernel's reciprocal / rsqrt).
 
 Each case draws 1-700 filters and 1-400 events per filter with per-filter type mixes (balanced,
 gyro-heavy, mag-starved, or strict gyro/acc/mag triples in random order), gaps of 0 ns (duplicate
@@ -24,6 +26,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+from oracle import frontend_numpy  # noqa: E402  (the checker)
 from poseestimationkf_amd import engine, synth  # noqa: E402
 
 KINDS = np.array([synth.EV_ACC, synth.EV_GYRO, synth.EV_MAG], np.uint32)
@@ -62,8 +65,45 @@ def draw_case(rng):
     return dict(ev=ev, K=K, E=E, mix=mix, X0=X0, P0=P0)
 
 
-def split(case):
+def _ulps(a, b):
+    """f32 ulps between a and b; NaN only where both are NaN (else a large number)."""
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    na, nb = np.isnan(a), np.isnan(b)
+    if (na != nb).any():
+        return 1 << 30
+    ia = a[~na].view(np.int32).astype(np.int64)
+    ib = b[~nb].view(np.int32).astype(np.int64)
+    return int(np.abs(ia - ib).max(initial=0))
+
+
+def check_records(case, win, counts, cols):
+    """Problems (strings) of the records of filters cols against the front-end restatement."""
+    ev, out = case["ev"], []
+    rec = win.download_filters(cols)
+    for j, k in enumerate(cols):
+        if not np.isfinite(ev["init_acc"][k]).all():
+            continue  # never ready: the kernels emit nothing, the restatement knows no phase 2
+        g, dt, a, m = frontend_numpy.run_frontend(ev["types"][:, k], ev["values"][:, k].astype(np.float64),
+                                                  ev["times"][:, k], ev["init_acc"][k], ev["init_mag"][k],
+                                                  ev["t_init"][k])
+        r = len(dt)
+        if counts[k] != r:
+            out.append("filter %d: %d records, restatement %d" % (k, counts[k], r))
+            continue
+        if not np.array_equal(rec.gyro[:r, j], g.astype(np.float32)):
+            out.append("filter %d: gyro" % k)
+        if not np.array_equal(rec.dt_ns[:r, j], dt.astype(np.float64)):
+            out.append("filter %d: dt" % k)
+        u = max(_ulps(rec.acc[:r, j], a), _ulps(rec.mag[:r, j], m))
+        if u > 1:
+            out.append("filter %d: acc / mag %d ulps" % (k, u))
+    return out
+
+
+def split(case, cols=None):
     win, counts = engine.run_frontend(case["ev"])
+    if cols is not None:
+        case["record_problems"] = check_records(case, win, counts, cols)
     f = engine.BatchedEKF(case["K"])
     if case["X0"] is not None:
         f.set_state(case["X0"], case["P0"])
@@ -96,7 +136,12 @@ def main(argv=None):
         if i and i % 25 == 0:
             print("%d cases, %d differ, %d records applied, %.0f s" % (i, fails, records, time.time() - t0), flush=True)
         case = draw_case(rng)
-        u, v = fused(case), split(case)
+        cols = rng.choice(case["K"], size=min(4, case["K"]), replace=False)
+        u, v = fused(case), split(case, cols)
+        if case["record_problems"]:
+            fails += 1
+            print("RECORDS case %d: %s  K=%d E=%d mix=%s" % (i, "; ".join(case["record_problems"][:4]), case["K"],
+                                                            case["E"], case["mix"]), flush=True)
         records += int(u[2].sum())
         same = all(np.array_equal(x, y, equal_nan=True) for x, y in zip(u, v))
         if not same:

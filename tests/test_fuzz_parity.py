@@ -4,7 +4,8 @@ trajectories, AoS / SoA state, FP64 / mixed precision, the batched engine and th
 random initial states, escaped dts and missing magnetometer samples.  The sweep is seeded, so a
 failure names a reproducible case; the GPU box runs longer sweeps of the same script
 (profiles/r3/fuzz/).  scripts/fuzz_live.py does the same for the fused front-end + filter kernel, which
-must equal the split pipeline bit for bit."""
+must equal the split pipeline bit for bit (and its records the front-end restatement's), and
+scripts/fuzz_percall.py the per-call operators item by item against the NumPy restatement."""
 from __future__ import annotations
 
 import importlib.util
@@ -55,3 +56,8 @@ def test_random_launch_shapes_vs_oracle(oracle_c):
 @pytest.mark.gpu
 def test_random_event_streams_live_equals_split():
     assert _fuzz("fuzz_live").main(["--cases", "20", "--seed", "7"]) == 0
+
+
+@pytest.mark.gpu
+def test_random_percall_items_vs_numpy_restatement(oracle_c):
+    assert _fuzz("fuzz_percall").main(["--cases", "3", "--seed", "7"]) == 0
