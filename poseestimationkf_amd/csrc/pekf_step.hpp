@@ -17,7 +17,7 @@ constexpr int kRunBlock = 256;
 
 // Cache policy of the record loads: nt (aux = 2), as each record is read once per launch.
 // Same box, config 3: 136.8 / 137.7 ms against 137.8 / 138.8 with the default policy
-// (profiles/r1/ab_nt_loads/); sc0 nt 137.0 / 137.9.
+// (profiles/r1/ab_nt_loads/); sc0 nt 137.0 / 137.9; nt sc1 and sc0 nt sc1 +0.2 % (profiles/r3/ab_rec_cache_policy/).
 #ifndef PEKF_REC_AUX
 #define PEKF_REC_AUX 2
 #endif
