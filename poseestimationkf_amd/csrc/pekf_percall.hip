@@ -429,8 +429,130 @@ __device__ __noinline__ void svc_run(uint32_t op, double *sh, int32_t *sh_status
     *sh_status = st;
 }
 
+// Prediction and Correction spread over the service wave's lanes.  On lane 0 alone a predict is ~620
+// serial FP64 instructions (~0.9 us of a 5.2 us call, scripts/percall_latency.cpp against the bare
+// round trip of scripts/pingpong_probe.hip), most of them the 4x4 products.  Here lane l < 16 forms
+// entry (l / 4, l % 4) of each product with the source expression matmul<> uses for that entry (a
+// dot product from s = 0.0, the same contraction), so every entry rounds as on lane 0: the answers
+// stay bit-identical to the launch per call and to the batched kernels (tests/test_percall_service.py).
+// The parts with no product structure -- RK4, the cofactor inverse, the Wahba solve -- run on every
+// lane at once, which costs what they cost on one.  sx: LDS scratch shared through the wave.
+constexpr int kSvcScratch = 112;
+
+// v[lane] for lanes 0..3 without indexing registers by a lane-varying value
+__device__ __forceinline__ double pick4(const double *v, int lane) {
+    return lane == 0 ? v[0] : lane == 1 ? v[1] : lane == 2 ? v[2] : v[3];
+}
+
+__device__ __forceinline__ double dot_row_col(const double *a, int as, const double *b, int bs, int n) {
+    double s = 0.0;
+    for (int t = 0; t < n; ++t) s += a[t * as] * b[t * bs];  // matmul<>'s entry: s += a * b from 0.0
+    return s;
+}
+
+// payload index of operand word k (8 lines of 7 doubles; sh[line * 8 + j])
+__device__ __forceinline__ constexpr int svc_at(int k) { return (k / kSvcLinePayload) * 8 + k % kSvcLinePayload; }
+
+__device__ __noinline__ void svc_predict_wave(double *sh, double *sx, int32_t *sh_status) {
+    const int lane = threadIdx.x, l = lane & 15, i = l >> 2, j = l & 3;
+    // operands (d_predict's order: gyro 3, dt 1, X 4, P 16, Q 9, R 16)
+    double g[3], dt, x[4];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) g[k] = sh[svc_at(k)];
+    dt = sh[svc_at(3)];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = sh[svc_at(4 + k)];
+    double *A = sx, *Jb = sx + 16, *P = sx + 28, *Q = sx + 44, *T = sx + 53, *T12 = sx + 69, *Si = sx + 81;
+    if (lane < 16) P[l] = sh[svc_at(8 + l)];
+    if (lane < 9) Q[lane] = sh[svc_at(24 + lane)];
+    const double R = sh[svc_at(33 + l)];
+    if (lane == 0) {
+        double a[16], jb[12];
+        omega_half(g, a);
+        xi_half(x, jb);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) A[k] = a[k];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) Jb[k] = jb[k];
+    }
+    __syncthreads();
+    // d_predict_cov: t16 = A P, t12 = Jb Q (lanes 16..27), then P- = t16 A^T + t12 Jb^T
+    if (lane < 16) T[l] = dot_row_col(A + 4 * i, 1, P + j, 4, 4);
+    if (lane >= 16 && lane < 28) {
+        const int r = (lane - 16) / 3, c = (lane - 16) % 3;
+        T12[lane - 16] = dot_row_col(Jb + 3 * r, 1, Q + c, 3, 3);
+    }
+    __syncthreads();
+    const double a16 = dot_row_col(T + 4 * i, 1, A + 4 * j, 1, 4);     // (A P) A^T: At[t][j] = A[j][t]
+    const double b16 = dot_row_col(T12 + 3 * i, 1, Jb + 3 * j, 1, 3);  // (Jb Q) Jb^T
+    const double pm = a16 + b16;
+    // d_predict_gain: S = P- + R, z = RK4, K = P- inv(S)
+    const double s = pm + R;
+    __syncthreads();
+    if (lane < 16) {
+        T[l] = s;
+        P[l] = pm;  // P is no longer needed: it holds P- from here
+    }
+    __syncthreads();
+    double S[16], inv[16], z[4];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) S[k] = T[k];
+    rk4_literal(x, dt, g, z);
+    const bool ok = inverse4(S, inv);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) Si[k] = inv[k];
+    }
+    __syncthreads();
+    const double kk = ok ? dot_row_col(P + 4 * i, 1, Si + j, 4, 4) : NAN;
+    __syncthreads();
+    // outputs in the order of call1_outputs: z 4, Pm 16, K 16
+    if (lane < 4) sh[lane] = pick4(z, lane);
+    if (lane < 16) {
+        sh[4 + l] = pm;
+        sh[20 + l] = kk;
+    }
+    if (lane == 0) *sh_status = ok ? 0 : 1;
+}
+
+__device__ __noinline__ void svc_correct_wave(double *sh, double *sx, int32_t *sh_status) {
+    const int lane = threadIdx.x, l = lane & 15, i = l >> 2, j = l & 3;
+    // operands (d_correct's order: mag 3, acc 3, z 4, P 16, K 16, acc0 3, mag0 3)
+    double mag[3], acc[3], z[4], a0[3], m0[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        mag[k] = sh[svc_at(k)];
+        acc[k] = sh[svc_at(3 + k)];
+        a0[k] = sh[svc_at(42 + k)];
+        m0[k] = sh[svc_at(45 + k)];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) z[k] = sh[svc_at(6 + k)];
+    double *P = sx, *K = sx + 16;
+    if (lane < 16) {
+        P[l] = sh[svc_at(10 + l)];
+        K[l] = sh[svc_at(26 + l)];
+    }
+    __syncthreads();
+    // d_correct_cov: P - K P, one entry per lane
+    const double pout = P[l] - dot_row_col(K + 4 * i, 1, P + j, 4, 4);
+    // d_correct_measure + d_correct_state on every lane (the same values on each)
+    double y[4], kr[16], X[4];
+    int32_t st = 0;
+    d_correct_measure(mag, acc, z, a0, m0, y, &st);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) kr[k] = K[k];
+    d_correct_state(y, z, kr, X);
+    __syncthreads();
+    // outputs: X 4, P 16
+    if (lane < 4) sh[lane] = pick4(X, lane);
+    if (lane < 16) sh[4 + l] = pout;
+    if (lane == 0) *sh_status = st;
+}
+
 __global__ __launch_bounds__(64) void k_service(char *box, unsigned long long idle_ticks) {
     __shared__ double sh[64];
+    __shared__ double sx[kSvcScratch];
     __shared__ int32_t sh_status;
     const int lane = threadIdx.x;
     const uint64_t *req = reinterpret_cast<const uint64_t *>(box);
@@ -466,7 +588,12 @@ __global__ __launch_bounds__(64) void k_service(char *box, unsigned long long id
         sh[lane] = __longlong_as_double((long long)w);
         __syncthreads();
         const int n_out = call1_outputs((int)op);
-        if (lane == 0) svc_run(op, sh, &sh_status);
+        if (op == kCallPredict)
+            svc_predict_wave(sh, sx, &sh_status);  // op is wave-uniform: every lane takes part
+        else if (op == kCallCorrect)
+            svc_correct_wave(sh, sx, &sh_status);
+        else if (lane == 0)
+            svc_run(op, sh, &sh_status);
         __syncthreads();
         if (lane < n_out) __hip_atomic_store(resp + lane, sh[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (lane == 0) __hip_atomic_store(resp_status, sh_status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -3,7 +3,10 @@
 The drop-in modules make one call per record (main_file.py:38-45).  By default those calls are
 answered by a resident one-wave kernel polling pinned host memory (csrc/pekf_percall.hip,
 `Service`); PEKF_PERCALL_LAUNCH launches k_call1 per call.  Both run the same device functions,
-so results must agree bit for bit with each other and with the batched kernels' rows.
+so results must agree bit for bit with each other and with the batched kernels' rows.  The service
+spreads Prediction's products and Correction's P - K P over its wave's lanes, one entry per lane with
+the expression the serial body uses (csrc/pekf_percall.hip, svc_predict_wave / svc_correct_wave), so
+a randomised sweep over general operands checks that bit-identity too.
 """
 from __future__ import annotations
 
@@ -141,3 +144,53 @@ def test_service_from_several_threads(eng, kat):
     assert not errors, errors
     for t in range(4):
         _same(ref[t::4], results[t])
+
+
+def _rand_operands(rng):
+    """One predict + correct operand set: general (non-symmetric) P, K; Q, R scalar or full; samples of
+    any magnitude; now and then a NaN, an inf or an exactly singular S (the reference raises)."""
+    g = rng.normal(0, 2, 3)
+    dt = float(rng.choice([rng.uniform(0, 2e9), rng.integers(0, 2**31), 0.0]))
+    X = rng.normal(0, 1, 4)
+    P = rng.normal(0, 1, (4, 4)) if rng.random() < 0.5 else np.eye(4) * rng.uniform(0.1, 3)
+    Q = np.eye(3) * rng.uniform(0.1, 2) if rng.random() < 0.5 else rng.normal(0, 1, (3, 3))
+    R = np.eye(4) * rng.uniform(0.01, 1) if rng.random() < 0.7 else rng.normal(0, 1, (4, 4))
+    mag, acc = rng.normal(0, 1, 3) * rng.uniform(0.1, 10), rng.normal(0, 1, 3) * rng.uniform(0.1, 10)
+    z, Pm, K = rng.normal(0, 1, 4), rng.normal(0, 1, (4, 4)), rng.normal(0, 1, (4, 4))
+    a0, m0 = rng.normal(0, 1, 3), rng.normal(0, 1, 3)
+    u = rng.random()
+    if u < 0.03:
+        P[rng.integers(4), rng.integers(4)] = np.nan
+    elif u < 0.06:
+        K[rng.integers(4), rng.integers(4)] = np.inf
+    elif u < 0.09:  # S = P- + R singular: zero rates and covariances
+        g, P, Q, R = np.zeros(3), np.zeros((4, 4)), np.zeros((3, 3)), np.zeros((4, 4))
+    return (g, dt, X, P, Q, R), (mag, acc, z, Pm, K, a0, m0)
+
+
+def _call(fn, *args):
+    try:
+        return tuple(np.array(r, copy=True) for r in fn(*args))
+    except np.linalg.LinAlgError as e:
+        return ("LinAlgError", str(e))
+
+
+@pytest.mark.gpu
+def test_service_wave_spread_bit_identical_to_launch_on_random_operands(eng):
+    rng = np.random.default_rng(20261017)
+    cases = [_rand_operands(rng) for _ in range(300)]
+    got = {}
+    for mode in (eng.PERCALL_SERVICE, eng.PERCALL_LAUNCH):
+        eng.percall_mode(mode)
+        got[mode] = [(_call(eng.predict, *p), _call(eng.correct, *c)) for p, c in cases]
+    raised = 0
+    for a, b in zip(got[eng.PERCALL_SERVICE], got[eng.PERCALL_LAUNCH]):
+        for x, y in zip(a, b):
+            if isinstance(x[0], str):
+                raised += 1
+                assert x == y
+                continue
+            assert len(x) == len(y)
+            for u, v in zip(x, y):
+                assert np.array_equal(u, v, equal_nan=True)
+    assert raised > 0  # the singular and non-finite cases were exercised
