@@ -498,8 +498,8 @@ __device__ __noinline__ void svc_predict_wave(double *sh, double *sx, int32_t *s
 #pragma unroll
     for (int k = 0; k < 16; ++k) S[k] = T[k];
     rk4_literal(x, dt, g, z);
-    const bool ok = inverse4(S, inv);
-    if (lane == 0) {
+    const bool ok = inverse4(S, inv);  // inv is written only when ok
+    if (lane == 0 && ok) {
 #pragma unroll
         for (int k = 0; k < 16; ++k) Si[k] = inv[k];
     }
