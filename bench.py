@@ -21,7 +21,10 @@ Prints ONE JSON line on rank 0.  `value` = filter-steps/s over all GPUs (the slo
 clock, gather included).  `roofline` is the fused kernel's achieved algorithmic HBM read rate per
 GPU (40 B x filters x records / kernel time, HIP events on the launch stream) against the 8 TB/s
 peak; `valu_roofline` is the resource that binds it, FP64 VALU issue; `cpu_baseline` times the
-NumPy restatement of the reference loop on the host cores (rank 0, N = 1 only, bounded sample).
+NumPy restatement of the reference loop on the job's host cores (rank 0, at every N, a bounded
+sample, before any GPU work; the core count comes from the cgroup's CPU quota / cpuset);
+`kernel_ms_per_gpu` / `gather_ms_per_gpu` attribute each GPU's share of the step.
+A rank that never joins or dies mid-run fails the job within PEKF_COMM_TIMEOUT_S (status 2).
 """
 from __future__ import annotations
 
@@ -135,19 +138,119 @@ def _cpu_worker(args):
     return len(ids) * n_rec, time.perf_counter() - t0
 
 
-def cpu_share(environ=os.environ):
-    """(processes to use, cores visible): the host cores this job may use.  On the GPU box the job's
-    CPU share is given by OMP_NUM_THREADS (16 per GPU) while sched_getaffinity shows the whole
-    machine; elsewhere all visible cores."""
-    cores = len(os.sched_getaffinity(0))
-    cap = environ.get("OMP_NUM_THREADS")
-    use = min(cores, int(cap)) if cap and cap.isdigit() and int(cap) > 0 else cores
-    return max(1, use), cores
+def _cpulist_count(text):
+    """Number of CPUs in a cpuset list such as "0-3,8,10-11" (0 for an empty list)."""
+    n = 0
+    for part in text.strip().split(","):
+        part = part.strip()
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        n += (int(hi) - int(lo) + 1) if hi else 1
+    return n
+
+
+def _read(path):
+    try:
+        with open(path) as fh:
+            return fh.read().strip()
+    except OSError:
+        return None
+
+
+def cgroup_cpu_limits(proc_cgroup="/proc/self/cgroup", root="/sys/fs/cgroup"):
+    """The CPU limits of this process's cgroup (v2 unified, or v1 cpu + cpuset controllers).
+
+    Every existing level from the process's own cgroup directory up to the mount root is read (a
+    cgroup namespace may hide the leaf, as on the GPU box): the quota is the smallest
+    quota / period on the path (v2 cpu.max "Q P" or "max P"; v1 cpu.cfs_quota_us / cpu.cfs_period_us,
+    -1 = none), the cpuset the deepest level's effective list.  Returns dict(quota_cores, quota_at,
+    cpuset_cores, cpuset_at, version); a limit that is not found is None."""
+    out = dict(quota_cores=None, quota_at=None, cpuset_cores=None, cpuset_at=None, version=None)
+    text = _read(proc_cgroup)
+    if text is None:
+        return out
+    paths = {}
+    for line in text.splitlines():
+        parts = line.split(":", 2)
+        if len(parts) == 3:
+            for ctl in (parts[1].split(",") if parts[1] else [""]):
+                paths[ctl] = parts[2]
+
+    def levels(base, rel):
+        rel = rel.strip("/")
+        segs = rel.split("/") if rel else []
+        for i in range(len(segs), -1, -1):
+            d = os.path.join(base, *segs[:i]) if i else base
+            if os.path.isdir(d):
+                yield d
+
+    def take_quota(q, where):
+        if q is not None and (out["quota_cores"] is None or q < out["quota_cores"]):
+            out["quota_cores"], out["quota_at"] = q, where
+
+    if "" in paths and os.path.exists(os.path.join(root, "cgroup.controllers")):   # v2
+        out["version"] = 2
+        for d in levels(root, paths[""]):
+            v = _read(os.path.join(d, "cpu.max"))
+            if v:
+                f = v.split()
+                if f[0] != "max" and len(f) == 2 and float(f[1]) > 0:
+                    take_quota(max(1, int(float(f[0]) // float(f[1]))), os.path.join(d, "cpu.max"))
+            c = _read(os.path.join(d, "cpuset.cpus.effective"))
+            if c and out["cpuset_cores"] is None:
+                out["cpuset_cores"], out["cpuset_at"] = _cpulist_count(c), os.path.join(d, "cpuset.cpus.effective")
+        return out
+    for ctl, rel in paths.items():                                                   # v1
+        names = ctl.split(",")
+        if "cpu" in names:
+            out["version"] = 1
+            for mount in ("cpu,cpuacct", "cpu", "cpuacct,cpu"):
+                base = os.path.join(root, mount)
+                if not os.path.isdir(base):
+                    continue
+                for d in levels(base, rel):
+                    q, per = _read(os.path.join(d, "cpu.cfs_quota_us")), _read(os.path.join(d, "cpu.cfs_period_us"))
+                    if q and per and int(q) > 0 and int(per) > 0:
+                        take_quota(max(1, int(q) // int(per)), os.path.join(d, "cpu.cfs_quota_us"))
+                break
+        if "cpuset" in names:
+            out["version"] = 1
+            base = os.path.join(root, "cpuset")
+            for d in levels(base, rel):
+                c = _read(os.path.join(d, "cpuset.effective_cpus")) or _read(os.path.join(d, "cpuset.cpus"))
+                if c:
+                    out["cpuset_cores"], out["cpuset_at"] = _cpulist_count(c), d
+                    break
+    return out
+
+
+def cpu_share(environ=os.environ, proc_cgroup="/proc/self/cgroup", cgroup_root="/sys/fs/cgroup", affinity=None):
+    """The host cores this job may use: min(affinity, cgroup CPU quota, cgroup cpuset).  On the GPU box
+    sched_getaffinity shows the whole machine (256) while the cgroup's cpu.max gives the job its share
+    (16 per GPU).  Only when no cgroup limit exists is OMP_NUM_THREADS taken as the declared share
+    (a launcher's per-job setting), and only when nothing at all limits the job, every affinity core.
+    Returns dict(use, affinity, quota_cores, cpuset_cores, omp_num_threads, share_source)."""
+    aff = len(os.sched_getaffinity(0)) if affinity is None else int(affinity)
+    lim = cgroup_cpu_limits(proc_cgroup, cgroup_root)
+    cands = [(aff, "sched_getaffinity")]
+    if lim["quota_cores"] is not None:
+        cands.append((lim["quota_cores"], "cgroup v%d CPU quota (%s)" % (lim["version"], lim["quota_at"])))
+    if lim["cpuset_cores"] is not None:
+        cands.append((lim["cpuset_cores"], "cgroup v%d cpuset (%s)" % (lim["version"], lim["cpuset_at"])))
+    use, source = min(cands, key=lambda c: c[0])
+    omp = environ.get("OMP_NUM_THREADS")
+    omp = int(omp) if omp and omp.isdigit() and int(omp) > 0 else None
+    if use == aff and lim["quota_cores"] is None and omp is not None and omp < aff:
+        use, source = omp, "OMP_NUM_THREADS (no cgroup CPU quota found)"
+    return dict(use=max(1, use), affinity=aff, quota_cores=lim["quota_cores"], cpuset_cores=lim["cpuset_cores"],
+                omp_num_threads=omp, share_source=source)
 
 
 def cpu_baseline(seed, missing, filters_per_core=160, n_rec=1500):
     import multiprocessing as mp
-    workers, cores = cpu_share()
+    share = cpu_share()
+    workers, cores = share["use"], share["affinity"]
     ctx = mp.get_context("fork")
     mgr = ctx.Manager()
     barrier = mgr.Barrier(workers)
@@ -155,14 +258,16 @@ def cpu_baseline(seed, missing, filters_per_core=160, n_rec=1500):
             for w in range(workers)]
     with ctx.Pool(workers) as pool:
         res = pool.map(_cpu_worker, jobs)
+    mgr.shutdown()
     steps = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
     return {"value": steps / wall, "unit": "EKF steps/s", "cores": workers, "kind": "port",
-            "per_core": steps / wall / workers, "cores_visible": cores,
+            "per_core": steps / wall / workers, "cores_visible": cores, "share_source": share["share_source"],
+            "cgroup_quota_cores": share["quota_cores"], "cgroup_cpuset_cores": share["cpuset_cores"],
             "sample": "NumPy restatement of main_file.py's per-record loop (oracle/ekf_numpy.py, bit-identical "
-                      "to the reference), %d processes (one per core of this job's CPU share, OMP_NUM_THREADS; "
-                      "%d cores visible on the host) x %d filters x %d records of the same synthetic stream"
-                      % (workers, cores, filters_per_core, n_rec),
+                      "to the reference), %d processes (one per core of this job's CPU share: %s; %d cores in "
+                      "the affinity mask) x %d filters x %d records of the same synthetic stream"
+                      % (workers, share["share_source"], cores, filters_per_core, n_rec),
             "seconds": wall}
 
 
@@ -175,7 +280,7 @@ def c_oracle_rate(seed, missing, n_filters=64, n_rec=1000):
     t0 = time.perf_counter()
     oracle_c.run(rec)
     dt = time.perf_counter() - t0
-    return {"value": n_filters * n_rec / dt, "threads": cpu_share()[0],
+    return {"value": n_filters * n_rec / dt, "threads": cpu_share()["use"],
             "what": "C FP64 restatement (oracle/ekf_oracle.c, Jacobi SVD), OpenMP over filters"}
 
 
@@ -184,7 +289,7 @@ class RankRun:
     """One process = one GPU (modes "single" and "ranks"): this rank's shard as an IMUWindow +
     BatchedEKF on device `dev`; with a communicator, each step ends with the RCCL gather to rank 0."""
 
-    def __init__(self, args, plan):
+    def __init__(self, args, plan, rdzv=None):
         import numpy as np
 
         from poseestimationkf_amd import engine, shard
@@ -197,7 +302,7 @@ class RankRun:
         self.stream = self.own_stream.handle
         self.comm = None
         if self.world > 1 or args.dist:
-            self.comm = shard.connect(self.rank, self.world)
+            self.comm = shard.connect(self.rank, self.world, rdzv)
             log("rank %d/%d: RCCL %d communicator on device %d" % (self.rank, self.world, shard.rccl_version(),
                                                                   self.comm.device))
         log("rank %d/%d: synthesizing filters [%d, %d) x %d records (%.1f GB resident)" %
@@ -211,28 +316,46 @@ class RankRun:
         self.ev = []
 
     def prepare(self, n_steps):
-        self.ev = [(self.engine.Event(), self.engine.Event()) for _ in range(n_steps)]
+        """ev[k] = (kernel start, kernel end, gather end) HIP events of step k on this rank's stream."""
+        self.ev = [tuple(self.engine.Event() for _ in range(3)) for _ in range(n_steps)]
 
     def sync(self):
-        self.engine.check(self.engine.lib.pekf_stream_sync(self.stream))
+        if self.comm is not None:  # drains the stream's collectives too, against PEKF_COMM_TIMEOUT_S
+            self.comm.wait(self.stream)
+        else:
+            self.engine.check(self.engine.lib.pekf_stream_sync(self.stream))
 
     def barrier(self):
         if self.comm is not None:
             self.comm.barrier(self.stream)
 
     def step(self, k, n_rec, row0):
-        e0, e1 = self.ev[k]
+        e0, e1, e2 = self.ev[k]
         e0.record(self.stream)
         self.filt.run_async(self.win, n_rec, row0, self.stream)
         e1.record(self.stream)
         if self.comm is not None:  # ONE RCCL gather of the final quaternions to rank 0 (pekf_gather_dev)
             self.shard.gather_quaternions(self.comm, self.filt.X.ptr, self.B, self.recv, 0, self.stream)
+        e2.record(self.stream)
 
     def kernel_ms(self, k):
         return self.ev[k][0].elapsed_ms(self.ev[k][1])
 
+    def gather_ms(self, k):
+        return self.ev[k][1].elapsed_ms(self.ev[k][2])
+
     def slowest(self, elapsed):
         return self.comm.max_over_ranks(elapsed, self.stream) if self.comm is not None else elapsed
+
+    def per_gpu(self, steps):
+        """(kernel ms, gather ms) per GPU in rank order, each the mean over `steps`: every rank's own
+        HIP-event times, exchanged with one RCCL all-reduce (collective: all ranks call it)."""
+        mine = [float(self.np.mean([self.kernel_ms(k) for k in steps])),
+                float(self.np.mean([self.gather_ms(k) for k in steps]))]
+        if self.comm is None:
+            return [mine[0]], [mine[1]]
+        allv = self.comm.all_values(mine, self.stream)
+        return [float(v) for v in allv[:, 0]], [float(v) for v in allv[:, 1]]
 
     def final_rows(self):
         """(global first filter id, X rows) available on this rank: every filter's final X on rank 0
@@ -269,14 +392,14 @@ class MultiRun:
         self.ev = []
 
     def prepare(self, n_steps):
-        """HIP events are per device: ev[k][i] = (start, end) of step k on device i."""
+        """HIP events are per device: ev[k][i] = (kernel start, kernel end, gather end) of step k on device i."""
         self.ev = []
         for _ in range(n_steps):
-            pairs = []
+            trip = []
             for d in self.devices:
                 self.engine.set_device(d)
-                pairs.append((self.engine.Event(), self.engine.Event()))
-            self.ev.append(pairs)
+                trip.append(tuple(self.engine.Event() for _ in range(3)))
+            self.ev.append(trip)
         self.engine.set_device(self.devices[0])
 
     def sync(self):
@@ -288,21 +411,34 @@ class MultiRun:
     def step(self, k, n_rec, row0):
         for i, d in enumerate(self.devices):
             self.engine.set_device(d)
-            e0, e1 = self.ev[k][i]
+            e0, e1, _ = self.ev[k][i]
             s = self.m.streams[i].handle
             e0.record(s)
             self.m.filts[i].run_async(self.m.wins[i], n_rec, row0, s)
             e1.record(s)
         self.engine.set_device(self.devices[0])
         self.m.gather_async()
+        for i, d in enumerate(self.devices):
+            self.engine.set_device(d)
+            self.ev[k][i][2].record(self.m.streams[i].handle)
+        self.engine.set_device(self.devices[0])
 
     def kernel_ms(self, k, device_index=None):
         """The slowest device's kernel time of step k (or one device's)."""
-        t = [e0.elapsed_ms(e1) for e0, e1 in self.ev[k]]
+        t = [e[0].elapsed_ms(e[1]) for e in self.ev[k]]
+        return max(t) if device_index is None else t[device_index]
+
+    def gather_ms(self, k, device_index=None):
+        t = [e[1].elapsed_ms(e[2]) for e in self.ev[k]]
         return max(t) if device_index is None else t[device_index]
 
     def slowest(self, elapsed):
         return elapsed
+
+    def per_gpu(self, steps):
+        n = len(self.devices)
+        mean = lambda f: [sum(f(k, i) for k in steps) / len(steps) for i in range(n)]  # noqa: E731
+        return mean(self.kernel_ms), mean(self.gather_ms)
 
     def final_rows(self):
         return 0, self.m.gathered()
@@ -332,7 +468,7 @@ def parity_check(first, rows, n_samples, n_records, args):
 
 
 # ----------------------------------------------------------------------------------- main
-def main(argv=None):
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -343,6 +479,9 @@ def main(argv=None):
     ap.add_argument("--missing", action="store_true", help="config 5: 30%% magnetometer-missing records")
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--cpu-baseline", choices=["port", "none"], default="port")
+    ap.add_argument("--cpu-filters-per-core", type=int, default=160,
+                    help="CPU baseline sample: filters per host process")
+    ap.add_argument("--cpu-records", type=int, default=1500, help="CPU baseline sample: records per filter")
     ap.add_argument("--parity-samples", type=int, default=16,
                     help="filters re-run by the C oracle (at least 4 per GPU when N > 1)")
     ap.add_argument("--precision", choices=["f64", "mixed"], default="f64",
@@ -353,32 +492,66 @@ def main(argv=None):
                     help="rehearse rank R's shard of a W-way job on one GPU (e.g. 7/8 at config 4)")
     ap.add_argument("--one-process", action="store_true",
                     help="drive the GPUs from one process (MultiDeviceEKF) even for --gpus 1")
-    args = ap.parse_args(argv)
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    """Runs the benchmark; a failed collective (a rank missing at communicator creation, a peer gone
+    mid-run: libpekf's PEKF_COMM_TIMEOUT_S deadlines) ends it with status 2, a message on stderr and
+    nothing on stdout."""
+    from poseestimationkf_amd import _lib
+    try:
+        return _main(argv)
+    except (_lib.CommTimeoutError, _lib.PekfError) as e:
+        if isinstance(e, _lib.CommTimeoutError) or e.status == _lib.PEKF_ERR_COMM:
+            raise BenchError("collective failed: %s" % e)
+        raise
+    except TimeoutError as e:   # FileRendezvous: no RCCL id from rank 0 within PEKF_RDZV_TIMEOUT_S
+        raise BenchError(str(e))
+    except RuntimeError as e:   # FileRendezvous: rank 0 failed before it had an id
+        from poseestimationkf_amd import shard
+        if isinstance(e, shard.RendezvousError):
+            raise BenchError(str(e))
+        raise
+
+
+def _main(argv=None):
+    args = parse_args(argv)
     plan = launch_plan(args.gpus, os.environ, args.shard_of, args.one_process)
     rank, world = plan["rank"], plan["world"]
     out_fd = StdoutForTheResult()
+    rdzv = None
+    if plan["mode"] == "ranks" and (world > 1 or args.dist):
+        from poseestimationkf_amd import shard
+        rdzv = shard.FileRendezvous(rank, world)
 
-    # CPU baseline first, in forked workers, before anything touches the GPU.
-    cpu = None
-    if args.cpu_baseline == "port" and rank == 0 and world == 1:
-        log("cpu baseline (NumPy restatement) ...")
-        cpu = cpu_baseline(args.seed, args.missing)
-        try:
-            cpu["c_oracle"] = c_oracle_rate(args.seed, args.missing)
-        except Exception as e:  # the C oracle is optional for the baseline line
-            cpu["c_oracle"] = {"error": str(e)}
-        log("cpu baseline: %.0f steps/s on %d cores" % (cpu["value"], cpu["cores"]))
+    try:
+        # CPU baseline first (rank 0, every N), in forked workers, before anything touches the GPU;
+        # the other ranks wait for rank 0's RCCL id meanwhile.
+        cpu = None
+        if args.cpu_baseline == "port" and rank == 0:
+            log("cpu baseline (NumPy restatement) ...")
+            cpu = cpu_baseline(args.seed, args.missing, args.cpu_filters_per_core, args.cpu_records)
+            try:
+                cpu["c_oracle"] = c_oracle_rate(args.seed, args.missing)
+            except Exception as e:  # the C oracle is optional for the baseline line
+                cpu["c_oracle"] = {"error": str(e)}
+            log("cpu baseline: %.0f steps/s on %d cores (%s)" % (cpu["value"], cpu["cores"], cpu["share_source"]))
 
-    from poseestimationkf_amd import _lib
-    visible = _lib.device_count()
-    if plan["mode"] == "ranks" and visible == 1 and plan["devices"][0] > 0:
-        plan["devices"] = [0]   # the launcher gave each rank its own GPU (HIP/CUDA_VISIBLE_DEVICES)
-    need = max(plan["devices"]) + 1
-    if visible < need:
-        raise BenchError("--gpus %d (%s) needs %d visible GPU(s), %d visible" %
-                         (args.gpus, plan["mode"], need, visible))
+        from poseestimationkf_amd import _lib
+        visible = _lib.device_count()
+        if plan["mode"] == "ranks" and visible == 1 and plan["devices"][0] > 0:
+            plan["devices"] = [0]   # the launcher gave each rank its own GPU (HIP/CUDA_VISIBLE_DEVICES)
+        need = max(plan["devices"]) + 1
+        if visible < need:
+            raise BenchError("--gpus %d (%s) needs %d visible GPU(s), %d visible" %
+                             (args.gpus, plan["mode"], need, visible))
+    except BaseException as e:
+        if rdzv is not None:   # rank 0 exits before it has an id: the other ranks stop waiting for one
+            rdzv.fail("%s: %s" % (type(e).__name__, e))
+        raise
 
-    run = MultiRun(args, plan) if plan["mode"] == "multi" else RankRun(args, plan)
+    run = MultiRun(args, plan) if plan["mode"] == "multi" else RankRun(args, plan, rdzv)
     N, W = args.records, args.window
     total = args.warmup + args.steps
     run.prepare(total)
@@ -386,7 +559,7 @@ def main(argv=None):
     for k in range(args.warmup):
         run.step(k, N, (k * N) % W)
         run.sync()
-        log("warmup %d: kernel %.1f ms" % (k, run.kernel_ms(k)))
+        log("warmup %d: kernel %.1f ms, gather %.3f ms" % (k, run.kernel_ms(k), run.gather_ms(k)))
 
     run.sync()
     run.barrier()
@@ -396,9 +569,12 @@ def main(argv=None):
     run.sync()
     run.barrier()
     elapsed = run.slowest(time.perf_counter() - t0)
-    kms = [run.kernel_ms(k) for k in range(args.warmup, total)]
-    log("timed: %.3f s for %d steps on %d GPU(s); kernel ms %s" %
-        (elapsed, args.steps, world, ", ".join("%.1f" % v for v in kms)))
+    timed = range(args.warmup, total)
+    kms = [run.kernel_ms(k) for k in timed]
+    per_gpu = run.per_gpu(timed)
+    log("timed: %.3f s for %d steps on %d GPU(s); kernel ms per GPU %s; gather ms per GPU %s" %
+        (elapsed, args.steps, world, ", ".join("%.1f" % v for v in per_gpu[0]),
+         ", ".join("%.3f" % v for v in per_gpu[1])))
 
     # final quaternions of every GPU's filters on rank 0 (the gathered rows), then all ranks part
     rows = run.final_rows() if rank == 0 and args.parity_samples > 0 else None
@@ -411,19 +587,21 @@ def main(argv=None):
             (parity["max_abs_err_vs_oracle"], parity["filters"], parity["shards_covered"]))
 
     if rank == 0:
-        out = result_line(args, plan, elapsed, kms, cpu, parity)
+        out = result_line(args, plan, elapsed, kms, cpu, parity, per_gpu)
         out_fd.emit(json.dumps(out))
     run.close()
     if parity is not None and not (parity["ok"] and parity["unit_norm_all"]):
         raise SystemExit("parity failed: %r" % parity)
 
 
-def result_line(args, plan, elapsed, kms, cpu, parity):
+def result_line(args, plan, elapsed, kms, cpu, parity, per_gpu=None):
     import numpy as np
     world, B, N = plan["world"], args.batch, args.records
     steps_total = world * B * N * args.steps
     value = steps_total / elapsed
-    k_s = float(np.mean(kms)) / 1e3   # per-GPU kernel time (multi: the slowest device per step)
+    if per_gpu is None:
+        per_gpu = ([float(np.mean(kms))], [0.0])
+    k_s = float(np.mean(per_gpu[0])) / 1e3   # one GPU's launch: the mean over the GPUs of their mean kernel time
     achieved = B * N * REC_BYTES / k_s / 1e9
     counts = ISA_COUNTS[args.precision]
     valu = counts["valu_instr"]
@@ -480,6 +658,11 @@ def result_line(args, plan, elapsed, kms, cpu, parity):
                           if cited else None),
         "cpu_baseline": cpu,
         "parity": parity,
+        "kernel_ms_per_gpu": per_gpu[0],
+        "gather_ms_per_gpu": per_gpu[1],
+        "timing_note": "per GPU, in rank order: the fused launch's and the RCCL gather's mean HIP-event time "
+                       "over the timed steps on that GPU's stream (gather 0 when nothing is gathered); "
+                       "ms_per_step is the slowest rank's wall clock",
     }
 
 

@@ -39,6 +39,7 @@ extern "C" {
 #define PEKF_ERR_SVD 5      /* non-finite Wahba matrix B: np.linalg.svd raises LinAlgError  */
                             /* "SVD did not converge" (Wahba.py:14)                         */
 #define PEKF_ERR_COMM 6     /* collective library (RCCL) unavailable or failed              */
+#define PEKF_ERR_TIMEOUT 7  /* a collective step passed its deadline; the communicator was aborted */
 
 /* Bit 31 of a stream record's dt word: magnetometer sample missing ("Wahba-skip"). */
 #define PEKF_MISSING_MAG_BIT 0x80000000u
@@ -186,6 +187,10 @@ int pekf_state_layout_dev(int64_t batch, double *X_aos, double *P_aos, double *X
  * logged as "q_gyro"; step = ExtendedKalmanFilter.py:25-41).  q_gyro[batch*4] in/out; traj optional. */
 int pekf_gyro_chain_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
                         const void *plane_gd, double *q_gyro, double *traj, void *stream);
+/* pekf_gyro_chain_dev for a window with escaped dt words: dt_ext = the window's dt side plane, float64
+ * [window][batch], read at rows whose dt word is PEKF_DT_ESCAPE (NULL = exactly pekf_gyro_chain_dev). */
+int pekf_gyro_chain_ext_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0, const void *plane_gd,
+                            const double *dt_ext, double *q_gyro, double *traj, void *stream);
 /* Pure-Wahba attitude of every record with fixed weights (main_file.py:40: getQuarternion(acc, mag,
  * 0.5, 0.5)), out[n_steps][batch][4], same branch/sign convention as Wahba.RotationMatrix2Quart. */
 int pekf_wahba_stream_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
@@ -339,10 +344,25 @@ int pekf_synth_dev(int64_t batch, int64_t window, int64_t first_filter, uint32_t
 typedef struct pekf_comm pekf_comm;
 int pekf_comm_version(int *version); /* RCCL's version code, e.g. 22707 */
 int pekf_comm_unique_id(void *id /* PEKF_COMM_ID_BYTES */);
+/* Communicator creation has a deadline: RCCL's non-blocking init (ncclCommInitRankConfig with
+ * blocking = 0, rccl.h:204) polled with ncclCommGetAsyncError (rccl.h:362).  If the other ranks do not
+ * all join within PEKF_COMM_TIMEOUT_S seconds (environment; default 300), the half-made communicator
+ * is aborted (ncclCommAbort, rccl.h:271) and the call returns PEKF_ERR_TIMEOUT, so a rank that died
+ * before joining fails the job instead of hanging it.  The communicator stays non-blocking: every
+ * call below settles RCCL's ncclInProgress before it returns. */
 int pekf_comm_init(const void *id, int nranks, int rank, pekf_comm **out);
+/* The same with an explicit deadline in seconds (<= 0: wait forever, the blocking behaviour). */
+int pekf_comm_init_timeout(const void *id, int nranks, int rank, double timeout_s, pekf_comm **out);
 /* devices: ndev device indices (NULL = 0 .. ndev-1); out: ndev communicators, rank i on devices[i] */
 int pekf_comm_init_all(int ndev, const int *devices, pekf_comm **out);
 int pekf_comm_destroy(pekf_comm *c);
+/* Abort a communicator (ncclCommAbort: its kernels in flight give up) and free it; for error paths. */
+int pekf_comm_abort(pekf_comm *c);
+/* Wait until `stream` has drained everything enqueued on it, collectives of c included, for at most
+ * timeout_s seconds (<= 0: no deadline), watching c for asynchronous RCCL errors meanwhile.  On expiry
+ * or error c is aborted (it must then only be destroyed) and PEKF_ERR_TIMEOUT / PEKF_ERR_COMM returned:
+ * a peer that died turns into an error here instead of a host thread stuck in hipStreamSynchronize. */
+int pekf_comm_wait(pekf_comm *c, void *stream, double timeout_s);
 int pekf_comm_rank(const pekf_comm *c, int *rank, int *nranks, int *device); /* outputs may be NULL */
 /* recv[nranks * count] on the root (rows in rank order) <- every rank's send[count]; device
  * pointers, enqueued on stream.  recv is ignored (may be NULL) on the other ranks. */

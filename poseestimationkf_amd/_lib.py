@@ -20,6 +20,7 @@ PEKF_ERR_SINGULAR = 3
 PEKF_ERR_NODEVICE = 4
 PEKF_ERR_SVD = 5
 PEKF_ERR_COMM = 6
+PEKF_ERR_TIMEOUT = 7
 MISSING_MAG_BIT = 0x80000000
 RUN_MIXED_PRECISION = 0x1
 RUN_STATE_SOA = 0x2
@@ -35,6 +36,10 @@ class PekfError(RuntimeError):
 
 class NoDeviceError(PekfError):
     pass
+
+
+class CommTimeoutError(PekfError):
+    """A collective step passed its deadline (PEKF_COMM_TIMEOUT_S); the communicator was aborted."""
 
 
 _i64, _u32, _int, _dbl, _sz, _vp = ctypes.c_int64, ctypes.c_uint32, ctypes.c_int, ctypes.c_double, ctypes.c_size_t, ctypes.c_void_p
@@ -96,6 +101,7 @@ SIGNATURES = {
     "pekf_filter_run": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "pekf_filter_run_ext": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "pekf_gyro_chain_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
+    "pekf_gyro_chain_ext_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp],
     "pekf_wahba_stream_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp],
     "pekf_quat_to_rpy": [_i64, _vp, _vp],
     "pekf_frontend_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
@@ -111,6 +117,9 @@ SIGNATURES = {
     "pekf_comm_version": [_ip],
     "pekf_comm_unique_id": [ctypes.c_char_p],
     "pekf_comm_init": [ctypes.c_char_p, _int, _int, ctypes.POINTER(_vp)],
+    "pekf_comm_init_timeout": [ctypes.c_char_p, _int, _int, _dbl, ctypes.POINTER(_vp)],
+    "pekf_comm_abort": [_vp],
+    "pekf_comm_wait": [_vp, _vp, _dbl],
     "pekf_comm_init_all": [_int, _ip, ctypes.POINTER(_vp)],
     "pekf_comm_destroy": [_vp],
     "pekf_comm_rank": [_vp, _ip, _ip, _ip],
@@ -153,6 +162,8 @@ def check(status):
         raise np.linalg.LinAlgError(msg or "SVD did not converge")
     if status == PEKF_ERR_NODEVICE:
         raise NoDeviceError(status, msg)
+    if status == PEKF_ERR_TIMEOUT:
+        raise CommTimeoutError(status, msg)
     raise PekfError(status, msg)
 
 

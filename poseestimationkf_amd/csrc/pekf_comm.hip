@@ -10,11 +10,19 @@
 // that never shards pays nothing for it, and in a process that already has an RCCL loaded (the
 // one PyTorch-ROCm bundles) the loader hands back that same library, so there is one RCCL and
 // one HIP runtime per process.
+//
+// Deadlines: a communicator is created non-blocking (ncclCommInitRankConfig, blocking = 0) and polled
+// against PEKF_COMM_TIMEOUT_S, and pekf_comm_wait drains a stream of collectives against a deadline;
+// on expiry the communicator is aborted (ncclCommAbort), so a rank that never joins or dies mid-run
+// ends the job with PEKF_ERR_TIMEOUT instead of leaving every other rank blocked inside RCCL.
 #include <dlfcn.h>
 
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -36,6 +44,9 @@ struct Rccl {
     decltype(&::ncclGroupEnd) group_end = nullptr;
     decltype(&::ncclGetErrorString) error_string = nullptr;
     decltype(&::ncclGetVersion) get_version = nullptr;
+    decltype(&::ncclCommInitRankConfig) init_rank_config = nullptr;  // optional: deadline-aware init
+    decltype(&::ncclCommGetAsyncError) async_error = nullptr;
+    decltype(&::ncclCommAbort) abort = nullptr;
     char why[256] = "";
     bool ok = false;
 };
@@ -69,7 +80,10 @@ Rccl &rccl() {
         sym(r.group_end, "ncclGroupEnd");
         sym(r.error_string, "ncclGetErrorString");
         sym(r.get_version, "ncclGetVersion");
+        sym(r.async_error, "ncclCommGetAsyncError");
+        sym(r.abort, "ncclCommAbort");
         r.ok = all;
+        r.init_rank_config = reinterpret_cast<decltype(r.init_rank_config)>(dlsym(h, "ncclCommInitRankConfig"));
     });
     return r;
 }
@@ -93,13 +107,74 @@ int nccl_fail(ncclResult_t e, const char *what) {
 
 static_assert(sizeof(ncclUniqueId) == PEKF_COMM_ID_BYTES, "RCCL unique id size");
 
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// PEKF_COMM_TIMEOUT_S (seconds; <= 0 disables the deadline), default 300
+double env_timeout_s() {
+    const char *v = getenv("PEKF_COMM_TIMEOUT_S");
+    if (!v || !*v) return 300.0;
+    char *end = nullptr;
+    const double t = strtod(v, &end);
+    return (end && end != v) ? t : 300.0;
+}
+
+double deadline_after(double timeout_s) { return timeout_s > 0 ? now_s() + timeout_s : 0.0; }
+
+// Polls a non-blocking communicator until RCCL has finished the call in progress on it.
+// Returns PEKF_OK, the RCCL error, or PEKF_ERR_TIMEOUT (*expired set) at the deadline (0 = none).
+int settle(ncclComm_t nc, double deadline, const char *what, bool *expired) {
+    *expired = false;
+    for (;;) {
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t e = rccl().async_error(nc, &st);
+        if (e != ncclSuccess) return nccl_fail(e, "ncclCommGetAsyncError");
+        if (st == ncclSuccess) return PEKF_OK;
+        if (st != ncclInProgress) return nccl_fail(st, what);
+        if (deadline > 0 && now_s() > deadline) {
+            *expired = true;
+            return PEKF_ERR_TIMEOUT;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(500));
+    }
+}
+
 }  // namespace
 }  // namespace pekf
 
 struct pekf_comm {
     ncclComm_t nc;
     int nranks, rank, device;
+    double timeout_s;  // deadline of each settle / wait on this communicator (<= 0: none)
 };
+
+namespace pekf {
+namespace {
+
+// Aborts c's RCCL communicator (kernels of it still in flight give up) and leaves c destroy-only.
+void abort_comm(pekf_comm *c) {
+    if (c->nc) (void)rccl().abort(c->nc);
+    c->nc = nullptr;
+}
+
+// Result of an enqueue on c: ncclInProgress (non-blocking communicator) is settled against c's
+// deadline; an expired deadline aborts c.
+int enqueued(pekf_comm *c, ncclResult_t e, const char *what) {
+    if (e == ncclSuccess) return PEKF_OK;
+    if (e != ncclInProgress) return nccl_fail(e, what);
+    bool expired = false;
+    const int st = settle(c->nc, deadline_after(c->timeout_s), what, &expired);
+    if (expired) {
+        abort_comm(c);
+        return set_error(PEKF_ERR_TIMEOUT, "%s: still in progress after %.0f s; communicator aborted", what,
+                         c->timeout_s);
+    }
+    return st;
+}
+
+}  // namespace
+}  // namespace pekf
 
 using namespace pekf;
 
@@ -121,7 +196,7 @@ int pekf_comm_unique_id(void *id) {
     return PEKF_OK;
 }
 
-int pekf_comm_init(const void *id, int nranks, int rank, pekf_comm **out) {
+int pekf_comm_init_timeout(const void *id, int nranks, int rank, double timeout_s, pekf_comm **out) {
     PEKF_CHECK_ARG(id && out, "null pointer");
     PEKF_CHECK_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "need 0 <= rank < nranks");
     *out = nullptr;
@@ -131,9 +206,38 @@ int pekf_comm_init(const void *id, int nranks, int rank, pekf_comm **out) {
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
     ncclComm_t nc = nullptr;
-    PEKF_NCCL(rccl().init_rank(&nc, nranks, u, rank));  // collective over the nranks processes
-    *out = new pekf_comm{nc, nranks, rank, dev};
+    Rccl &r = rccl();
+    if (timeout_s <= 0 || !r.init_rank_config) {
+        PEKF_NCCL(r.init_rank(&nc, nranks, u, rank));  // collective over the nranks processes, no deadline
+        *out = new pekf_comm{nc, nranks, rank, dev, 0.0};
+        return PEKF_OK;
+    }
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;  // returns at once (ncclInProgress); completion is polled below
+    const double deadline = deadline_after(timeout_s);
+    const ncclResult_t e = r.init_rank_config(&nc, nranks, u, rank, &cfg);
+    if (e != ncclSuccess && e != ncclInProgress) {
+        if (nc) (void)r.abort(nc);
+        return nccl_fail(e, "ncclCommInitRankConfig");
+    }
+    if (!nc) return set_error(PEKF_ERR_COMM, "ncclCommInitRankConfig returned no communicator");
+    bool expired = false;
+    const int st = settle(nc, deadline, "ncclCommInitRankConfig", &expired);
+    if (st != PEKF_OK) {
+        (void)r.abort(nc);
+        if (expired)
+            return set_error(PEKF_ERR_TIMEOUT,
+                             "RCCL communicator init (ncclCommInitRankConfig, rank %d of %d, device %d): not all %d "
+                             "ranks joined within %.0f s (PEKF_COMM_TIMEOUT_S); communicator aborted",
+                             rank, nranks, dev, nranks, timeout_s);
+        return st;
+    }
+    *out = new pekf_comm{nc, nranks, rank, dev, timeout_s};
     return PEKF_OK;
+}
+
+int pekf_comm_init(const void *id, int nranks, int rank, pekf_comm **out) {
+    return pekf_comm_init_timeout(id, nranks, rank, env_timeout_s(), out);
 }
 
 int pekf_comm_init_all(int ndev, const int *devices, pekf_comm **out) {
@@ -148,16 +252,58 @@ int pekf_comm_init_all(int ndev, const int *devices, pekf_comm **out) {
     }
     std::vector<ncclComm_t> nc(ndev, nullptr);
     PEKF_NCCL(rccl().init_all(nc.data(), ndev, devs.data()));
-    for (int i = 0; i < ndev; ++i) out[i] = new pekf_comm{nc[i], ndev, i, devs[i]};
+    for (int i = 0; i < ndev; ++i) out[i] = new pekf_comm{nc[i], ndev, i, devs[i], env_timeout_s()};
     return PEKF_OK;
 }
 
 int pekf_comm_destroy(pekf_comm *c) {
     if (!c) return PEKF_OK;
-    const ncclResult_t e = rccl().destroy(c->nc);
+    if (!c->nc) {  // aborted: nothing left to destroy
+        delete c;
+        return PEKF_OK;
+    }
+    ncclResult_t e = rccl().destroy(c->nc);
+    if (e == ncclInProgress) {  // non-blocking communicator: wait for the teardown
+        bool expired = false;
+        if (settle(c->nc, deadline_after(c->timeout_s), "ncclCommDestroy", &expired) == PEKF_OK) e = ncclSuccess;
+        else (void)rccl().abort(c->nc);
+    }
     delete c;
-    if (e != ncclSuccess) return nccl_fail(e, "ncclCommDestroy");
+    if (e != ncclSuccess && e != ncclInProgress) return nccl_fail(e, "ncclCommDestroy");
     return PEKF_OK;
+}
+
+int pekf_comm_abort(pekf_comm *c) {
+    if (!c) return PEKF_OK;
+    abort_comm(c);
+    delete c;
+    return PEKF_OK;
+}
+
+int pekf_comm_wait(pekf_comm *c, void *stream, double timeout_s) {
+    PEKF_CHECK_ARG(c, "null communicator");
+    PEKF_CHECK_ARG(c->nc, "communicator was aborted");
+    const hipStream_t s = as_stream(stream);
+    const double deadline = deadline_after(timeout_s);
+    for (;;) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) return PEKF_OK;
+        if (q != hipErrorNotReady) return hip_fail(q, "hipStreamQuery");
+        ncclResult_t st = ncclSuccess;
+        if (rccl().async_error(c->nc, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress) {
+            abort_comm(c);
+            return set_error(PEKF_ERR_COMM, "RCCL asynchronous error on rank %d of %d: %s (%d); communicator aborted",
+                             c->rank, c->nranks, rccl().error_string(st), (int)st);
+        }
+        if (deadline > 0 && now_s() > deadline) {
+            abort_comm(c);
+            return set_error(PEKF_ERR_TIMEOUT,
+                             "rank %d of %d: the stream's collectives did not complete within %.0f s (a peer rank "
+                             "gone?); communicator aborted",
+                             c->rank, c->nranks, timeout_s);
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
 }
 
 int pekf_comm_rank(const pekf_comm *c, int *rank, int *nranks, int *device) {
@@ -173,8 +319,9 @@ int pekf_gather_dev(pekf_comm *c, const double *send, int64_t count, double *rec
     PEKF_CHECK_ARG(count >= 0, "negative size");
     PEKF_CHECK_ARG(root >= 0 && root < c->nranks, "root out of range");
     PEKF_CHECK_ARG(c->rank != root || recv, "the root needs a receive buffer of nranks * count doubles");
-    PEKF_NCCL(rccl().gather(send, recv, (size_t)count, ncclFloat64, root, c->nc, as_stream(stream)));
-    return PEKF_OK;
+    PEKF_CHECK_ARG(c->nc, "communicator was aborted");
+    return enqueued(c, rccl().gather(send, recv, (size_t)count, ncclFloat64, root, c->nc, as_stream(stream)),
+                    "ncclGather");
 }
 
 int pekf_gather_multi_dev(int ndev, pekf_comm *const *comms, const double *const *send, int64_t count,
@@ -182,6 +329,7 @@ int pekf_gather_multi_dev(int ndev, pekf_comm *const *comms, const double *const
     PEKF_CHECK_ARG(ndev >= 1 && comms && send && streams, "null pointer");
     PEKF_CHECK_ARG(count >= 0, "negative size");
     PEKF_CHECK_ARG(root >= 0 && root < ndev && recv, "root out of range or no receive buffer");
+    for (int i = 0; i < ndev; ++i) PEKF_CHECK_ARG(comms[i] && comms[i]->nc, "null or aborted communicator");
     PEKF_NCCL(rccl().group_start());
     for (int i = 0; i < ndev; ++i) {
         const ncclResult_t e = rccl().gather(send[i], i == root ? recv : nullptr, (size_t)count, ncclFloat64, root,
@@ -198,8 +346,9 @@ int pekf_gather_multi_dev(int ndev, pekf_comm *const *comms, const double *const
 int pekf_allreduce_max_dev(pekf_comm *c, double *buf, int64_t count, void *stream) {
     PEKF_CHECK_ARG(c && buf, "null pointer");
     PEKF_CHECK_ARG(count >= 0, "negative size");
-    PEKF_NCCL(rccl().all_reduce(buf, buf, (size_t)count, ncclFloat64, ncclMax, c->nc, as_stream(stream)));
-    return PEKF_OK;
+    PEKF_CHECK_ARG(c->nc, "communicator was aborted");
+    return enqueued(c, rccl().all_reduce(buf, buf, (size_t)count, ncclFloat64, ncclMax, c->nc, as_stream(stream)),
+                    "ncclAllReduce");
 }
 
 }  // extern "C"

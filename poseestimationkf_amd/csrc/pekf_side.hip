@@ -22,8 +22,12 @@ constexpr int kDepth = 8;
 
 __device__ __forceinline__ int64_t next_row(int64_t r, int64_t window) { return r + 1 == window ? 0 : r + 1; }
 
+// LONGDT: the window has a dt side plane dtx[window][batch] (float64 ns); a record whose dt word is
+// PEKF_DT_ESCAPE takes its dt from there, exactly as the filter does (k_run<..., LONGDT>).
+template <bool LONGDT>
 __global__ __launch_bounds__(kSideBlock) void k_gyro_chain(int64_t batch, int64_t n_steps, int64_t window,
                                                            int64_t step0, const float4 *__restrict__ gd,
+                                                           const double *__restrict__ dtx,
                                                            double *__restrict__ q, double *__restrict__ traj) {
     const int64_t b = (int64_t)blockIdx.x * kSideBlock + threadIdx.x;
     if (b >= batch) return;
@@ -45,7 +49,11 @@ __global__ __launch_bounds__(kSideBlock) void k_gyro_chain(int64_t batch, int64_
             ring[k] = (gd + pf * batch)[lane];
             pf = next_row(pf, window);
             const double hw[3] = {0.5 * (double)r.x, 0.5 * (double)r.y, 0.5 * (double)r.z};
-            const double dt_ns = (double)(__float_as_uint(r.w) & 0x7FFFFFFFu);
+            const uint32_t word = __float_as_uint(r.w) & PEKF_DT_MASK;
+            double dt_ns = (double)word;
+            if constexpr (LONGDT) {  // off the fast path: the escaped record's row, (step0 + t) % window
+                if (word == PEKF_DT_ESCAPE) dt_ns = dtx[((step0 + t) % window) * batch + b];
+            }
             double z[4];
             rk4_closed(x, x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3], dt_ns, hw, z);
             x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
@@ -147,17 +155,27 @@ using namespace pekf;
 
 extern "C" {
 
-int pekf_gyro_chain_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
-                        const void *plane_gd, double *q_gyro, double *traj, void *stream) {
+int pekf_gyro_chain_ext_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0, const void *plane_gd,
+                            const double *dt_ext, double *q_gyro, double *traj, void *stream) {
     PEKF_CHECK_ARG(batch >= 0 && n_steps >= 0, "negative size");
     if (batch == 0 || n_steps == 0) return PEKF_OK;
     PEKF_CHECK_ARG(window > 0 && step0 >= 0, "window must be > 0 and step0 >= 0");
     PEKF_CHECK_ARG(batch < ((int64_t)1 << 28), "batch must be < 2^28 filters per launch");
     PEKF_CHECK_ARG(plane_gd && q_gyro, "null pointer");
-    hipLaunchKernelGGL(k_gyro_chain, dim3(grid_for(batch, kSideBlock)), dim3(kSideBlock), 0,
-                       as_stream(stream), batch, n_steps, window, step0,
-                       static_cast<const float4 *>(plane_gd), q_gyro, traj);
+    const dim3 grid(grid_for(batch, kSideBlock)), block(kSideBlock);
+    const float4 *gd = static_cast<const float4 *>(plane_gd);
+    if (dt_ext)
+        hipLaunchKernelGGL(k_gyro_chain<true>, grid, block, 0, as_stream(stream), batch, n_steps, window, step0, gd,
+                           dt_ext, q_gyro, traj);
+    else
+        hipLaunchKernelGGL(k_gyro_chain<false>, grid, block, 0, as_stream(stream), batch, n_steps, window, step0, gd,
+                           nullptr, q_gyro, traj);
     return launched("k_gyro_chain");
+}
+
+int pekf_gyro_chain_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
+                        const void *plane_gd, double *q_gyro, double *traj, void *stream) {
+    return pekf_gyro_chain_ext_dev(batch, n_steps, window, step0, plane_gd, nullptr, q_gyro, traj, stream);
 }
 
 int pekf_wahba_stream_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,

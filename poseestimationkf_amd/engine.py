@@ -21,6 +21,7 @@ class DeviceBuffer:
 
     def __init__(self, nbytes):
         self.nbytes = int(nbytes)
+        self._lib = lib   # freed by the library that allocated it
         p = ctypes.c_void_p()
         check(lib.pekf_malloc(ctypes.byref(p), max(1, self.nbytes)))
         self.ptr = p.value
@@ -39,7 +40,7 @@ class DeviceBuffer:
 
     def free(self):
         if getattr(self, "ptr", None):
-            lib.pekf_free(self.ptr)
+            self._lib.pekf_free(self.ptr)
             self.ptr = None
 
     def __del__(self):
@@ -51,23 +52,25 @@ class DeviceBuffer:
 
 class Stream:
     def __init__(self):
+        self._lib = lib
         s = ctypes.c_void_p()
         check(lib.pekf_stream_create(ctypes.byref(s)))
         self.handle = s.value
 
     def sync(self):
-        check(lib.pekf_stream_sync(self.handle))
+        check(self._lib.pekf_stream_sync(self.handle))
 
     def __del__(self):
         try:
             if self.handle:
-                lib.pekf_stream_destroy(self.handle)
+                self._lib.pekf_stream_destroy(self.handle)
         except Exception:
             pass
 
 
 class Event:
     def __init__(self):
+        self._lib = lib
         e = ctypes.c_void_p()
         check(lib.pekf_event_create(ctypes.byref(e)))
         self.handle = e.value
@@ -86,7 +89,7 @@ class Event:
     def __del__(self):
         try:
             if self.handle:
-                lib.pekf_event_destroy(self.handle)
+                self._lib.pekf_event_destroy(self.handle)
         except Exception:
             pass
 
@@ -207,12 +210,12 @@ class IMUWindow:
                 out.append(pad)
             return np.concatenate(out, axis=1)
         escaped = any(r.dtx is not None for r in recs)
-        for r in recs:
-            if escaped and r.dtx is None:
-                r.dtx = np.zeros(r.dtw.shape, np.float64)
+        dtx = None
+        if escaped:  # logs without escapes get a zero side plane (never read: their words are not escapes)
+            dtx = [r.dtx if r.dtx is not None else np.zeros(r.dtw.shape, np.float64) for r in recs]
+            dtx = np.concatenate([np.pad(d[:n], ((0, n - min(n, d.shape[0])), (0, 0))) for d in dtx], axis=1)
         rec = synth.Records(cat("gyro"), cat("acc"), cat("mag"), cat("dtw"),
-                            np.concatenate([r.acc0 for r in recs]), np.concatenate([r.mag0 for r in recs]),
-                            cat("dtx") if escaped else None)
+                            np.concatenate([r.acc0 for r in recs]), np.concatenate([r.mag0 for r in recs]), dtx)
         win = cls.from_records(rec)
         win.counts = np.minimum(lens, n).astype(np.int32)
         return win
@@ -243,8 +246,10 @@ class IMUWindow:
         q = np.tile([1.0, 0.0, 0.0, 0.0], (self.batch, 1)) if q0 is None else f64(q0, (self.batch, 4))
         qb = DeviceBuffer(32 * self.batch).upload(q)
         tb = DeviceBuffer(32 * n_steps * self.batch) if want_traj else None
-        check(lib.pekf_gyro_chain_dev(self.batch, n_steps, self.window, int(step0), self.gd.ptr, qb.ptr,
-                                      tb.ptr if tb is not None else None, None))
+        # escaped records (a dt the word cannot hold) take their dt from the window's side plane, as in the filter
+        check(lib.pekf_gyro_chain_ext_dev(self.batch, n_steps, self.window, int(step0), self.gd.ptr,
+                                          self.dtx.ptr if self.dtx is not None else None, qb.ptr,
+                                          tb.ptr if tb is not None else None, None))
         check(lib.pekf_device_sync())
         return (qb.download((self.batch, 4), np.float64),
                 tb.download((n_steps, self.batch, 4), np.float64) if want_traj else None)

@@ -28,6 +28,20 @@ from ._lib import check, lib
 
 COMM_ID_BYTES = 128
 _RDZV_MAGIC = b"PEKFRDZV1"
+_RDZV_FAIL = b"PEKFRDZVX"   # rank 0 failed before it could publish an id; the message follows
+
+
+class RendezvousError(RuntimeError):
+    """Rank 0 published a failure instead of the RCCL id (FileRendezvous.fail)."""
+
+
+def comm_timeout():
+    """Deadline in seconds of each collective step (PEKF_COMM_TIMEOUT_S, default 300; <= 0: none) --
+    the same value libpekf applies to communicator creation (include/pekf.h)."""
+    try:
+        return float(os.environ.get("PEKF_COMM_TIMEOUT_S", "300"))
+    except ValueError:
+        return 300.0
 
 
 def shard_range(global_batch, rank, world):
@@ -48,16 +62,17 @@ class Communicator:
     """One rank of an RCCL communicator on the current device, owned through libpekf."""
 
     def __init__(self, unique_id: bytes, nranks: int, rank: int, _handle=None):
+        self._lib = lib   # the library that owns the handle (closes it, even if `lib` is rebound later)
         if _handle is not None:  # from init_all
             self.handle = _handle
         else:
             if len(unique_id) != COMM_ID_BYTES:
                 raise ValueError("an RCCL unique id is %d bytes" % COMM_ID_BYTES)
-            h = ctypes.c_void_p()
+            h = ctypes.c_void_p()   # non-blocking RCCL init polled against PEKF_COMM_TIMEOUT_S (pekf.h)
             check(lib.pekf_comm_init(bytes(unique_id), int(nranks), int(rank), ctypes.byref(h)))
             self.handle = h.value
         r, n, d = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        check(lib.pekf_comm_rank(self.handle, ctypes.byref(r), ctypes.byref(n), ctypes.byref(d)))
+        check(self._lib.pekf_comm_rank(self.handle, ctypes.byref(r), ctypes.byref(n), ctypes.byref(d)))
         self.rank, self.nranks, self.device = r.value, n.value, d.value
 
     @staticmethod
@@ -76,18 +91,37 @@ class Communicator:
 
     def gather(self, send_ptr, count, recv_ptr=None, root=0, stream=None):
         """recv[nranks*count] on root <- every rank's send[count] float64 (device pointers, enqueued)."""
-        check(lib.pekf_gather_dev(self.handle, send_ptr, int(count), recv_ptr, int(root), stream))
+        check(self._lib.pekf_gather_dev(self.handle, send_ptr, int(count), recv_ptr, int(root), stream))
 
     def allreduce_max(self, buf_ptr, count, stream=None):
-        check(lib.pekf_allreduce_max_dev(self.handle, buf_ptr, int(count), stream))
+        check(self._lib.pekf_allreduce_max_dev(self.handle, buf_ptr, int(count), stream))
 
-    def max_over_ranks(self, value, stream=None):
-        """max of a host float over all ranks (one RCCL all-reduce of 8 bytes, then a stream sync)."""
+    def wait(self, stream=None, timeout=None):
+        """Drain `stream` (collectives of this communicator included) within the deadline (default
+        comm_timeout()); a peer that never arrives raises CommTimeoutError and aborts the communicator."""
+        check(self._lib.pekf_comm_wait(self.handle, stream, comm_timeout() if timeout is None else float(timeout)))
+
+    def max_over_ranks_array(self, values, stream=None):
+        """Elementwise max of a host float64 vector over all ranks (one RCCL all-reduce, a deadline-bound
+        wait).  With every rank writing only its own slots (the rest -inf), it is an all-gather of them."""
         from .engine import DeviceBuffer
 
-        b = DeviceBuffer(8).upload(np.array([value], np.float64), stream)
-        self.allreduce_max(b.ptr, 1, stream)
-        return float(b.download((1,), np.float64, stream)[0])
+        v = np.ascontiguousarray(values, np.float64).ravel()
+        b = DeviceBuffer(v.nbytes).upload(v, stream)
+        self.allreduce_max(b.ptr, v.size, stream)
+        self.wait(stream)
+        return b.download(v.shape, np.float64, stream)
+
+    def max_over_ranks(self, value, stream=None):
+        """max of a host float over all ranks (one RCCL all-reduce of 8 bytes, then a deadline-bound wait)."""
+        return float(self.max_over_ranks_array([value], stream)[0])
+
+    def all_values(self, values, stream=None):
+        """Every rank's `values` (same length on each), as an (nranks, len) array on every rank."""
+        v = np.ascontiguousarray(values, np.float64).ravel()
+        slots = np.full((self.nranks, v.size), -np.inf)
+        slots[self.rank] = v
+        return self.max_over_ranks_array(slots, stream).reshape(self.nranks, v.size)
 
     def barrier(self, stream=None):
         """Every rank has reached this point (and its stream has drained up to it)."""
@@ -96,7 +130,13 @@ class Communicator:
     def close(self):
         if getattr(self, "handle", None):
             h, self.handle = self.handle, None
-            check(lib.pekf_comm_destroy(h))
+            check(self._lib.pekf_comm_destroy(h))
+
+    def abort(self):
+        """ncclCommAbort (error paths: the peers' collectives with this rank give up)."""
+        if getattr(self, "handle", None):
+            h, self.handle = self.handle, None
+            check(self._lib.pekf_comm_abort(h))
 
     def __del__(self):
         try:
@@ -122,22 +162,32 @@ class FileRendezvous:
     ever ran on the node, so a file left behind by another job is never read.  Rank 0 writes the id
     atomically (temp file + rename); the others poll for it.  `key` / PEKF_RDZV_KEY override the key
     for launchers whose ranks do not share a parent; PEKF_RDZV_DIR names the directory (it must be
-    shared by every rank, e.g. a network file system when ranks span nodes).
+    shared by every rank, e.g. a network file system when ranks span nodes).  A job that spans nodes
+    must name its key: the default (the local parent) differs between nodes, so it is refused there.
+    If rank 0 fails before it has an id, `fail(msg)` publishes the failure and the other ranks raise
+    at once instead of waiting out `timeout` (PEKF_RDZV_TIMEOUT_S, default 600 s).
     RCCL's communicator creation is itself collective, so after it returns on rank 0 every rank
     has read the file and `done()` removes it."""
 
-    def __init__(self, rank, world, key=None, directory=None, timeout=600.0):
+    def __init__(self, rank, world, key=None, directory=None, timeout=None, environ=None):
+        env = os.environ if environ is None else environ
+        if timeout is None:
+            timeout = float(env.get("PEKF_RDZV_TIMEOUT_S", "600"))
         self.rank, self.world, self.timeout = int(rank), int(world), float(timeout)
         if not 0 <= self.rank < self.world:
             raise ValueError("need 0 <= rank < world")
         if key is None:
-            key = os.environ.get("PEKF_RDZV_KEY")
+            key = env.get("PEKF_RDZV_KEY")
+        if key is None and self.world > 1 and _spans_nodes(env):
+            raise ValueError("FileRendezvous: this job spans nodes (GROUP_WORLD_SIZE / LOCAL_WORLD_SIZE), so its ranks "
+                             "have no common parent; set PEKF_RDZV_KEY to one job-wide value and PEKF_RDZV_DIR to a "
+                             "directory every node shares")
         if key is None:
             ppid = os.getppid()
-            key = "%s_%s_%d_%d" % (os.environ.get("MASTER_ADDR", "local"), os.environ.get("MASTER_PORT", "0"),
+            key = "%s_%s_%d_%d" % (env.get("MASTER_ADDR", "local"), env.get("MASTER_PORT", "0"),
                                    ppid, _proc_start_ticks(ppid))
         key = "".join(c if c.isalnum() or c in "-_." else "_" for c in str(key))
-        directory = directory or os.environ.get("PEKF_RDZV_DIR") or tempfile.gettempdir()
+        directory = directory or env.get("PEKF_RDZV_DIR") or tempfile.gettempdir()
         self.path = os.path.join(directory, "pekf-rdzv-%s.id" % key)
 
     def share_id(self, make_id=None):
@@ -161,12 +211,23 @@ class FileRendezvous:
                     blob = fh.read()
                 if blob.startswith(_RDZV_MAGIC) and len(blob) == len(_RDZV_MAGIC) + COMM_ID_BYTES:
                     return blob[len(_RDZV_MAGIC):]
+                if blob.startswith(_RDZV_FAIL):
+                    raise RendezvousError("rank %d: rank 0 failed before publishing the RCCL id: %s"
+                                       % (self.rank, blob[len(_RDZV_FAIL):].decode(errors="replace")))
             except FileNotFoundError:
                 pass
             if time.monotonic() > deadline:
                 raise TimeoutError("rank %d: no RCCL id from rank 0 at %s after %.0f s"
                                    % (self.rank, self.path, self.timeout))
             time.sleep(0.01)
+
+    def fail(self, message):
+        """Rank 0 could not create the id (it is exiting): publish that, so the others stop waiting."""
+        if self.rank == 0 and self.world > 1:
+            tmp = "%s.%d.tmp" % (self.path, os.getpid())
+            with open(tmp, "wb") as fh:
+                fh.write(_RDZV_FAIL + str(message).encode()[:4000])
+            os.replace(tmp, self.path)
 
     def done(self):
         """Rank 0 removes the published id (call after the communicator exists on rank 0)."""
@@ -175,6 +236,17 @@ class FileRendezvous:
                 os.unlink(self.path)
             except FileNotFoundError:
                 pass
+
+
+def _spans_nodes(env):
+    """True when the launcher says the job has ranks on more than one node (torchrun's variables)."""
+    try:
+        if int(env.get("GROUP_WORLD_SIZE", "1")) > 1:
+            return True
+        lws = env.get("LOCAL_WORLD_SIZE")
+        return lws is not None and "WORLD_SIZE" in env and int(env["WORLD_SIZE"]) != int(lws)
+    except ValueError:
+        return False
 
 
 def connect(rank, world, rendezvous=None):

@@ -61,11 +61,14 @@ def test_config4_shard_plan_covers_8m_filters():
 
 
 def test_cpu_share_follows_the_job_share():
+    """This machine's own share: never more processes than the affinity mask, the cgroup quota or the
+    cpuset allow (the per-case cgroup layouts are in test_bench_multi.py)."""
     bench = _bench()
-    use, cores = bench.cpu_share({"OMP_NUM_THREADS": "1"})
-    assert use == 1 and cores >= 1
-    use, cores = bench.cpu_share({})
-    assert use == cores
+    s = bench.cpu_share({})
+    assert 1 <= s["use"] <= s["affinity"] == len(os.sched_getaffinity(0))
+    for lim in (s["quota_cores"], s["cpuset_cores"]):
+        assert lim is None or s["use"] <= lim
+    assert s["share_source"]
 
 
 def test_more_gpus_than_visible_exits_nonzero():
@@ -121,6 +124,7 @@ def test_one_process_multi_device_path_on_one_gpu():
     gather) at N = 1: one JSON line, n_gpus = the devices used, parity of the gathered rows."""
     d, err = _run_bench("--one-process")
     assert d["n_gpus"] == 1 and "ncclCommInitAll" in d["config"]["launch"]
+    assert len(d["kernel_ms_per_gpu"]) == 1 and d["kernel_ms_per_gpu"][0] > 0 and d["gather_ms_per_gpu"][0] > 0
     assert d["parity"]["ok"] and d["parity"]["max_abs_err_vs_oracle"] < 1e-9 and d["parity"]["unit_norm_all"]
     assert "ncclCommInitAll" in err
 
@@ -132,6 +136,7 @@ def test_launcher_rank_path_world1():
     d, err = _run_bench("--dist", env={"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0",
                                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29561"})
     assert d["n_gpus"] == 1 and d["config"]["launch"].startswith("one process per GPU")
+    assert d["kernel_ms_per_gpu"][0] > 0 and d["gather_ms_per_gpu"][0] > 0
     assert d["parity"]["ok"] and d["parity"]["max_abs_err_vs_oracle"] < 1e-9
 
 
@@ -147,3 +152,24 @@ def test_config4_rank7_shard_on_one_gpu():
     assert p["records"] == 10000 and p["filters"] == 64 and p["shards_covered"] == [7]
     assert p["global_filter_ids"][0] == 7 << 20 and p["global_filter_ids"][1] == (8 << 20) - 1
     assert p["max_abs_err_vs_oracle"] < 1e-9 and p["unit_norm_all"]
+
+
+@pytest.mark.gpu
+def test_missing_rank_fails_within_the_comm_deadline():
+    """A 2-rank job whose rank 1 never starts: rank 0's RCCL communicator creation (non-blocking
+    ncclCommInitRankConfig polled against PEKF_COMM_TIMEOUT_S) gives up, aborts the communicator and
+    bench.py exits 2 with a message naming the init -- instead of blocking inside RCCL forever."""
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env.update(RANK="0", WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29577",
+               PEKF_COMM_TIMEOUT_S="20", PEKF_RDZV_KEY="missing-rank-test-%d" % os.getpid())
+    t0 = time.monotonic()
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", "4096",
+                          "--records", "64", "--window", "32", "--cpu-baseline", "none"],
+                         capture_output=True, text=True, timeout=100, cwd=ROOT, env=env)
+    wall = time.monotonic() - t0
+    print("missing rank: exit %d after %.1f s; %s" % (out.returncode, wall, out.stderr.strip().splitlines()[-1]))
+    assert out.returncode == 2, out.stderr[-3000:]
+    assert "ncclCommInitRankConfig" in out.stderr and "20 s" in out.stderr
+    assert out.stdout.strip() == ""
+    assert wall < 60

@@ -309,3 +309,26 @@ def test_phase2_with_pauses_and_clock_steps(eng):
         if o["ready"]:
             assert got["t_init"][k] == o["t_init"]
             assert np.array_equal(got["init"][k], np.array(o["acc"] + o["mag"]))
+
+
+@pytest.mark.gpu
+def test_gyro_chain_reads_escaped_dts(eng):
+    """The pure-gyro side output (KFS/KalmanFilter.cpp:149, RungeKutta4 of ExtendedKalmanFilter.py:25-41 on
+    the gyro records alone) takes an escaped record's dt from the window's side plane, as the filter does:
+    a 5 s pause or a clock stepping back integrates that dt, never the escape word's 2^31 - 1 ns."""
+    from oracle import ekf_numpy as npo
+    rec = _escaped_records(K=64, W=40)
+    win = eng.IMUWindow.from_records(rec)
+    assert win.dtx is not None
+    qf, tr = win.gyro_chain(n_steps=50, step0=3, want_traj=True)   # wraps the 40-record window
+    dt = rec.dt_ns
+    err = 0.0
+    for k in (0, 5, 17, 63):
+        q = np.array([1.0, 0, 0, 0])
+        for t in range(50):
+            row = (3 + t) % 40
+            q = npo.rk4(q, dt[row, k], rec.gyro[row, k].astype(np.float64))
+            err = max(err, _err(tr[t, k], q))
+    assert np.array_equal(qf, tr[-1])
+    print("gyro chain over escaped dts vs the NumPy restatement: max |dq| = %.3e" % err)
+    assert err < 1e-12

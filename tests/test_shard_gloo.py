@@ -158,3 +158,27 @@ def test_two_rank_gloo_gather_equals_single_process(tmp_path):
     assert uid == ID
     assert got.shape == (16, 4)
     assert np.array_equal(got, X)
+
+
+def test_rendezvous_multinode_needs_a_key_and_rank0_failure_is_published(tmp_path):
+    """A job spanning nodes (torchrun's GROUP_WORLD_SIZE > 1, or WORLD_SIZE != LOCAL_WORLD_SIZE) has no
+    common parent, so the default key is refused at once; with PEKF_RDZV_KEY it is accepted.  A rank 0
+    that fails before it has an id publishes the failure, and a waiting rank raises at once."""
+    env = {"WORLD_SIZE": "16", "LOCAL_WORLD_SIZE": "8", "GROUP_WORLD_SIZE": "2"}
+    with pytest.raises(ValueError, match="PEKF_RDZV_KEY"):
+        shard.FileRendezvous(3, 16, directory=str(tmp_path), environ=env)
+    with pytest.raises(ValueError, match="PEKF_RDZV_KEY"):
+        shard.FileRendezvous(3, 16, directory=str(tmp_path), environ={"WORLD_SIZE": "16", "LOCAL_WORLD_SIZE": "8"})
+    ok = shard.FileRendezvous(3, 16, directory=str(tmp_path), environ=dict(env, PEKF_RDZV_KEY="job42"))
+    assert os.path.basename(ok.path) == "pekf-rdzv-job42.id"
+    assert shard.FileRendezvous(1, 8, directory=str(tmp_path),
+                                environ={"WORLD_SIZE": "8", "LOCAL_WORLD_SIZE": "8"}).path   # one node: default key
+    r0 = shard.FileRendezvous(0, 2, key="jobF", directory=str(tmp_path))
+    r0.fail("BenchError: no GPU")
+    r1 = shard.FileRendezvous(1, 2, key="jobF", directory=str(tmp_path), timeout=60)
+    import time
+    t0 = time.monotonic()
+    with pytest.raises(shard.RendezvousError, match="no GPU"):
+        r1.share_id()
+    assert time.monotonic() - t0 < 5
+    assert shard.FileRendezvous(0, 2, key="t", directory=str(tmp_path), environ={"PEKF_RDZV_TIMEOUT_S": "7"}).timeout == 7
