@@ -504,7 +504,10 @@ def main(argv=None):
         return _main(argv)
     except (_lib.CommTimeoutError, _lib.PekfError) as e:
         if isinstance(e, _lib.CommTimeoutError) or e.status == _lib.PEKF_ERR_COMM:
-            raise BenchError("collective failed: %s" % e)
+            # an abandoned RCCL init thread (or an aborted communicator) may still hold RCCL's locks, so
+            # leave without the interpreter's and the runtimes' exit handlers
+            print("[bench] error: collective failed: %s" % e, file=sys.stderr, flush=True)
+            os._exit(2)
         raise
     except TimeoutError as e:   # FileRendezvous: no RCCL id from rank 0 within PEKF_RDZV_TIMEOUT_S
         raise BenchError(str(e))

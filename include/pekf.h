@@ -344,12 +344,11 @@ int pekf_synth_dev(int64_t batch, int64_t window, int64_t first_filter, uint32_t
 typedef struct pekf_comm pekf_comm;
 int pekf_comm_version(int *version); /* RCCL's version code, e.g. 22707 */
 int pekf_comm_unique_id(void *id /* PEKF_COMM_ID_BYTES */);
-/* Communicator creation has a deadline: RCCL's non-blocking init (ncclCommInitRankConfig with
- * blocking = 0, rccl.h:204) polled with ncclCommGetAsyncError (rccl.h:362).  If the other ranks do not
- * all join within PEKF_COMM_TIMEOUT_S seconds (environment; default 300), the half-made communicator
- * is aborted (ncclCommAbort, rccl.h:271) and the call returns PEKF_ERR_TIMEOUT, so a rank that died
- * before joining fails the job instead of hanging it.  The communicator stays non-blocking: every
- * call below settles RCCL's ncclInProgress before it returns. */
+/* Communicator creation has a deadline: ncclCommInitRank (rccl.h) runs on a helper thread and the call
+ * waits for it at most PEKF_COMM_TIMEOUT_S seconds (environment; default 300).  If the other ranks do not
+ * all join by then it returns PEKF_ERR_TIMEOUT, so a rank that died before joining fails the job instead
+ * of hanging it; the abandoned helper stays blocked inside RCCL until the process exits (exit soon).
+ * (RCCL 2.27's non-blocking ncclCommInitRankConfig still blocks the caller while a rank is missing.) */
 int pekf_comm_init(const void *id, int nranks, int rank, pekf_comm **out);
 /* The same with an explicit deadline in seconds (<= 0: wait forever, the blocking behaviour). */
 int pekf_comm_init_timeout(const void *id, int nranks, int rank, double timeout_s, pekf_comm **out);

@@ -11,13 +11,14 @@
 // one PyTorch-ROCm bundles) the loader hands back that same library, so there is one RCCL and
 // one HIP runtime per process.
 //
-// Deadlines: a communicator is created non-blocking (ncclCommInitRankConfig, blocking = 0) and polled
-// against PEKF_COMM_TIMEOUT_S, and pekf_comm_wait drains a stream of collectives against a deadline;
-// on expiry the communicator is aborted (ncclCommAbort), so a rank that never joins or dies mid-run
-// ends the job with PEKF_ERR_TIMEOUT instead of leaving every other rank blocked inside RCCL.
+// Deadlines: communicator creation waits for the (blocking) ncclCommInitRank on a helper thread for at
+// most PEKF_COMM_TIMEOUT_S, and pekf_comm_wait drains a stream of collectives against a deadline,
+// aborting the communicator (ncclCommAbort) on expiry, so a rank that never joins or dies mid-run ends
+// the job with PEKF_ERR_TIMEOUT instead of leaving every other rank blocked inside RCCL.
 #include <dlfcn.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -44,7 +45,6 @@ struct Rccl {
     decltype(&::ncclGroupEnd) group_end = nullptr;
     decltype(&::ncclGetErrorString) error_string = nullptr;
     decltype(&::ncclGetVersion) get_version = nullptr;
-    decltype(&::ncclCommInitRankConfig) init_rank_config = nullptr;  // optional: deadline-aware init
     decltype(&::ncclCommGetAsyncError) async_error = nullptr;
     decltype(&::ncclCommAbort) abort = nullptr;
     char why[256] = "";
@@ -83,7 +83,7 @@ Rccl &rccl() {
         sym(r.async_error, "ncclCommGetAsyncError");
         sym(r.abort, "ncclCommAbort");
         r.ok = all;
-        r.init_rank_config = reinterpret_cast<decltype(r.init_rank_config)>(dlsym(h, "ncclCommInitRankConfig"));
+
     });
     return r;
 }
@@ -122,6 +122,23 @@ double env_timeout_s() {
 
 double deadline_after(double timeout_s) { return timeout_s > 0 ? now_s() + timeout_s : 0.0; }
 
+// PEKF_COMM_DEBUG=1: a stderr line per step of communicator creation / teardown (diagnosing hangs)
+bool comm_debug() {
+    static const bool on = [] {
+        const char *v = getenv("PEKF_COMM_DEBUG");
+        return v && *v && *v != '0';
+    }();
+    return on;
+}
+#define PEKF_COMM_TRACE(...)                                                          \
+    do {                                                                              \
+        if (comm_debug()) {                                                           \
+            fprintf(stderr, "[pekf_comm %.3f] ", now_s());                            \
+            fprintf(stderr, __VA_ARGS__);                                             \
+            fputc('\n', stderr);                                                      \
+        }                                                                             \
+    } while (0)
+
 // Polls a non-blocking communicator until RCCL has finished the call in progress on it.
 // Returns PEKF_OK, the RCCL error, or PEKF_ERR_TIMEOUT (*expired set) at the deadline (0 = none).
 int settle(ncclComm_t nc, double deadline, const char *what, bool *expired) {
@@ -134,6 +151,7 @@ int settle(ncclComm_t nc, double deadline, const char *what, bool *expired) {
         if (st != ncclInProgress) return nccl_fail(st, what);
         if (deadline > 0 && now_s() > deadline) {
             *expired = true;
+            PEKF_COMM_TRACE("%s: deadline passed", what);
             return PEKF_ERR_TIMEOUT;
         }
         std::this_thread::sleep_for(std::chrono::microseconds(500));
@@ -205,34 +223,57 @@ int pekf_comm_init_timeout(const void *id, int nranks, int rank, double timeout_
     PEKF_HIP(hipGetDevice(&dev));
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
-    ncclComm_t nc = nullptr;
     Rccl &r = rccl();
-    if (timeout_s <= 0 || !r.init_rank_config) {
+    if (timeout_s <= 0) {
+        ncclComm_t nc = nullptr;
         PEKF_NCCL(r.init_rank(&nc, nranks, u, rank));  // collective over the nranks processes, no deadline
         *out = new pekf_comm{nc, nranks, rank, dev, 0.0};
         return PEKF_OK;
     }
-    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-    cfg.blocking = 0;  // returns at once (ncclInProgress); completion is polled below
-    const double deadline = deadline_after(timeout_s);
-    const ncclResult_t e = r.init_rank_config(&nc, nranks, u, rank, &cfg);
-    if (e != ncclSuccess && e != ncclInProgress) {
-        if (nc) (void)r.abort(nc);
-        return nccl_fail(e, "ncclCommInitRankConfig");
+    // RCCL 2.27's "non-blocking" init (ncclCommInitRankConfig, blocking = 0) still waits in the calling
+    // thread for every rank to reach the bootstrap root (measured on the box: it never returned with a
+    // rank missing, scripts/comm_timeout_probe.py), so the deadline is kept here instead: the blocking
+    // init runs on a helper thread and this thread waits for it until the deadline.  On expiry the
+    // helper is abandoned -- it stays blocked inside RCCL until the process exits, and if the missing
+    // rank turns up after all it aborts the communicator it gets -- and PEKF_ERR_TIMEOUT is returned.
+    struct Job {
+        std::mutex m;
+        std::condition_variable cv;
+        bool done = false, abandoned = false;
+        ncclResult_t res = ncclSuccess;
+        ncclComm_t nc = nullptr;
+    };
+    auto job = std::make_shared<Job>();
+    PEKF_COMM_TRACE("rank %d/%d on device %d: ncclCommInitRank on a helper thread (deadline %.0f s)", rank, nranks,
+                    dev, timeout_s);
+    std::thread([job, nranks, u, rank, dev] {
+        ncclComm_t nc = nullptr;
+        ncclResult_t res = ncclSuccess;
+        if (hipSetDevice(dev) != hipSuccess) res = ncclUnhandledCudaError;
+        else res = rccl().init_rank(&nc, nranks, u, rank);
+        std::lock_guard<std::mutex> g(job->m);
+        if (job->abandoned) {
+            if (nc) (void)rccl().abort(nc);
+            return;
+        }
+        job->res = res;
+        job->nc = nc;
+        job->done = true;
+        job->cv.notify_all();
+    }).detach();
+    std::unique_lock<std::mutex> lk(job->m);
+    const bool finished = job->cv.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return job->done; });
+    if (!finished) {
+        job->abandoned = true;
+        PEKF_COMM_TRACE("rank %d/%d: deadline passed; init abandoned", rank, nranks);
+        return set_error(PEKF_ERR_TIMEOUT,
+                         "RCCL communicator init (ncclCommInitRank, rank %d of %d, device %d): not all %d ranks "
+                         "joined within %.0f s (PEKF_COMM_TIMEOUT_S); init abandoned",
+                         rank, nranks, dev, nranks, timeout_s);
     }
-    if (!nc) return set_error(PEKF_ERR_COMM, "ncclCommInitRankConfig returned no communicator");
-    bool expired = false;
-    const int st = settle(nc, deadline, "ncclCommInitRankConfig", &expired);
-    if (st != PEKF_OK) {
-        (void)r.abort(nc);
-        if (expired)
-            return set_error(PEKF_ERR_TIMEOUT,
-                             "RCCL communicator init (ncclCommInitRankConfig, rank %d of %d, device %d): not all %d "
-                             "ranks joined within %.0f s (PEKF_COMM_TIMEOUT_S); communicator aborted",
-                             rank, nranks, dev, nranks, timeout_s);
-        return st;
-    }
-    *out = new pekf_comm{nc, nranks, rank, dev, timeout_s};
+    PEKF_COMM_TRACE("rank %d/%d: ncclCommInitRank returned %d", rank, nranks, (int)job->res);
+    if (job->res != ncclSuccess) return nccl_fail(job->res, "ncclCommInitRank");
+    *out = new pekf_comm{job->nc, nranks, rank, dev, timeout_s};
     return PEKF_OK;
 }
 

@@ -156,9 +156,9 @@ def test_config4_rank7_shard_on_one_gpu():
 
 @pytest.mark.gpu
 def test_missing_rank_fails_within_the_comm_deadline():
-    """A 2-rank job whose rank 1 never starts: rank 0's RCCL communicator creation (non-blocking
-    ncclCommInitRankConfig polled against PEKF_COMM_TIMEOUT_S) gives up, aborts the communicator and
-    bench.py exits 2 with a message naming the init -- instead of blocking inside RCCL forever."""
+    """A 2-rank job whose rank 1 never starts: rank 0's RCCL communicator creation (ncclCommInitRank on a
+    helper thread, waited for until PEKF_COMM_TIMEOUT_S) gives up and bench.py exits 2 with a message
+    naming the init -- instead of blocking inside RCCL forever."""
     import time
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     env.update(RANK="0", WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29577",
@@ -170,6 +170,6 @@ def test_missing_rank_fails_within_the_comm_deadline():
     wall = time.monotonic() - t0
     print("missing rank: exit %d after %.1f s; %s" % (out.returncode, wall, out.stderr.strip().splitlines()[-1]))
     assert out.returncode == 2, out.stderr[-3000:]
-    assert "ncclCommInitRankConfig" in out.stderr and "20 s" in out.stderr
+    assert "ncclCommInitRank" in out.stderr and "within 20 s" in out.stderr
     assert out.stdout.strip() == ""
     assert wall < 60

@@ -81,3 +81,28 @@ def test_multi_device_ekf_equals_single_batch(eng):
     X, _ = f.get_state()
     assert np.array_equal(got, X)
     assert np.allclose(np.linalg.norm(got, axis=1), 1.0, atol=1e-12)
+
+
+def test_comm_wait_deadline_aborts(eng):
+    """pekf_comm_wait drains a stream against a deadline: on a stream still busy when it passes (here a
+    long fused launch standing in for a collective a dead peer never completes) it aborts the
+    communicator and raises CommTimeoutError; a drained stream returns at once."""
+    import time
+
+    from poseestimationkf_amd import shard
+    from poseestimationkf_amd._lib import CommTimeoutError, PekfError
+    c = shard.Communicator(shard.Communicator.unique_id(), 1, 0)
+    B = 1 << 18
+    win = eng.IMUWindow(B, 64).synthesize(seed=synth.DEFAULT_SEED)
+    f = eng.BatchedEKF(B)
+    s = eng.Stream()
+    c.wait(s.handle, timeout=5)                      # idle stream: returns
+    f.run_async(win, 20000, 0, s.handle)             # ~60 ms of work
+    t0 = time.monotonic()
+    with pytest.raises(CommTimeoutError, match="did not complete within"):
+        c.wait(s.handle, timeout=0.005)
+    assert time.monotonic() - t0 < 0.05
+    with pytest.raises(PekfError, match="aborted"):
+        c.allreduce_max(f.X.ptr, 1, s.handle)       # the aborted communicator refuses further work
+    s.sync()
+    c.close()                                        # an aborted communicator only frees
