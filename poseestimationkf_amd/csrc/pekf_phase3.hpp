@@ -75,6 +75,11 @@ struct Phase3 {
     F3 acc0, mag0;
     bool acc0_mean, mag0_mean;  // acc_0 / mag_0 is still the phase-2 mean
     double t_acc0, t_mag0, prev_t, t;
+    // The latest acc / mag sample and its time.  The Parser's acc_1 / mag_1 is always the latest sample
+    // while it is set (it is written by every sample after the gyro, and nothing else moves until the
+    // record completes or the next gyro shifts it to acc_0 / mag_0), so it is not held separately: each
+    // event updates the latest sample once and acc_0 / mag_0 copy it when the Parser would, 10 VALU
+    // per event fewer than moving acc_1 / mag_1 and acc_0 / mag_0 through two selects each.
     F3 acc1, mag1;
     F3 gyro;
     double t_acc1, t_mag1, t_gyro;
@@ -140,10 +145,11 @@ struct Phase3 {
         const bool gs = gyro_set;
         const F3 v = {v4.x, v4.y, v4.z};
         const bool wA1 = isA && gs, wM1 = isM && gs;
-        acc1 = sel(wA1, v, acc1);
-        t_acc1 = wA1 ? t : t_acc1;
-        mag1 = sel(wM1, v, mag1);
-        t_mag1 = wM1 ? t : t_mag1;
+        // acc1 / mag1: the latest sample (equal to the Parser's acc_1 / mag_1 whenever that is set)
+        acc1 = sel(isA, v, acc1);
+        t_acc1 = isA ? t : t_acc1;
+        mag1 = sel(isM, v, mag1);
+        t_mag1 = isM ? t : t_mag1;
         const bool a1s = wA1 || (acc1_set && !(isG && gs)), m1s = wM1 || (mag1_set && !(isG && gs));
         const bool sA = isG && gs && acc1_set, sM = isG && gs && mag1_set;  // gyro shift
         // ExecuteKalmanFilter (Parser.cpp:229-257) once acc_1 and mag_1 are both set: record its
@@ -158,14 +164,14 @@ struct Phase3 {
             on_done(r);
             prev_t = t_gyro;
         }
-        const bool wA0 = isA && !gs, wM0 = isM && !gs;
-        const bool cA = sA || done, cM = sM || done;  // acc_0 <- acc_1 (shift or after a record)
-        acc0 = sel(wA0, v, sel(cA, acc1, acc0));
-        acc0_mean = acc0_mean && !wA0 && !cA;
-        t_acc0 = wA0 ? t : (cA ? t_acc1 : t_acc0);
-        mag0 = sel(wM0, v, sel(cM, mag1, mag0));
-        mag0_mean = mag0_mean && !wM0 && !cM;
-        t_mag0 = wM0 ? t : (cM ? t_mag1 : t_mag0);
+        // acc_0 <- the sample before any gyro (then acc1 = v), or acc_1 on a shift or after a record
+        const bool cA = (isA && !gs) || sA || done, cM = (isM && !gs) || sM || done;
+        acc0 = sel(cA, acc1, acc0);
+        acc0_mean = acc0_mean && !cA;
+        t_acc0 = cA ? t_acc1 : t_acc0;
+        mag0 = sel(cM, mag1, mag0);
+        mag0_mean = mag0_mean && !cM;
+        t_mag0 = cM ? t_mag1 : t_mag0;
         gyro = sel(isG, v, gyro);
         t_gyro = isG ? t : t_gyro;
         gyro_set = (gs || isG) && !done;
