@@ -202,8 +202,14 @@ struct Phase3 {
         // division taken as one reciprocal.  Timestamps are integer ns held in doubles (exact below
         // 2^53), so t3 - t1 and t2 - t1 are the exact differences (double)t3 - (double)t1 gives.
         const double fa = q.an * recip<true>(q.ad), fm = q.mn * recip<true>(q.md);
-        const V3 a0 = sel(q.acc0_mean, mean_acc, widen(q.acc0)), a1 = widen(q.acc1);
-        const V3 m0 = sel(q.mag0_mean, mean_mag, widen(q.mag0)), m1 = widen(q.mag1);
+        V3 a0 = widen(q.acc0), m0 = widen(q.mag0);
+        const V3 a1 = widen(q.acc1), m1 = widen(q.mag1);
+        // acc_0 / mag_0 can still be the phase-2 mean only up to a lane's first record, so the wave
+        // selects it behind a wave-uniform test that is false for all but its first few emits
+        if (__builtin_expect(__any(q.acc0_mean || q.mag0_mean), 0)) {
+            a0 = sel(q.acc0_mean, mean_acc, a0);
+            m0 = sel(q.mag0_mean, mean_mag, m0);
+        }
         const V3 a = normalised({(a1.x - a0.x) * fa + a0.x, (a1.y - a0.y) * fa + a0.y, (a1.z - a0.z) * fa + a0.z});
         const V3 m = normalised({(m1.x - m0.x) * fm + m0.x, (m1.y - m0.y) * fm + m0.y, (m1.z - m0.z) * fm + m0.z});
         lpf_mag = {alpha * m.x + beta * lpf_mag.x, alpha * m.y + beta * lpf_mag.y, alpha * m.z + beta * lpf_mag.z};
