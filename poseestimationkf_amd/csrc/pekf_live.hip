@@ -229,19 +229,22 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
 
     // Events stream through a register ring of kRing rows loaded kRing events ahead (the loop is
     // unrolled by kRing so every ring index is static; rows past the end are clamped to the last one).
+    // 32-bit event counters (n_events < 2^30, checked on the host): the wave-uniform bounds tests are
+    // then scalar compares, where 64-bit ones took a VALU move and compare each, twice per event.
     const uint32_t lane = (uint32_t)b;
-    auto load = [&](int64_t e) -> float4 {
-        const int64_t row = e < n_events ? e : n_events - 1;
-        return (ev + row * batch)[lane];
+    const int32_t n_ev = (int32_t)n_events;
+    auto load = [&](int32_t e) -> float4 {
+        const int32_t row = e < n_ev ? e : n_ev - 1;
+        return (ev + (int64_t)row * batch)[lane];
     };
-    if (n_events > 0) {
+    if (n_ev > 0) {
         float4 ring[kRing];
 #pragma unroll
         for (int k = 0; k < kRing; ++k) ring[k] = load(k);
-        for (int64_t e0 = 0; e0 < n_events; e0 += kRing) {
+        for (int32_t e0 = 0; e0 < n_ev; e0 += kRing) {
 #pragma unroll
             for (int k = 0; k < kRing; ++k) {
-                if (e0 + k >= n_events) break;  // uniform
+                if (e0 + k >= n_ev) break;  // uniform
                 const float4 v4 = ring[k];
                 ring[k] = load(e0 + k + kRing);
                 on_event(v4);
@@ -250,7 +253,7 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
             flush();  // a record completed in a trailing partial block (nothing pending after a full one)
             // wave-uniform: a step while some lane could overflow in the next block, then one more if
             // a quorum of lanes has a record; after the last event until every queue is empty
-            const bool last = e0 + kRing >= n_events;
+            const bool last = e0 + kRing >= n_ev;
             for (;;) {
                 const uint64_t queued = __ballot(queue.n > 0);
                 if (queued == 0) break;
@@ -276,6 +279,7 @@ extern "C" int pekf_live_ext_dev(int64_t batch, int64_t n_events, const void *ev
     PEKF_CHECK_ARG((flags & ~PEKF_EV_TIME_EVENTS) == 0, "unknown flags");
     if (batch == 0) return PEKF_OK;
     PEKF_CHECK_ARG(batch < ((int64_t)1 << 28), "batch must be < 2^28 filters per launch");
+    PEKF_CHECK_ARG(n_events < ((int64_t)1 << 30), "n_events must be < 2^30 per launch");
     PEKF_CHECK_ARG(ev_planes && init && t_init && X && P && counts && refs, "null pointer");
     PEKF_CHECK_ARG((uintptr_t)ev_planes % 16 == 0, "misaligned event planes");
     PEKF_CHECK_ARG(r > 0.0, "r must be > 0 (S = P- + rI must be SPD)");
