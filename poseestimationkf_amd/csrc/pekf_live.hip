@@ -237,29 +237,42 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
         const int32_t row = e < n_ev ? e : n_ev - 1;
         return (ev + (int64_t)row * batch)[lane];
     };
+    // wave-uniform: a step while some lane could overflow in the next block, then one more if a quorum
+    // of lanes has a record; after the last event until every queue is empty
+    auto want_step = [&](bool last) {
+        const uint64_t queued = __ballot(queue.n > 0);
+        return queued != 0 && (last || __any(queue.n > kQueue - kPush) || __popcll(queued) >= kQuorum);
+    };
+    auto steps = [&](bool last) {
+        // tested before the loop, so a block that runs no step does not pass the loop's header
+        if (want_step(last)) {
+            do {
+                filter_step();
+            } while (want_step(last));
+        }
+    };
     if (n_ev > 0) {
         float4 ring[kRing];
 #pragma unroll
         for (int k = 0; k < kRing; ++k) ring[k] = load(k);
+        // No exit inside the unrolled body (one per event made the compiler copy the ring on the back
+        // edge, behind a wait for the loads just issued): the last, partial block is padded with null
+        // events -- a zero-step time event {0, 0, 0, word 3} moves no state, with or without TE -- so
+        // every block runs whole, and nothing is pending after a whole block.
         for (int32_t e0 = 0; e0 < n_ev; e0 += kRing) {
+            if (e0 + kRing > n_ev) {  // uniform, once per launch
+#pragma unroll
+                for (int k = 0; k < kRing; ++k)
+                    if (e0 + k >= n_ev) ring[k] = make_float4(0.f, 0.f, 0.f, __uint_as_float(PEKF_EV_TIME));
+            }
 #pragma unroll
             for (int k = 0; k < kRing; ++k) {
-                if (e0 + k >= n_ev) break;  // uniform
                 const float4 v4 = ring[k];
                 ring[k] = load(e0 + k + kRing);
                 on_event(v4);
                 if ((k + 1) % kFlush == 0) flush();
             }
-            flush();  // a record completed in a trailing partial block (nothing pending after a full one)
-            // wave-uniform: a step while some lane could overflow in the next block, then one more if
-            // a quorum of lanes has a record; after the last event until every queue is empty
-            const bool last = e0 + kRing >= n_ev;
-            for (;;) {
-                const uint64_t queued = __ballot(queue.n > 0);
-                if (queued == 0) break;
-                if (!(last || __any(queue.n > kQueue - kPush) || __popcll(queued) >= kQuorum)) break;
-                filter_step();
-            }
+            steps(e0 + kRing >= n_ev);
         }
     }
     counts[b] = applied;
