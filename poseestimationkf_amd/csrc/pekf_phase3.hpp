@@ -193,6 +193,15 @@ struct Phase3 {
         return emit(p, esc);
     }
 
+    // The low-pass step l <- alpha x + beta l (KalmanFilter.cpp:285,298), rounded as fma(beta, l, alpha x)
+    // -- the contraction the compiler chose for the expression -- but written into l's own register: the
+    // compiler's accumulating v_fmac form left the result in the product's register and copied it back
+    // (6 moves per emit).
+    __device__ __forceinline__ void lpf_step(double &l, double x) const {
+        const double ax = alpha * x;
+        asm("v_fma_f64 %0, %1, %0, %2" : "+v"(l) : "v"(beta), "v"(ax));
+    }
+
     // A captured record, in the order they complete: interpolation, normalisation, low-pass, f32
     // packing.  esc: its dt does not fit the dt word (not in [0, 2^31 - 1) ns): the word is
     // PEKF_DT_ESCAPE and the caller keeps q.dt beside the record (pekf.h).
@@ -212,8 +221,8 @@ struct Phase3 {
         }
         const V3 a = normalised({(a1.x - a0.x) * fa + a0.x, (a1.y - a0.y) * fa + a0.y, (a1.z - a0.z) * fa + a0.z});
         const V3 m = normalised({(m1.x - m0.x) * fm + m0.x, (m1.y - m0.y) * fm + m0.y, (m1.z - m0.z) * fm + m0.z});
-        lpf_mag = {alpha * m.x + beta * lpf_mag.x, alpha * m.y + beta * lpf_mag.y, alpha * m.z + beta * lpf_mag.z};
-        lpf_acc = {alpha * a.x + beta * lpf_acc.x, alpha * a.y + beta * lpf_acc.y, alpha * a.z + beta * lpf_acc.z};
+        lpf_step(lpf_mag.x, m.x); lpf_step(lpf_mag.y, m.y); lpf_step(lpf_mag.z, m.z);
+        lpf_step(lpf_acc.x, a.x); lpf_step(lpf_acc.y, a.y); lpf_step(lpf_acc.z, a.z);
         esc = !(q.dt >= 0.0 && q.dt < (double)PEKF_DT_ESCAPE);
         Rec r;
         r.gd = make_float4((float)q.gyro.x, (float)q.gyro.y, (float)q.gyro.z,
