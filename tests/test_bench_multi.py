@@ -5,7 +5,7 @@ code the driver's 8-GPU run executes:
 
 * one process over 8 devices (`bench.py --gpus 8`: shard.MultiDeviceEKF, ncclCommInitAll, one
   grouped gather per step);
-* one process per rank (`torchrun ... bench.py --gpus 2`: FileRendezvous, RCCL init, per-step
+* one process per rank (`torchrun ... bench.py --gpus 2` and `--gpus 4`: FileRendezvous, RCCL init, per-step
   gather, max-over-ranks time, per-GPU timings exchanged by one all-reduce);
 * rank 0 failing before it has an RCCL id: the other rank stops waiting and exits 2 at once.
 
@@ -120,15 +120,16 @@ def _run_ranks(tmp_path, world, n_devices_of=lambda r: 1, timeout=240):
     return codes, texts, time.monotonic() - t0
 
 
-def test_two_ranks_one_process_each(tmp_path):
-    """`torchrun --nproc-per-node 2 bench.py --gpus 2`: two processes, rank 0 prints the one line."""
-    codes, texts, _ = _run_ranks(tmp_path, 2)
-    assert codes == [0, 0], texts
+@pytest.mark.parametrize("world", [2, 4])
+def test_ranks_one_process_each(tmp_path, world):
+    """`torchrun --nproc-per-node N bench.py --gpus N`: N processes, rank 0 prints the one line."""
+    codes, texts, _ = _run_ranks(tmp_path, world)
+    assert codes == [0] * world, texts
     d = _one_line(texts[0])
-    assert texts[1].strip() == ""                                  # only rank 0 prints
-    _check_line(d, 2)
+    assert all(t.strip() == "" for t in texts[1:])                 # only rank 0 prints
+    _check_line(d, world)
     assert d["config"]["launch"].startswith("one process per GPU")
-    assert d["gather_ms_per_gpu"][0] > 0 and d["gather_ms_per_gpu"][1] > 0   # gloo gathers, host-timed
+    assert all(v > 0 for v in d["gather_ms_per_gpu"])              # gloo gathers, host-timed
 
 
 def test_rank0_failure_releases_the_other_ranks(tmp_path):
