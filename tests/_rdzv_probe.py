@@ -9,4 +9,5 @@ from poseestimationkf_amd import shard  # noqa: E402
 r, w = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 z = shard.FileRendezvous(r, w, timeout=60)
 uid = z.share_id(make_id=lambda: bytes([7]) * 128)
-print("RDZV rank=%d ok=%d torch=%d" % (r, uid == bytes([7]) * 128, "torch" in sys.modules), flush=True)
+# one write of the whole line (the ranks share the launcher's stdout)
+os.write(1, b"RDZV rank=%d ok=%d torch=%d\n" % (r, uid == bytes([7]) * 128, "torch" in sys.modules))

@@ -9,6 +9,7 @@
   as pekf_gather_dev lays them out on the root, equal a single-process run.  gloo only stands in
   for the RCCL gather (which needs GPUs: tests/test_gpu_comm.py and bench.py on the box)."""
 import os
+import re
 import socket
 import sys
 
@@ -109,7 +110,8 @@ def test_file_rendezvous_under_torchrun(tmp_path):
                           os.path.join(os.path.dirname(__file__), "_rdzv_probe.py")],
                          capture_output=True, text=True, timeout=240, env=env)
     assert out.returncode == 0, out.stderr[-2000:]
-    lines = sorted(l for l in out.stdout.splitlines() if l.startswith("RDZV"))
+    # the ranks share torchrun's stdout, so their lines may interleave: take each report wherever it is
+    lines = sorted(re.findall(r"RDZV rank=\d+ ok=\d torch=\d", out.stdout))
     assert lines == ["RDZV rank=%d ok=1 torch=0" % r for r in range(3)], out.stdout
 
 
