@@ -280,7 +280,10 @@ def c_oracle_rate(seed, missing, n_filters=64, n_rec=1000):
     t0 = time.perf_counter()
     oracle_c.run(rec)
     dt = time.perf_counter() - t0
-    return {"value": n_filters * n_rec / dt, "threads": cpu_share()["use"],
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return {"value": n_filters * n_rec / dt,
+            "threads": int(omp) if omp.isdigit() else len(os.sched_getaffinity(0)),
+            "threads_source": "OMP_NUM_THREADS" if omp.isdigit() else "OpenMP default (affinity mask)",
             "what": "C FP64 restatement (oracle/ekf_oracle.c, Jacobi SVD), OpenMP over filters"}
 
 
