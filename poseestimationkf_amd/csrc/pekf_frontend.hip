@@ -116,17 +116,28 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend_init(int64_t batch, int64
     bool kalman = false;
     int64_t t = t_start[b], t_last = t;
     // events come kInitRing rows at a time, all loads issued before the first is used (the loop body
-    // is a few adds, so without it each wave would wait out one memory latency per event); rows past
-    // the end are clamped to the last row and not processed
+    // is a few adds, so without it each wave would wait out one memory latency per event).  32-bit
+    // event counters (n_events < 2^30, checked on the host) keep the uniform bounds tests scalar; the
+    // rows past the end of the last block are null events (a zero-step time event, which phase 2 skips
+    // in both passes), so no exit sits inside the unrolled body.
     constexpr int kInitRing = 8;
-    auto row = [&](int64_t e) -> float4 { return (ev + (e < n_events ? e : n_events - 1) * batch)[lane]; };
-    for (int64_t e0 = 0; e0 < n_events; e0 += kInitRing) {
+    const int32_t n_ev = (int32_t)n_events;
+    const float4 null_ev = make_float4(0.f, 0.f, 0.f, __uint_as_float(PEKF_EV_TIME));
+    auto row = [&](int32_t e) -> float4 { return (ev + (int64_t)(e < n_ev ? e : n_ev - 1) * batch)[lane]; };
+    auto pad = [&](int32_t e0, float4 (&r)[kInitRing]) {
+        if (e0 + kInitRing > n_ev) {  // uniform: the last block only
+#pragma unroll
+            for (int k = 0; k < kInitRing; ++k)
+                if (e0 + k >= n_ev) r[k] = null_ev;
+        }
+    };
+    for (int32_t e0 = 0; e0 < n_ev; e0 += kInitRing) {
         float4 r[kInitRing];
 #pragma unroll
         for (int k = 0; k < kInitRing; ++k) r[k] = row(e0 + k);
+        pad(e0, r);
 #pragma unroll
         for (int k = 0; k < kInitRing; ++k) {
-            if (e0 + k >= n_events) break;  // uniform
             const float4 v4 = r[k];
             const uint32_t word = __float_as_uint(v4.w);
             const int ty = (int)(word & 3u);
@@ -160,14 +171,14 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend_init(int64_t batch, int64
     // second pass: the variance of the first n_avg samples of each type, in their order
     double var[3][3] = {};
     int c2[3] = {0, 0, 0};
-    for (int64_t e0 = 0; e0 < n_events; e0 += kInitRing) {
+    for (int32_t e0 = 0; e0 < n_ev; e0 += kInitRing) {
         if (c2[0] >= n_avg && c2[1] >= n_avg && c2[2] >= n_avg) break;
         float4 r[kInitRing];
 #pragma unroll
         for (int k = 0; k < kInitRing; ++k) r[k] = row(e0 + k);
+        pad(e0, r);
 #pragma unroll
         for (int k = 0; k < kInitRing; ++k) {
-            if (e0 + k >= n_events) break;  // uniform
             const float4 v4 = r[k];
             const int ty = (int)(__float_as_uint(v4.w) & 3u);
             if (ty <= 2 && c2[ty] < n_avg) {
@@ -209,6 +220,7 @@ extern "C" int pekf_frontend_init_dev(int64_t batch, int64_t n_events, const voi
                                       void *stream) {
     PEKF_CHECK_ARG(batch >= 0 && n_events >= 0, "negative size");
     PEKF_CHECK_ARG(n_avg >= 2, "n_avg must be >= 2 (the variance divides by n_avg - 1)");
+    PEKF_CHECK_ARG(n_events < ((int64_t)1 << 30), "n_events must be < 2^30 per launch");
     if (batch == 0) return PEKF_OK;
     PEKF_CHECK_ARG(ev_planes && t_start && init && t_init && ready, "null pointer");
     hipLaunchKernelGGL(k_frontend_init, dim3(grid_for(batch, kFeBlock)), dim3(kFeBlock), 0, as_stream(stream), batch,
