@@ -141,3 +141,24 @@ def test_round3_entry_points_check_their_arguments():
     st = L.pekf_filter_run_ext(None, 2, 1, 0, None, None, None, None, None, None, None)
     assert st == _lib.PEKF_ERR_INVALID and "handle" in _lib.last_error()
     assert h.value is None
+
+
+def test_round4_entry_points_check_their_arguments():
+    """The collective deadlines and the escaped-dt gyro chain validate before touching a device (CPU)."""
+    from poseestimationkf_amd import _lib
+    L = _lib.lib
+    h = ctypes.c_void_p()
+    assert L.pekf_comm_init_timeout(bytes(128), 2, 5, 10.0, ctypes.byref(h)) == _lib.PEKF_ERR_INVALID
+    assert "rank" in _lib.last_error() and not h.value
+    assert L.pekf_comm_wait(None, None, 1.0) == _lib.PEKF_ERR_INVALID and "communicator" in _lib.last_error()
+    assert L.pekf_comm_abort(None) == _lib.PEKF_OK
+    st = L.pekf_gyro_chain_ext_dev(4, 8, 4, 0, None, None, None, None, None)
+    assert st == _lib.PEKF_ERR_INVALID and "null" in _lib.last_error()
+    assert L.pekf_gyro_chain_ext_dev(0, 8, 4, 0, None, None, None, None, None) == _lib.PEKF_OK   # empty batch
+    st = L.pekf_live_ext_dev(4, 1 << 30, 16, 16, 16, 0.1, 16, 16, 1.0, 0.1, 16, 16, 0, None, None)
+    assert st == _lib.PEKF_ERR_INVALID and "2^30" in _lib.last_error()
+    st = L.pekf_frontend_init_dev(4, 1 << 30, 16, 16, 100, 16, 16, None, 16, None)
+    assert st == _lib.PEKF_ERR_INVALID and "2^30" in _lib.last_error()
+    assert _lib.PEKF_ERR_TIMEOUT == 7 and issubclass(_lib.CommTimeoutError, _lib.PekfError)
+    with pytest.raises(_lib.CommTimeoutError):
+        _lib.check(_lib.PEKF_ERR_TIMEOUT)
