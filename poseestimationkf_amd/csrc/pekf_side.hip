@@ -20,7 +20,11 @@ constexpr int kSideBlock = 256;
 // the loads past the last step read valid (unused) records and need no predicate.
 constexpr int kDepth = 8;
 
-__device__ __forceinline__ int64_t next_row(int64_t r, int64_t window) { return r + 1 == window ? 0 : r + 1; }
+// 32-bit row and step counters (window, n_steps < 2^31: checked on the host), so the wave-uniform
+// tests are scalar compares; the time loop runs whole blocks of kDepth records with no exit inside the
+// unrolled body (an exit per record made the compiler copy the ring on the back edge, behind a wait
+// for the loads just issued), then the last n_steps % kDepth records.
+__device__ __forceinline__ int32_t next_row(int32_t r, int32_t window) { return r + 1 == window ? 0 : r + 1; }
 
 // LONGDT: the window has a dt side plane dtx[window][batch] (float64 ns); a record whose dt word is
 // PEKF_DT_ESCAPE takes its dt from there, exactly as the filter does (k_run<..., LONGDT>).
@@ -32,37 +36,44 @@ __global__ __launch_bounds__(kSideBlock) void k_gyro_chain(int64_t batch, int64_
     const int64_t b = (int64_t)blockIdx.x * kSideBlock + threadIdx.x;
     if (b >= batch) return;
     const uint32_t lane = (uint32_t)b;
+    const int32_t n = (int32_t)n_steps, W = (int32_t)window;
     double x[4] = {q[4 * b], q[4 * b + 1], q[4 * b + 2], q[4 * b + 3]};
     float4 ring[kDepth];
-    int64_t pf = step0 % window;  // next row to prefetch
+    int32_t pf = (int32_t)(step0 % window);  // next row to prefetch
 #pragma unroll
     for (int k = 0; k < kDepth; ++k) {
-        ring[k] = (gd + pf * batch)[lane];
-        pf = next_row(pf, window);
+        ring[k] = (gd + (int64_t)pf * batch)[lane];
+        pf = next_row(pf, W);
     }
-    for (int64_t t0 = 0; t0 < n_steps; t0 += kDepth) {
-#pragma unroll
-        for (int k = 0; k < kDepth; ++k) {
-            const int64_t t = t0 + k;
-            if (t >= n_steps) break;
-            const float4 r = ring[k];
-            ring[k] = (gd + pf * batch)[lane];
-            pf = next_row(pf, window);
-            const double hw[3] = {0.5 * (double)r.x, 0.5 * (double)r.y, 0.5 * (double)r.z};
-            const uint32_t word = __float_as_uint(r.w) & PEKF_DT_MASK;
-            double dt_ns = (double)word;
-            if constexpr (LONGDT) {  // off the fast path: the escaped record's row, (step0 + t) % window
-                if (word == PEKF_DT_ESCAPE) dt_ns = dtx[((step0 + t) % window) * batch + b];
-            }
-            double z[4];
-            rk4_closed(x, x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3], dt_ns, hw, z);
-            x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
-            if (traj) {
-                double2 *o = reinterpret_cast<double2 *>(traj + t * batch * 4) + 2 * (int64_t)lane;
-                o[0] = make_double2(x[0], x[1]);
-                o[1] = make_double2(x[2], x[3]);
-            }
+    auto one = [&](int k, int32_t t) {
+        const float4 r = ring[k];
+        ring[k] = (gd + (int64_t)pf * batch)[lane];
+        pf = next_row(pf, W);
+        const double hw[3] = {0.5 * (double)r.x, 0.5 * (double)r.y, 0.5 * (double)r.z};
+        const uint32_t word = __float_as_uint(r.w) & PEKF_DT_MASK;
+        double dt_ns = (double)word;
+        if constexpr (LONGDT) {  // off the fast path: the escaped record's row, (step0 + t) % window
+            if (word == PEKF_DT_ESCAPE) dt_ns = dtx[((step0 + t) % window) * batch + b];
         }
+        double z[4];
+        rk4_closed(x, x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3], dt_ns, hw, z);
+        x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
+        if (traj) {
+            double2 *o = reinterpret_cast<double2 *>(traj + (int64_t)t * batch * 4) + 2 * (int64_t)lane;
+            o[0] = make_double2(x[0], x[1]);
+            o[1] = make_double2(x[2], x[3]);
+        }
+    };
+    const int32_t n_full = n - n % kDepth;
+    int32_t t0 = 0;
+    for (; t0 < n_full; t0 += kDepth) {
+#pragma unroll
+        for (int k = 0; k < kDepth; ++k) one(k, t0 + k);
+    }
+#pragma unroll
+    for (int k = 0; k < kDepth; ++k) {
+        if (t0 + k >= n) break;  // uniform
+        one(k, t0 + k);
     }
     q[4 * b] = x[0]; q[4 * b + 1] = x[1]; q[4 * b + 2] = x[2]; q[4 * b + 3] = x[3];
 }
@@ -75,6 +86,7 @@ __global__ __launch_bounds__(kSideBlock) void k_wahba_stream(int64_t batch, int6
     const int64_t b = (int64_t)blockIdx.x * kSideBlock + threadIdx.x;
     if (b >= batch) return;
     const uint32_t lane = (uint32_t)b;
+    const int32_t n = (int32_t)n_steps, W = (int32_t)window;
     Frame Wf;
     {
         const double a0[3] = {refs[6 * b + 0], refs[6 * b + 1], refs[6 * b + 2]};
@@ -84,39 +96,45 @@ __global__ __launch_bounds__(kSideBlock) void k_wahba_stream(int64_t batch, int6
     const double sg = wahba_sign(ka, km);
     float4 ra[kDepth];
     float2 rm[kDepth];
-    int64_t pf = step0 % window;
+    int32_t pf = (int32_t)(step0 % window);
 #pragma unroll
     for (int k = 0; k < kDepth; ++k) {
-        ra[k] = (am + pf * batch)[lane];
-        rm[k] = (my + pf * batch)[lane];
-        pf = next_row(pf, window);
+        ra[k] = (am + (int64_t)pf * batch)[lane];
+        rm[k] = (my + (int64_t)pf * batch)[lane];
+        pf = next_row(pf, W);
     }
-    for (int64_t t0 = 0; t0 < n_steps; t0 += kDepth) {
-#pragma unroll
-        for (int k = 0; k < kDepth; ++k) {
-            const int64_t t = t0 + k;
-            if (t >= n_steps) break;
-            const float4 a = ra[k];
-            const float2 m = rm[k];
-            ra[k] = (am + pf * batch)[lane];
-            rm[k] = (my + pf * batch)[lane];
-            pf = next_row(pf, window);
-            const double acc[3] = {a.x, a.y, a.z}, mag[3] = {a.w, m.x, m.y};
-            Frame Vf;
-            make_frame<true>(acc, mag, Vf, sg);
-            double R[9], y[4];
-            wahba_rotation<true>(Wf, Vf, ka, km, R);
-            if (frame_degenerate(Vf)) {  // a zero sample or acc parallel to mag: B has rank 1 (pekf_math.hpp)
-                const double ra[3] = {a.x, a.y, a.z}, rm[3] = {a.w, m.x, m.y};  // from the f32 record again
-                double a0[3], m0[3];
-                frame_pair(Wf, a0, m0);
-                wahba_current_rank1<1>(a0, m0, ra, rm, ka, km, R);
-            }
-            rotm_to_quat_fast(R, y);  // keeps the reference's branch / sign convention
-            double2 *o = reinterpret_cast<double2 *>(out + t * batch * 4) + 2 * (int64_t)lane;
-            o[0] = make_double2(y[0], y[1]);
-            o[1] = make_double2(y[2], y[3]);
+    auto one = [&](int k, int32_t t) {
+        const float4 a = ra[k];
+        const float2 m = rm[k];
+        ra[k] = (am + (int64_t)pf * batch)[lane];
+        rm[k] = (my + (int64_t)pf * batch)[lane];
+        pf = next_row(pf, W);
+        const double acc[3] = {a.x, a.y, a.z}, mag[3] = {a.w, m.x, m.y};
+        Frame Vf;
+        make_frame<true>(acc, mag, Vf, sg);
+        double R[9], y[4];
+        wahba_rotation<true>(Wf, Vf, ka, km, R);
+        if (frame_degenerate(Vf)) {  // a zero sample or acc parallel to mag: B has rank 1 (pekf_math.hpp)
+            const double sa[3] = {a.x, a.y, a.z}, sm[3] = {a.w, m.x, m.y};  // from the f32 record again
+            double a0[3], m0[3];
+            frame_pair(Wf, a0, m0);
+            wahba_current_rank1<1>(a0, m0, sa, sm, ka, km, R);
         }
+        rotm_to_quat_fast(R, y);  // keeps the reference's branch / sign convention
+        double2 *o = reinterpret_cast<double2 *>(out + (int64_t)t * batch * 4) + 2 * (int64_t)lane;
+        o[0] = make_double2(y[0], y[1]);
+        o[1] = make_double2(y[2], y[3]);
+    };
+    const int32_t n_full = n - n % kDepth;
+    int32_t t0 = 0;
+    for (; t0 < n_full; t0 += kDepth) {
+#pragma unroll
+        for (int k = 0; k < kDepth; ++k) one(k, t0 + k);
+    }
+#pragma unroll
+    for (int k = 0; k < kDepth; ++k) {
+        if (t0 + k >= n) break;  // uniform
+        one(k, t0 + k);
     }
 }
 
@@ -162,6 +180,7 @@ int pekf_gyro_chain_ext_dev(int64_t batch, int64_t n_steps, int64_t window, int6
     PEKF_CHECK_ARG(window > 0 && step0 >= 0, "window must be > 0 and step0 >= 0");
     PEKF_CHECK_ARG(batch < ((int64_t)1 << 28), "batch must be < 2^28 filters per launch");
     PEKF_CHECK_ARG(plane_gd && q_gyro, "null pointer");
+    PEKF_CHECK_ARG(n_steps < ((int64_t)1 << 31) && window < ((int64_t)1 << 31), "n_steps and window must be < 2^31");
     const dim3 grid(grid_for(batch, kSideBlock)), block(kSideBlock);
     const float4 *gd = static_cast<const float4 *>(plane_gd);
     if (dt_ext)
@@ -186,6 +205,7 @@ int pekf_wahba_stream_dev(int64_t batch, int64_t n_steps, int64_t window, int64_
     PEKF_CHECK_ARG(window > 0 && step0 >= 0, "window must be > 0 and step0 >= 0");
     PEKF_CHECK_ARG(batch < ((int64_t)1 << 28), "batch must be < 2^28 filters per launch");
     PEKF_CHECK_ARG(plane_am && plane_my && refs && out, "null pointer");
+    PEKF_CHECK_ARG(n_steps < ((int64_t)1 << 31) && window < ((int64_t)1 << 31), "n_steps and window must be < 2^31");
     hipLaunchKernelGGL(k_wahba_stream, dim3(grid_for(batch, kSideBlock)), dim3(kSideBlock), 0,
                        as_stream(stream), batch, n_steps, window, step0,
                        static_cast<const float4 *>(plane_am), static_cast<const float2 *>(plane_my),

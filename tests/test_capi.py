@@ -154,6 +154,8 @@ def test_round4_entry_points_check_their_arguments():
     assert L.pekf_comm_abort(None) == _lib.PEKF_OK
     st = L.pekf_gyro_chain_ext_dev(4, 8, 4, 0, None, None, None, None, None)
     assert st == _lib.PEKF_ERR_INVALID and "null" in _lib.last_error()
+    st = L.pekf_gyro_chain_ext_dev(4, 1 << 31, 4, 0, 16, None, 16, None, None)
+    assert st == _lib.PEKF_ERR_INVALID and "2^31" in _lib.last_error()
     assert L.pekf_gyro_chain_ext_dev(0, 8, 4, 0, None, None, None, None, None) == _lib.PEKF_OK   # empty batch
     st = L.pekf_live_ext_dev(4, 1 << 30, 16, 16, 16, 0.1, 16, 16, 1.0, 0.1, 16, 16, 0, None, None)
     assert st == _lib.PEKF_ERR_INVALID and "2^30" in _lib.last_error()
