@@ -41,7 +41,8 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
 #pragma unroll
         for (int k = 0; k < 6; ++k) refs[6 * b + k] = rf[k];
     }
-    int64_t r = 0;
+    int32_t r = 0;  // this filter's records so far (r_max < 2^31, checked on the host)
+    const int32_t rmax = (int32_t)r_max;
     int bad = 0;
     // the pending record (Phase3::pend) is emitted every kFlush events; a lane never has two
     constexpr int kFlush = 3;
@@ -51,8 +52,8 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
         const Rec rc = fe.emit(esc);
         if (!ready) return;
         if (esc) bad |= dtx ? 4 : 1;
-        if (r < r_max) {
-            const int64_t o = r * batch + b;
+        if (r < rmax) {
+            const int64_t o = (int64_t)r * batch + b;
             gd[o] = rc.gd;
             am[o] = rc.am;
             my[o] = rc.my;
@@ -63,33 +64,40 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
         ++r;
     };
 
-    // Events stream through a register ring of kRing records loaded kRing events ahead (the
-    // loop is unrolled by kRing so every ring index is static; the row is clamped to the last
-    // event, so the loads past the end read a valid row and need no predicate).
+    // Events stream through a register ring of kRing records loaded kRing events ahead (the loop is
+    // unrolled by kRing so every ring index is static; the row is clamped to the last event, so the
+    // loads past the end read a valid row and need no predicate).  32-bit event counters (n_events <
+    // 2^30, checked on the host) keep the uniform tests scalar, and the last block is padded with null
+    // events (a zero-step time event moves no state) so no exit sits inside the unrolled body; nothing
+    // is pending after a whole block.
     const uint32_t lane = (uint32_t)b;
-    auto load = [&](int64_t e) -> float4 {
-        const int64_t row = e < n_events ? e : n_events - 1;
-        return (ev + row * batch)[lane];
+    const int32_t n_ev = (int32_t)n_events;
+    auto load = [&](int32_t e) -> float4 {
+        const int32_t row = e < n_ev ? e : n_ev - 1;
+        return (ev + (int64_t)row * batch)[lane];
     };
-    if (n_events > 0) {
+    if (n_ev > 0) {
         constexpr int kRing = PEKF_FE_RING;  // events in flight per lane (a multiple of kFlush)
         static_assert(kRing % kFlush == 0, "the ring depth must be a multiple of the flush period");
         float4 ring[kRing];
 #pragma unroll
         for (int k = 0; k < kRing; ++k) ring[k] = load(k);
-        for (int64_t e0 = 0; e0 < n_events; e0 += kRing) {
+        for (int32_t e0 = 0; e0 < n_ev; e0 += kRing) {
+            if (e0 + kRing > n_ev) {  // uniform, once per launch
+#pragma unroll
+                for (int k = 0; k < kRing; ++k)
+                    if (e0 + k >= n_ev) ring[k] = make_float4(0.f, 0.f, 0.f, __uint_as_float(PEKF_EV_TIME));
+            }
 #pragma unroll
             for (int k = 0; k < kRing; ++k) {
-                if (e0 + k >= n_events) break;  // uniform
                 const float4 v4 = ring[k];
                 ring[k] = load(e0 + k + kRing);
                 fe.event<TE>(v4);
                 if ((k + 1) % kFlush == 0) flush();
             }
         }
-        flush();  // a record completed in a trailing partial group
     }
-    counts[b] = (int32_t)(r < r_max ? r : r_max);
+    counts[b] = r < rmax ? r : rmax;
     if (bad && err) atomicOr(err, bad);
 }
 
@@ -237,6 +245,8 @@ extern "C" int pekf_frontend_ext_dev(int64_t batch, int64_t n_events, const void
     PEKF_CHECK_ARG(batch >= 0 && n_events >= 0 && r_max >= 0, "negative size");
     PEKF_CHECK_ARG((flags & ~PEKF_EV_TIME_EVENTS) == 0, "unknown flags");
     if (batch == 0) return PEKF_OK;
+    PEKF_CHECK_ARG(n_events < ((int64_t)1 << 30), "n_events must be < 2^30 per launch");
+    PEKF_CHECK_ARG(r_max < ((int64_t)1 << 31), "r_max must be < 2^31");
     PEKF_CHECK_ARG(ev_planes && init && t_init && plane_gd && plane_am && plane_my && counts && refs,
                    "null pointer");
     const auto *ev = static_cast<const float4 *>(ev_planes);
