@@ -47,10 +47,11 @@ def _same(a, b):
         assert np.array_equal(u, v, equal_nan=True)
 
 
-@pytest.mark.parametrize("K,E,seed", [(1000, 1500, 21), (64, 37, 22), (4096, 300, 23)])
+@pytest.mark.parametrize("K,E,seed", [(1000, 1500, 21), (64, 37, 22), (4096, 300, 23), (512, 200, 27)])
 def test_live_equals_split_pipeline_bit_for_bit(eng, K, E, seed):
-    """Ragged record counts, a partial last wave (K = 1000), an event count that is no multiple of the
-    ring (E = 37) and short streams where the end-of-stream drain does most of the steps."""
+    """Ragged record counts, a partial last wave (K = 1000), event counts that are no multiple of the
+    3-event ring (E = 37, 200: the last block padded with 2 or 1 null events) and short streams where the
+    end-of-stream drain does most of the steps."""
     ev = synth.generate_events(np.arange(K), E, seed=seed)
     fused, split = _fused(eng, ev, K), _split(eng, ev, K)
     assert fused[2].min() >= 0 and fused[2].max() > 0
