@@ -165,14 +165,14 @@ class FileRendezvous:
     shared by every rank, e.g. a network file system when ranks span nodes).  A job that spans nodes
     must name its key: the default (the local parent) differs between nodes, so it is refused there.
     If rank 0 fails before it has an id, `fail(msg)` publishes the failure and the other ranks raise
-    at once instead of waiting out `timeout` (PEKF_RDZV_TIMEOUT_S, default 600 s).
+    at once instead of waiting out `timeout` (PEKF_RDZV_TIMEOUT_S, default 300 s, as PEKF_COMM_TIMEOUT_S).
     RCCL's communicator creation is itself collective, so after it returns on rank 0 every rank
     has read the file and `done()` removes it."""
 
     def __init__(self, rank, world, key=None, directory=None, timeout=None, environ=None):
         env = os.environ if environ is None else environ
         if timeout is None:
-            timeout = float(env.get("PEKF_RDZV_TIMEOUT_S", "600"))
+            timeout = float(env.get("PEKF_RDZV_TIMEOUT_S", "300"))
         self.rank, self.world, self.timeout = int(rank), int(world), float(timeout)
         if not 0 <= self.rank < self.world:
             raise ValueError("need 0 <= rank < world")
