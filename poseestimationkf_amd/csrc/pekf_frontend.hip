@@ -14,14 +14,42 @@
 namespace pekf {
 
 constexpr int kFeBlock = 256;
+// k_frontend's per-wave LDS record queue (profiles/r4/frontend_stage/: 8-16 rows x thresholds 52-60
+// swept; 10 rows = 25.6 KB per wave, 6 waves per CU): rows held (0: every record stored where it is
+// made), and the queue's oldest row is written once at most 64 - THR ready lanes still lack it.
+#ifndef PEKF_FE_STAGE
+#define PEKF_FE_STAGE 10
+#endif
+#ifndef PEKF_FE_STAGE_THR
+#define PEKF_FE_STAGE_THR 56
+#endif
+
+// The staged form's LDS: each lane's queued records, one row per slot (row % S), lane-minor so a
+// lane's accesses are its own column (no other lane reads them: no barrier).
+template <int S>
+struct FeStage {
+    float4 gd[S][64];
+    float4 am[S][64];
+    float2 my[S][64];
+};
 #ifndef PEKF_FE_RING
 #define PEKF_FE_RING 9
 #endif
 
 // TE: the event planes may hold time events (Phase3::event).  dtx (may be null): the window's dt side
 // plane [r_max][batch]; an escaped record's float64 dt goes there (err bit 4), else err bit 1.
-template <bool TE>
-__global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_events,
+//
+// STG > 0 (one wave per block): lanes' record rows drift apart (a wave's lanes span ~20 rows, p90 7.5
+// from its median, scripts/record_drift.py), so a record stored where it is made writes 16 / 16 / 8 B
+// into its own row, and about one 32 B sector per store leaves L2: 2.6x the record bytes, half the
+// kernel's time (profiles/r4/frontend_occ/).  Here the wave keeps rows [base, base + STG) in LDS: a
+// lane's record for a row in that range is queued, any other (a lane that has fallen behind base, or
+// is STG rows ahead of it) is stored directly; row base is written by every lane holding it, as one
+// coalesced row, once at most 64 - THR ready lanes still lack it, and the queue drains after the last
+// event.  The records and their rows are unchanged; only the order of the stores differs.  10 rows:
+// 1.7x the record bytes written, -20 % time (profiles/r4/frontend_stage/).
+template <bool TE, int STG>
+__global__ __launch_bounds__(STG ? 64 : kFeBlock) void k_frontend(int64_t batch, int64_t n_events,
                                                        const float4 *__restrict__ ev,
                                                        const double *__restrict__ init,
                                                        const int64_t *__restrict__ t_init, double alpha,
@@ -30,7 +58,8 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
                                                        double *__restrict__ dtx,
                                                        int32_t *__restrict__ counts, double *__restrict__ refs,
                                                        int *__restrict__ err) {
-    const int64_t b = (int64_t)blockIdx.x * kFeBlock + threadIdx.x;
+    constexpr int kBlock = STG ? 64 : kFeBlock;
+    const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (b >= batch) return;
     Phase3 fe;
     fe.start(init + 6 * b, t_init[b], alpha);
@@ -44,6 +73,12 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
     int32_t r = 0;  // this filter's records so far (r_max < 2^31, checked on the host)
     const int32_t rmax = (int32_t)r_max;
     int bad = 0;
+    static_assert(STG >= 0 && STG <= 32, "the queue's rows are bits of one 32-bit mask");
+    constexpr int kS = STG ? STG : 1;
+    __shared__ FeStage<kS> st;
+    const int col = threadIdx.x & 63;
+    int32_t base = 0;   // STG: the oldest row the wave's queue holds (wave-uniform)
+    uint32_t held = 0;  // STG: bit row % STG = this lane's record for that row is queued
     // the pending record (Phase3::pend) is emitted every kFlush events; a lane never has two
     constexpr int kFlush = 3;
     auto flush = [&]() {
@@ -54,14 +89,43 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
         if (esc) bad |= dtx ? 4 : 1;
         if (r < rmax) {
             const int64_t o = (int64_t)r * batch + b;
-            gd[o] = rc.gd;
-            am[o] = rc.am;
-            my[o] = rc.my;
+            if (STG && r >= base && r < base + kS) {
+                const int sl = r % kS;
+                st.gd[sl][col] = rc.gd;
+                st.am[sl][col] = rc.am;
+                st.my[sl][col] = rc.my;
+                held |= 1u << sl;
+            } else {
+                gd[o] = rc.gd;
+                am[o] = rc.am;
+                my[o] = rc.my;
+            }
             if (esc && dtx) dtx[o] = fe.p.dt;
         } else {
             bad |= 2;  // more records than the output window holds
         }
         ++r;
+    };
+    // STG: write out queued rows -- while few enough ready lanes still lack row base, or (all) until
+    // no lane holds any
+    auto drain = [&](bool all) {
+        for (;;) {
+            if (all) {
+                if (!__any(held != 0)) break;
+            } else {
+                const int behind = __popcll(__ballot(ready && r <= base && r < rmax));
+                if (behind > 64 - PEKF_FE_STAGE_THR || !__any(held != 0)) break;
+            }
+            const int sl = base % kS;
+            if (held & (1u << sl)) {
+                const int64_t o = (int64_t)base * batch + b;
+                gd[o] = st.gd[sl][col];
+                am[o] = st.am[sl][col];
+                my[o] = st.my[sl][col];
+                held &= ~(1u << sl);
+            }
+            ++base;
+        }
     };
 
     // Events stream through a register ring of kRing records loaded kRing events ahead (the loop is
@@ -93,10 +157,14 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend(int64_t batch, int64_t n_
                 const float4 v4 = ring[k];
                 ring[k] = load(e0 + k + kRing);
                 fe.event<TE>(v4);
-                if ((k + 1) % kFlush == 0) flush();
+                if ((k + 1) % kFlush == 0) {
+                    flush();
+                    if constexpr (STG > 0) drain(false);
+                }
             }
         }
     }
+    if constexpr (STG > 0) drain(true);
     counts[b] = r < rmax ? r : rmax;
     if (bad && err) atomicOr(err, bad);
 }
@@ -253,13 +321,15 @@ extern "C" int pekf_frontend_ext_dev(int64_t batch, int64_t n_events, const void
     auto *gd = static_cast<float4 *>(plane_gd);
     auto *am = static_cast<float4 *>(plane_am);
     auto *my = static_cast<float2 *>(plane_my);
-    const dim3 grid(grid_for(batch, kFeBlock)), block(kFeBlock);
+    constexpr int kStg = PEKF_FE_STAGE;
+    constexpr int kBlock = kStg ? 64 : kFeBlock;
+    const dim3 grid(grid_for(batch, kBlock)), block(kBlock);
     if (flags & PEKF_EV_TIME_EVENTS)
-        hipLaunchKernelGGL(k_frontend<true>, grid, block, 0, as_stream(stream), batch, n_events, ev, init, t_init,
-                           alpha, r_max, gd, am, my, dt_ext, counts, refs, dev_error);
+        hipLaunchKernelGGL((k_frontend<true, kStg>), grid, block, 0, as_stream(stream), batch, n_events, ev, init,
+                           t_init, alpha, r_max, gd, am, my, dt_ext, counts, refs, dev_error);
     else
-        hipLaunchKernelGGL(k_frontend<false>, grid, block, 0, as_stream(stream), batch, n_events, ev, init, t_init,
-                           alpha, r_max, gd, am, my, dt_ext, counts, refs, dev_error);
+        hipLaunchKernelGGL((k_frontend<false, kStg>), grid, block, 0, as_stream(stream), batch, n_events, ev, init,
+                           t_init, alpha, r_max, gd, am, my, dt_ext, counts, refs, dev_error);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_frontend");
     return PEKF_OK;
