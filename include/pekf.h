@@ -274,7 +274,8 @@ int pekf_live_ext_dev(int64_t batch, int64_t n_events, const void *ev_planes, co
  * after its first n_avg and one more event has arrived (the KalmanFilter construction, :41-55); later
  * events move t_init to their time (:57-62).  Outputs (device): init[batch*6] = raw means {acc xyz, mag
  * xyz} and t_init[batch] -- pekf_frontend_dev's init / t_init --, ready[batch] (0: not enough phase-2
- * events; init is then NaN), stats[batch*12] (optional) = {gyro mean, acc / mag / gyro variance}. */
+ * events; init is then NaN), stats[batch*12] (optional) = {gyro mean, acc / mag / gyro variance};
+ * with stats NULL the second pass over the events (the variances) is skipped. */
 int pekf_frontend_init_dev(int64_t batch, int64_t n_events, const void *ev_planes, const int64_t *t_start,
                            int n_avg, double *init, int64_t *t_init, double *stats, int32_t *ready, void *stream);
 

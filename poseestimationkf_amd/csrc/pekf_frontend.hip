@@ -244,11 +244,13 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend_init(int64_t batch, int64
     for (int k = 0; k < 3; ++k)
 #pragma unroll
         for (int j = 0; j < 3; ++j) mean[k][j] = sum[k][j] / (double)n_avg;
-    // second pass: the variance of the first n_avg samples of each type, in their order
+    // second pass: the variance of the first n_avg samples of each type, in their order -- only when
+    // it is asked for (stats; pekf_live's session path takes the means alone)
     double var[3][3] = {};
     int c2[3] = {0, 0, 0};
-    for (int32_t e0 = 0; e0 < n_ev; e0 += kInitRing) {
-        if (c2[0] >= n_avg && c2[1] >= n_avg && c2[2] >= n_avg) break;
+    for (int32_t e0 = 0; stats && e0 < n_ev; e0 += kInitRing) {
+        // done once every type has its n_avg; a filter that never got ready reports NaN, so reads none
+        if (!kalman || (c2[0] >= n_avg && c2[1] >= n_avg && c2[2] >= n_avg)) break;
         float4 r[kInitRing];
 #pragma unroll
         for (int k = 0; k < kInitRing; ++k) r[k] = row(e0 + k);

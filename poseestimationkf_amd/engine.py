@@ -313,21 +313,26 @@ def run_frontend(ev, alpha=0.1, r_max=None):
     return win, win.counts
 
 
-def frontend_init(ev, n_avg=100):
+def frontend_init(ev, n_avg=100, stats=True):
     """Phase-2 events (synth.generate_events layout; ev["t_init"] = the time before the first one) ->
     dict(init (K, 6) raw {acc, mag} means, t_init (K,) int64, ready (K,) bool, gyro_mean (K, 3),
     var_acc / var_mag / var_gyro (K, 3)) by pekf_frontend_init_dev: the inputs run_frontend needs
-    for phase 3 (KFS/Parser.cpp:36-58,84-140, KFS/InitialValues.cpp)."""
+    for phase 3 (KFS/Parser.cpp:36-58,84-140, KFS/InitialValues.cpp).  stats=False: init / t_init /
+    ready only (the kernel then skips its second pass, the variances)."""
     K = np.asarray(ev["types"]).shape[1]
     evb, E, _ = _event_planes(ev)   # phase 2 always honours time events
     tsb = DeviceBuffer(8 * K).upload(np.ascontiguousarray(ev["t_init"], np.int64))
-    ib, tib, sb, rb = DeviceBuffer(48 * K), DeviceBuffer(8 * K), DeviceBuffer(96 * K), DeviceBuffer(4 * K)
-    check(lib.pekf_frontend_init_dev(K, E, evb.ptr, tsb.ptr, int(n_avg), ib.ptr, tib.ptr, sb.ptr, rb.ptr, None))
+    ib, tib, rb = DeviceBuffer(48 * K), DeviceBuffer(8 * K), DeviceBuffer(4 * K)
+    sb = DeviceBuffer(96 * K) if stats else None
+    check(lib.pekf_frontend_init_dev(K, E, evb.ptr, tsb.ptr, int(n_avg), ib.ptr, tib.ptr,
+                                     sb.ptr if stats else None, rb.ptr, None))
     check(lib.pekf_device_sync())
-    st = sb.download((K, 12), np.float64)
-    return dict(init=ib.download((K, 6), np.float64), t_init=tib.download((K,), np.int64),
-                ready=rb.download((K,), np.int32).astype(bool), gyro_mean=st[:, 0:3], var_acc=st[:, 3:6],
-                var_mag=st[:, 6:9], var_gyro=st[:, 9:12])
+    out = dict(init=ib.download((K, 6), np.float64), t_init=tib.download((K,), np.int64),
+               ready=rb.download((K,), np.int32).astype(bool))
+    if stats:
+        st = sb.download((K, 12), np.float64)
+        out.update(gyro_mean=st[:, 0:3], var_acc=st[:, 3:6], var_mag=st[:, 6:9], var_gyro=st[:, 9:12])
+    return out
 
 
 def run_session(phase2, phase3, filters, n_avg=100, alpha=0.1):

@@ -156,6 +156,14 @@ def main():
                             "ready": int(rb2.download((K,), np.int32).sum()), "bytes": byts,
                             "gbs": byts / (ms * 1e-3) / 1e9, "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM}
     log("frontend phase 2: %.2f ms" % ms)
+    # the means alone (stats = NULL, as engine.run_session asks): pass 1 only
+    ms = timed(lambda: check(lib.pekf_frontend_init_dev(K, E, evb.ptr, tb.ptr, 100, ib2.ptr, tb2.ptr, None,
+                                                        rb2.ptr, s)), s)
+    byts = 16 * K * E
+    res["frontend_init_means"] = {"filters": K, "events_per_filter": E, "kernel_ms": ms,
+                                  "events_per_s": K * E / (ms * 1e-3), "bytes": byts,
+                                  "gbs": byts / (ms * 1e-3) / 1e9, "hbm_frac": byts / (ms * 1e-3) / 1e9 / HBM}
+    log("frontend phase 2, means only: %.2f ms" % ms)
     del ib2, tb2, sb2, rb2
     # the filter over the front-end's records (split pipeline, second half): one multi-record launch
     # with counts, as engine.BatchedEKF.run does for a front-end window

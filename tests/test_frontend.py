@@ -218,6 +218,11 @@ def test_frontend_init_kernel_vs_oracle(eng, E, n_avg):
         for name in ("acc", "mag", "gyro"):
             assert np.array_equal(got["var_" + name][k], np.array(o["var_" + name]))
     assert n_ready > 0 and (E != 520 or n_ready < K)
+    # without stats (run_session's call) the kernel skips the variance pass; the rest is unchanged
+    means = eng.frontend_init(ev, n_avg=n_avg, stats=False)
+    assert set(means) == {"init", "t_init", "ready"}
+    assert np.array_equal(means["ready"], got["ready"]) and np.array_equal(means["t_init"], got["t_init"])
+    assert np.array_equal(means["init"], got["init"], equal_nan=True)
 
 
 @pytest.mark.gpu
