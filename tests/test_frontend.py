@@ -127,6 +127,55 @@ def _events(K, spec):
 
 
 @pytest.mark.gpu
+def test_frontend_row_queue_with_drifting_lanes(eng):
+    """k_frontend stages a wave's records in a 10-row LDS queue and writes whole rows; records of
+    lanes too far behind or ahead of the queue are stored directly.  Lanes drifting 0-12 rows apart
+    (acc-only lead-ins), a slow lane (a record per 5 events), a late lane, one with no records, one
+    never ready, and a partial last wave: every record of every filter equals the restatement's."""
+    A, G, M = synth.EV_ACC, synth.EV_GYRO, synth.EV_MAG
+    K, E = 64 * 2 + 5, 600
+    types = np.empty((E, K), np.uint32)
+    for k in range(K):
+        lane = k % 64
+        if lane < 58:      # triples after a lead-in of (lane % 13) x 3 acc events
+            seq = [A] * (3 * (lane % 13)) + [G, A, M] * E
+        elif lane < 60:    # slow: G A M G A, one record per 5 events
+            seq = [G, A, M, G, A] * E
+        elif lane < 62:    # late: half the stream acc only
+            seq = [A] * (E // 2) + [G, A, M] * E
+        else:              # no record (62), or never ready (63)
+            seq = [A, M] * E
+            if lane == 63:
+                seq = [G, A, M] * E
+        types[:, k] = seq[:E]
+    e = np.arange(E)[:, None]
+    gaps = 900 + (e * 7 + np.arange(K)[None, :] * 13) % 400
+    times = synth.T_INIT_NS + np.cumsum(gaps, axis=0)
+    vals = (np.sin(0.05 * e[..., None] + 0.1 * np.arange(K)[None, :, None] + np.arange(3)[None, None, :]) +
+            np.where(types[..., None] == A, [0, 0, 9.0], [0, 0, 0])).astype(np.float32)
+    init_acc = np.tile([0.1, 0.2, 9.8], (K, 1))
+    init_acc[np.arange(K) % 64 == 63] = np.nan
+    ev = dict(types=types, values=vals, times=times, init_acc=init_acc,
+              init_mag=np.tile([20.0, 1.0, -40.0], (K, 1)), t_init=np.full(K, synth.T_INIT_NS, np.int64))
+    win, counts = eng.run_frontend(ev)
+    rec = win.download_filters(np.arange(K))
+    spread = []
+    for k in range(K):
+        if k % 64 == 63:
+            assert counts[k] == 0
+            continue
+        g, dt, a, m = _oracle_records(ev, k)
+        r = len(dt)
+        spread.append(r)
+        assert counts[k] == r
+        assert np.array_equal(rec.gyro[:r, k], g.astype(np.float32))
+        assert np.array_equal(rec.dtw[:r, k], dt.astype(np.uint32))
+        assert _f32_ulps(rec.acc[:r, k], a) <= 1
+        assert _f32_ulps(rec.mag[:r, k], m) <= 1
+    assert max(spread) - min(spread) > 100 and 0 in spread
+
+
+@pytest.mark.gpu
 def test_frontend_streams_without_records(eng):
     K = 70
     for spec in ([], [(synth.EV_ACC, 10), (synth.EV_MAG, 10)] * 5,            # nothing, or no gyro at all
