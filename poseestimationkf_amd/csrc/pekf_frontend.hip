@@ -14,9 +14,18 @@
 namespace pekf {
 
 constexpr int kFeBlock = 256;
+typedef float nv4f __attribute__((ext_vector_type(4)));  // the native vector the nontemporal builtins take
 // k_frontend's per-wave LDS record queue (profiles/r4/frontend_stage/: 8-16 rows x thresholds 52-60
 // swept; 10 rows = 25.6 KB per wave, 6 waves per CU): rows held (0: every record stored where it is
 // made), and the queue's oldest row is written once at most 64 - THR ready lanes still lack it.
+// Non-temporal event loads (every event is read once per pass): k_frontend -1.7 %, phase 2's means
+// -5 % (profiles/r4/ntload/).
+#ifndef PEKF_FE_NTL
+#define PEKF_FE_NTL 1
+#endif
+#ifndef PEKF_INIT_NTL
+#define PEKF_INIT_NTL 1
+#endif
 #ifndef PEKF_FE_STAGE
 #define PEKF_FE_STAGE 10
 #endif
@@ -138,7 +147,12 @@ __global__ __launch_bounds__(STG ? 64 : kFeBlock) void k_frontend(int64_t batch,
     const int32_t n_ev = (int32_t)n_events;
     auto load = [&](int32_t e) -> float4 {
         const int32_t row = e < n_ev ? e : n_ev - 1;
+#if PEKF_FE_NTL
+        const nv4f v = __builtin_nontemporal_load((const nv4f *)(ev + (int64_t)row * batch + lane));
+        return make_float4(v.x, v.y, v.z, v.w);
+#else
         return (ev + (int64_t)row * batch)[lane];
+#endif
     };
     if (n_ev > 0) {
         constexpr int kRing = PEKF_FE_RING;  // events in flight per lane (a multiple of kFlush)
@@ -199,7 +213,15 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend_init(int64_t batch, int64
     constexpr int kInitRing = 8;
     const int32_t n_ev = (int32_t)n_events;
     const float4 null_ev = make_float4(0.f, 0.f, 0.f, __uint_as_float(PEKF_EV_TIME));
-    auto row = [&](int32_t e) -> float4 { return (ev + (int64_t)(e < n_ev ? e : n_ev - 1) * batch)[lane]; };
+    auto row = [&](int32_t e) -> float4 {
+        const float4 *q = ev + (int64_t)(e < n_ev ? e : n_ev - 1) * batch + lane;
+#if PEKF_INIT_NTL
+        const nv4f v = __builtin_nontemporal_load((const nv4f *)q);
+        return make_float4(v.x, v.y, v.z, v.w);
+#else
+        return *q;
+#endif
+    };
     auto pad = [&](int32_t e0, float4 (&r)[kInitRing]) {
         if (e0 + kInitRing > n_ev) {  // uniform: the last block only
 #pragma unroll

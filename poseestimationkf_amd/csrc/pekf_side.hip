@@ -12,6 +12,14 @@
 
 namespace pekf {
 
+// The gyro chain's record loads carry the non-temporal hint (each record is read once): 28.9 -> 26.7 ms
+// at 1M x 10,000 records; the Wahba stream's do not (+1 % with it) (profiles/r4/ntload/).
+__device__ __forceinline__ float4 ld_nt(const float4 *p) {
+    typedef float v4 __attribute__((ext_vector_type(4)));
+    const v4 v = __builtin_nontemporal_load((const v4 *)p);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 constexpr int kSideBlock = 256;
 
 // Both stream kernels are HBM-bound (a few dozen FP64 ops per 16-24 B record), so each lane keeps
@@ -42,12 +50,12 @@ __global__ __launch_bounds__(kSideBlock) void k_gyro_chain(int64_t batch, int64_
     int32_t pf = (int32_t)(step0 % window);  // next row to prefetch
 #pragma unroll
     for (int k = 0; k < kDepth; ++k) {
-        ring[k] = (gd + (int64_t)pf * batch)[lane];
+        ring[k] = ld_nt(gd + (int64_t)pf * batch + lane);
         pf = next_row(pf, W);
     }
     auto one = [&](int k, int32_t t) {
         const float4 r = ring[k];
-        ring[k] = (gd + (int64_t)pf * batch)[lane];
+        ring[k] = ld_nt(gd + (int64_t)pf * batch + lane);
         pf = next_row(pf, W);
         const double hw[3] = {0.5 * (double)r.x, 0.5 * (double)r.y, 0.5 * (double)r.z};
         const uint32_t word = __float_as_uint(r.w) & PEKF_DT_MASK;

@@ -2,9 +2,10 @@
 """The front-end kernel alone (the bench_aux.py workload: 16K generated event streams tiled x64 ->
 1,048,576 filters x 1,024 events), for rocprofv3 PMC passes that should see only k_frontend; with
 --live the fused front-end + filter kernel (pekf_live_dev) on the same events instead, with --init
-phase 2 (pekf_frontend_init_dev, the means / variances of the first 100 samples).
+phase 2 (pekf_frontend_init_dev, the means / variances of the first 100 samples; --init-means: the
+means alone, no stats, as engine.run_session calls it).
 
-usage: python3 scripts/frontend_probe.py [reps] [--live | --init]
+usage: python3 scripts/frontend_probe.py [reps] [--live | --init | --init-means]
 """
 from __future__ import annotations
 
@@ -23,7 +24,8 @@ from poseestimationkf_amd._lib import check, lib  # noqa: E402
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     live = "--live" in sys.argv
-    phase2 = "--init" in sys.argv
+    means_only = "--init-means" in sys.argv
+    phase2 = "--init" in sys.argv or means_only
     reps = int(args[0]) if args else 3
     st = engine.Stream()
     s = st.handle
@@ -49,7 +51,8 @@ def main():
     for _ in range(reps):
         e0.record(s)
         if phase2:
-            check(lib.pekf_frontend_init_dev(K, E, evb.ptr, tb.ptr, 100, ob.ptr, tob.ptr, sb.ptr, rb.ptr, s))
+            check(lib.pekf_frontend_init_dev(K, E, evb.ptr, tb.ptr, 100, ob.ptr, tob.ptr,
+                                             None if means_only else sb.ptr, rb.ptr, s))
         elif live:
             f.run_events_async(evb, E, ib, tb, cnt, win.refs, 0.1, s)
         else:
@@ -60,9 +63,11 @@ def main():
         times.append(e0.elapsed_ms(e1))
     if phase2:
         ready = int(rb.download((K,), np.int32).sum())
-        digest = float(np.nansum(sb.download((K, 12), np.float64)))
-        print("frontend_probe --init: %d filters x %d events, %d ready, stats digest %.17g, ms %s"
-              % (K, E, ready, digest, ["%.3f" % t for t in times]))
+        src = ob.download((K, 6), np.float64) if means_only else sb.download((K, 12), np.float64)
+        digest = float(np.nansum(src)) + float(tob.download((K,), np.int64).astype(np.float64).sum())
+        print("frontend_probe %s: %d filters x %d events, %d ready, %s digest %.17g, ms %s"
+              % ("--init-means" if means_only else "--init", K, E, ready, "means" if means_only else "stats",
+                 digest, ["%.3f" % t for t in times]))
         return
     recs = int(cnt.download((K,), np.int32).sum())
     print("frontend_probe%s: %d filters x %d events, %d records, ms %s"
