@@ -348,20 +348,28 @@ int pekf_comm_unique_id(void *id /* PEKF_COMM_ID_BYTES */);
 /* Communicator creation has a deadline: ncclCommInitRank (rccl.h) runs on a helper thread and the call
  * waits for it at most PEKF_COMM_TIMEOUT_S seconds (environment; default 300).  If the other ranks do not
  * all join by then it returns PEKF_ERR_TIMEOUT, so a rank that died before joining fails the job instead
- * of hanging it; the abandoned helper stays blocked inside RCCL until the process exits (exit soon).
+ * of hanging it.  The abandoned helper stays blocked inside RCCL until the process exits: after an init
+ * timeout the PROCESS MUST EXIT (without its exit handlers, e.g. _exit); until then every later
+ * pekf_comm_init* call fails at once with PEKF_ERR_COMM rather than reuse RCCL's bootstrap state.
  * (RCCL 2.27's non-blocking ncclCommInitRankConfig still blocks the caller while a rank is missing.) */
 int pekf_comm_init(const void *id, int nranks, int rank, pekf_comm **out);
 /* The same with an explicit deadline in seconds (<= 0: wait forever, the blocking behaviour). */
 int pekf_comm_init_timeout(const void *id, int nranks, int rank, double timeout_s, pekf_comm **out);
-/* devices: ndev device indices (NULL = 0 .. ndev-1); out: ndev communicators, rank i on devices[i] */
+/* devices: ndev device indices (NULL = 0 .. ndev-1); out: ndev communicators, rank i on devices[i].
+ * ncclCommInitAll (rccl.h:236) under the same PEKF_COMM_TIMEOUT_S deadline and rules as pekf_comm_init. */
 int pekf_comm_init_all(int ndev, const int *devices, pekf_comm **out);
+/* The same with an explicit deadline in seconds (<= 0: none). */
+int pekf_comm_init_all_timeout(int ndev, const int *devices, double timeout_s, pekf_comm **out);
 int pekf_comm_destroy(pekf_comm *c);
 /* Abort a communicator (ncclCommAbort: its kernels in flight give up) and free it; for error paths. */
 int pekf_comm_abort(pekf_comm *c);
-/* Wait until `stream` has drained everything enqueued on it, collectives of c included, for at most
- * timeout_s seconds (<= 0: no deadline), watching c for asynchronous RCCL errors meanwhile.  On expiry
- * or error c is aborted (it must then only be destroyed) and PEKF_ERR_TIMEOUT / PEKF_ERR_COMM returned:
- * a peer that died turns into an error here instead of a host thread stuck in hipStreamSynchronize. */
+/* Wait until `stream` has drained everything enqueued on it, collectives of c included, watching c for
+ * asynchronous RCCL errors meanwhile.  The deadline timeout_s (<= 0: none) applies to each collective of c
+ * enqueued on `stream` (pekf_gather_dev, pekf_gather_multi_dev, pekf_allreduce_max_dev) and starts when the
+ * stream reaches it -- the work queued before it has finished -- so compute ahead of a collective, however
+ * long, is never charged to it.  On expiry or error c is aborted (it must then only be destroyed) and
+ * PEKF_ERR_TIMEOUT / PEKF_ERR_COMM returned: a peer that died turns into an error here instead of a host
+ * thread stuck in hipStreamSynchronize. */
 int pekf_comm_wait(pekf_comm *c, void *stream, double timeout_s);
 int pekf_comm_rank(const pekf_comm *c, int *rank, int *nranks, int *device); /* outputs may be NULL */
 /* recv[nranks * count] on the root (rows in rank order) <- every rank's send[count]; device

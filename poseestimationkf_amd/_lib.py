@@ -39,7 +39,10 @@ class NoDeviceError(PekfError):
 
 
 class CommTimeoutError(PekfError):
-    """A collective step passed its deadline (PEKF_COMM_TIMEOUT_S); the communicator was aborted."""
+    """A collective step passed its deadline (PEKF_COMM_TIMEOUT_S); the communicator was aborted.
+
+    After a communicator-creation timeout the process must exit (os._exit: the abandoned RCCL init
+    thread still holds RCCL's bootstrap state); until it does, every later creation fails at once."""
 
 
 _i64, _u32, _int, _dbl, _sz, _vp = ctypes.c_int64, ctypes.c_uint32, ctypes.c_int, ctypes.c_double, ctypes.c_size_t, ctypes.c_void_p
@@ -121,6 +124,7 @@ SIGNATURES = {
     "pekf_comm_abort": [_vp],
     "pekf_comm_wait": [_vp, _vp, _dbl],
     "pekf_comm_init_all": [_int, _ip, ctypes.POINTER(_vp)],
+    "pekf_comm_init_all_timeout": [_int, _ip, _dbl, ctypes.POINTER(_vp)],
     "pekf_comm_destroy": [_vp],
     "pekf_comm_rank": [_vp, _ip, _ip, _ip],
     "pekf_gather_dev": [_vp, _vp, _i64, _vp, _int, _vp],

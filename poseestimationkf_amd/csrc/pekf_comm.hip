@@ -11,13 +11,20 @@
 // one PyTorch-ROCm bundles) the loader hands back that same library, so there is one RCCL and
 // one HIP runtime per process.
 //
-// Deadlines: communicator creation waits for the (blocking) ncclCommInitRank on a helper thread for at
-// most PEKF_COMM_TIMEOUT_S, and pekf_comm_wait drains a stream of collectives against a deadline,
-// aborting the communicator (ncclCommAbort) on expiry, so a rank that never joins or dies mid-run ends
-// the job with PEKF_ERR_TIMEOUT instead of leaving every other rank blocked inside RCCL.
+// Deadlines (PEKF_COMM_TIMEOUT_S, default 300 s):
+//  * communicator creation -- ncclCommInitRank (one process per GPU) and ncclCommInitAll (one process
+//    for several GPUs) -- runs on a helper thread that the caller waits for until the deadline;
+//  * pekf_comm_wait drains a stream, and every collective enqueued on it through this file gets the
+//    deadline from the moment the stream reaches it (its inputs are ready: the compute queued before
+//    it has finished), so a long compute queue is never mistaken for a dead peer, while a collective
+//    that a peer never joins is aborted (ncclCommAbort) at its deadline.
+// Either way a rank that never joins or dies mid-run ends the job with PEKF_ERR_TIMEOUT instead of
+// leaving every other rank blocked inside RCCL.
 #include <dlfcn.h>
 
+#include <atomic>
 #include <chrono>
+#include <deque>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -164,11 +171,89 @@ int settle(ncclComm_t nc, double deadline, const char *what, bool *expired) {
 struct pekf_comm {
     ncclComm_t nc;
     int nranks, rank, device;
-    double timeout_s;  // deadline of each settle / wait on this communicator (<= 0: none)
+    double timeout_s;  // deadline of each settle on this communicator (<= 0: none)
+    // The collectives enqueued on this communicator through this file and not yet seen complete, oldest
+    // first: an event recorded just before each (its inputs are ready once it completes) and one just
+    // after (the collective has completed).  pekf_comm_wait starts a collective's deadline when it sees
+    // the first event complete, so only the collective itself, never the compute ahead of it, is timed.
+    struct Pending {
+        hipEvent_t pre, post;
+        hipStream_t stream;
+        const char *what;
+        double ready_at;  // when pekf_comm_wait first saw `pre` complete (0: not yet)
+    };
+    std::deque<Pending> pending{};
+    std::vector<hipEvent_t> spare{};  // events of retired entries, for reuse (on `device`)
 };
 
 namespace pekf {
 namespace {
+
+// Makes `dev` current for the scope (events and the null stream belong to the current device).
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess || prev == dev) prev = -1;
+        else (void)hipSetDevice(dev);
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+constexpr size_t kMaxPending = 1024;  // beyond this the oldest collective goes untracked (never waited on)
+
+void release(pekf_comm *c, const pekf_comm::Pending &p) {
+    c->spare.push_back(p.pre);
+    c->spare.push_back(p.post);
+}
+
+// Drops the completed collectives at the front of c's list.
+void retire(pekf_comm *c) {
+    while (!c->pending.empty() && hipEventQuery(c->pending.front().post) == hipSuccess) {
+        release(c, c->pending.front());
+        c->pending.pop_front();
+    }
+}
+
+// An event recorded on s now (nullptr if the runtime refused: the collective then goes untracked).
+hipEvent_t mark(pekf_comm *c, hipStream_t s) {
+    DeviceScope on(c->device);
+    hipEvent_t ev = nullptr;
+    if (!c->spare.empty()) {
+        ev = c->spare.back();
+        c->spare.pop_back();
+    } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+        return nullptr;
+    }
+    if (hipEventRecord(ev, s) != hipSuccess) {
+        c->spare.push_back(ev);
+        return nullptr;
+    }
+    return ev;
+}
+
+void track(pekf_comm *c, hipStream_t s, hipEvent_t pre, hipEvent_t post, const char *what) {
+    if (!pre || !post) {
+        if (pre) c->spare.push_back(pre);
+        if (post) c->spare.push_back(post);
+        return;
+    }
+    retire(c);
+    if (c->pending.size() >= kMaxPending) {
+        release(c, c->pending.front());
+        c->pending.pop_front();
+    }
+    c->pending.push_back({pre, post, s, what, 0.0});
+}
+
+void drop_events(pekf_comm *c) {
+    DeviceScope on(c->device);
+    for (const auto &p : c->pending) release(c, p);
+    c->pending.clear();
+    for (hipEvent_t e : c->spare) (void)hipEventDestroy(e);
+    c->spare.clear();
+}
 
 // Aborts c's RCCL communicator (kernels of it still in flight give up) and leaves c destroy-only.
 void abort_comm(pekf_comm *c) {
@@ -189,6 +274,79 @@ int enqueued(pekf_comm *c, ncclResult_t e, const char *what) {
                          c->timeout_s);
     }
     return st;
+}
+
+// Enqueues one collective of c on s between the two tracking events.
+template <class Enqueue>
+int tracked(pekf_comm *c, hipStream_t s, const char *what, Enqueue enqueue) {
+    hipEvent_t pre = mark(c, s);
+    const int st = enqueued(c, enqueue(), what);
+    if (st != PEKF_OK || !c->nc) {
+        if (pre) c->spare.push_back(pre);
+        return st;
+    }
+    track(c, s, pre, mark(c, s), what);
+    return PEKF_OK;
+}
+
+// Communicator creations abandoned at their deadline whose helper thread is still blocked inside RCCL.
+// While there is one, RCCL's bootstrap state is not to be trusted: later creations fail at once.
+std::atomic<int> g_abandoned_inits{0};
+
+enum class InitEnd { done, timed_out };
+
+// Runs `init` (a blocking RCCL communicator creation filling n communicators) on a helper thread and
+// waits for it at most timeout_s (<= 0: inline, no deadline).  On expiry the helper is abandoned: it
+// stays blocked inside RCCL until the process exits, and if the creation completes after all it
+// aborts the communicators it got.  *res is RCCL's result when the creation ended in time.
+template <class Init>
+InitEnd init_with_deadline(double timeout_s, int n, Init init, std::vector<ncclComm_t> *comms, ncclResult_t *res) {
+    comms->assign(n, nullptr);
+    if (timeout_s <= 0) {
+        *res = init(comms->data());
+        return InitEnd::done;
+    }
+    struct Job {
+        std::mutex m;
+        std::condition_variable cv;
+        bool done = false, abandoned = false;
+        ncclResult_t res = ncclSuccess;
+        std::vector<ncclComm_t> nc;
+    };
+    auto job = std::make_shared<Job>();
+    job->nc.assign(n, nullptr);
+    std::thread([job, init] {
+        std::vector<ncclComm_t> nc(job->nc.size(), nullptr);
+        const ncclResult_t r = init(nc.data());
+        std::lock_guard<std::mutex> g(job->m);
+        if (job->abandoned) {
+            for (ncclComm_t x : nc)
+                if (x) (void)rccl().abort(x);
+            g_abandoned_inits.fetch_sub(1);
+            return;
+        }
+        job->res = r;
+        job->nc = nc;
+        job->done = true;
+        job->cv.notify_all();
+    }).detach();
+    std::unique_lock<std::mutex> lk(job->m);
+    if (!job->cv.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return job->done; })) {
+        job->abandoned = true;
+        g_abandoned_inits.fetch_add(1);
+        return InitEnd::timed_out;
+    }
+    *res = job->res;
+    *comms = job->nc;
+    return InitEnd::done;
+}
+
+int refuse_after_abandoned_init() {
+    if (g_abandoned_inits.load() > 0)
+        return set_error(PEKF_ERR_COMM,
+                         "an earlier RCCL communicator creation passed its deadline and is still blocked inside "
+                         "RCCL; this process must exit before it can create another communicator");
+    return PEKF_OK;
 }
 
 }  // namespace
@@ -219,61 +377,31 @@ int pekf_comm_init_timeout(const void *id, int nranks, int rank, double timeout_
     PEKF_CHECK_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "need 0 <= rank < nranks");
     *out = nullptr;
     if (int st = need_rccl()) return st;
+    if (int st = refuse_after_abandoned_init()) return st;
     int dev = 0;
     PEKF_HIP(hipGetDevice(&dev));
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
-    Rccl &r = rccl();
-    if (timeout_s <= 0) {
-        ncclComm_t nc = nullptr;
-        PEKF_NCCL(r.init_rank(&nc, nranks, u, rank));  // collective over the nranks processes, no deadline
-        *out = new pekf_comm{nc, nranks, rank, dev, 0.0};
-        return PEKF_OK;
-    }
     // RCCL 2.27's "non-blocking" init (ncclCommInitRankConfig, blocking = 0) still waits in the calling
     // thread for every rank to reach the bootstrap root (measured on the box: it never returned with a
-    // rank missing, scripts/comm_timeout_probe.py), so the deadline is kept here instead: the blocking
-    // init runs on a helper thread and this thread waits for it until the deadline.  On expiry the
-    // helper is abandoned -- it stays blocked inside RCCL until the process exits, and if the missing
-    // rank turns up after all it aborts the communicator it gets -- and PEKF_ERR_TIMEOUT is returned.
-    struct Job {
-        std::mutex m;
-        std::condition_variable cv;
-        bool done = false, abandoned = false;
-        ncclResult_t res = ncclSuccess;
-        ncclComm_t nc = nullptr;
+    // rank missing, scripts/comm_timeout_probe.py), so the deadline is kept here, on a helper thread.
+    PEKF_COMM_TRACE("rank %d/%d on device %d: ncclCommInitRank (deadline %.0f s)", rank, nranks, dev, timeout_s);
+    std::vector<ncclComm_t> nc;
+    ncclResult_t res = ncclSuccess;
+    const auto init = [nranks, u, rank, dev](ncclComm_t *c) {
+        if (hipSetDevice(dev) != hipSuccess) return ncclUnhandledCudaError;
+        return rccl().init_rank(c, nranks, u, rank);
     };
-    auto job = std::make_shared<Job>();
-    PEKF_COMM_TRACE("rank %d/%d on device %d: ncclCommInitRank on a helper thread (deadline %.0f s)", rank, nranks,
-                    dev, timeout_s);
-    std::thread([job, nranks, u, rank, dev] {
-        ncclComm_t nc = nullptr;
-        ncclResult_t res = ncclSuccess;
-        if (hipSetDevice(dev) != hipSuccess) res = ncclUnhandledCudaError;
-        else res = rccl().init_rank(&nc, nranks, u, rank);
-        std::lock_guard<std::mutex> g(job->m);
-        if (job->abandoned) {
-            if (nc) (void)rccl().abort(nc);
-            return;
-        }
-        job->res = res;
-        job->nc = nc;
-        job->done = true;
-        job->cv.notify_all();
-    }).detach();
-    std::unique_lock<std::mutex> lk(job->m);
-    const bool finished = job->cv.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return job->done; });
-    if (!finished) {
-        job->abandoned = true;
+    if (init_with_deadline(timeout_s, 1, init, &nc, &res) == InitEnd::timed_out) {
         PEKF_COMM_TRACE("rank %d/%d: deadline passed; init abandoned", rank, nranks);
         return set_error(PEKF_ERR_TIMEOUT,
                          "RCCL communicator init (ncclCommInitRank, rank %d of %d, device %d): not all %d ranks "
                          "joined within %.0f s (PEKF_COMM_TIMEOUT_S); init abandoned",
                          rank, nranks, dev, nranks, timeout_s);
     }
-    PEKF_COMM_TRACE("rank %d/%d: ncclCommInitRank returned %d", rank, nranks, (int)job->res);
-    if (job->res != ncclSuccess) return nccl_fail(job->res, "ncclCommInitRank");
-    *out = new pekf_comm{job->nc, nranks, rank, dev, timeout_s};
+    PEKF_COMM_TRACE("rank %d/%d: ncclCommInitRank returned %d", rank, nranks, (int)res);
+    if (res != ncclSuccess) return nccl_fail(res, "ncclCommInitRank");
+    *out = new pekf_comm{nc[0], nranks, rank, dev, timeout_s > 0 ? timeout_s : 0.0};
     return PEKF_OK;
 }
 
@@ -281,9 +409,11 @@ int pekf_comm_init(const void *id, int nranks, int rank, pekf_comm **out) {
     return pekf_comm_init_timeout(id, nranks, rank, env_timeout_s(), out);
 }
 
-int pekf_comm_init_all(int ndev, const int *devices, pekf_comm **out) {
+int pekf_comm_init_all_timeout(int ndev, const int *devices, double timeout_s, pekf_comm **out) {
     PEKF_CHECK_ARG(out && ndev >= 1, "need ndev >= 1 and an output array");
+    for (int i = 0; i < ndev; ++i) out[i] = nullptr;
     if (int st = need_rccl()) return st;
+    if (int st = refuse_after_abandoned_init()) return st;
     int visible = 0;
     PEKF_HIP(hipGetDeviceCount(&visible));
     std::vector<int> devs(ndev);
@@ -291,14 +421,30 @@ int pekf_comm_init_all(int ndev, const int *devices, pekf_comm **out) {
         devs[i] = devices ? devices[i] : i;
         PEKF_CHECK_ARG(devs[i] >= 0 && devs[i] < visible, "device index out of range");
     }
-    std::vector<ncclComm_t> nc(ndev, nullptr);
-    PEKF_NCCL(rccl().init_all(nc.data(), ndev, devs.data()));
-    for (int i = 0; i < ndev; ++i) out[i] = new pekf_comm{nc[i], ndev, i, devs[i], env_timeout_s()};
+    PEKF_COMM_TRACE("ncclCommInitAll over %d devices (deadline %.0f s)", ndev, timeout_s);
+    std::vector<ncclComm_t> nc;
+    ncclResult_t res = ncclSuccess;
+    const auto init = [ndev, devs](ncclComm_t *c) { return rccl().init_all(c, ndev, devs.data()); };
+    if (init_with_deadline(timeout_s, ndev, init, &nc, &res) == InitEnd::timed_out) {
+        PEKF_COMM_TRACE("ncclCommInitAll: deadline passed; init abandoned");
+        return set_error(PEKF_ERR_TIMEOUT,
+                         "RCCL communicator init (ncclCommInitAll over %d devices): not done within %.0f s "
+                         "(PEKF_COMM_TIMEOUT_S); init abandoned",
+                         ndev, timeout_s);
+    }
+    PEKF_COMM_TRACE("ncclCommInitAll returned %d", (int)res);
+    if (res != ncclSuccess) return nccl_fail(res, "ncclCommInitAll");
+    for (int i = 0; i < ndev; ++i) out[i] = new pekf_comm{nc[i], ndev, i, devs[i], timeout_s > 0 ? timeout_s : 0.0};
     return PEKF_OK;
+}
+
+int pekf_comm_init_all(int ndev, const int *devices, pekf_comm **out) {
+    return pekf_comm_init_all_timeout(ndev, devices, env_timeout_s(), out);
 }
 
 int pekf_comm_destroy(pekf_comm *c) {
     if (!c) return PEKF_OK;
+    drop_events(c);
     if (!c->nc) {  // aborted: nothing left to destroy
         delete c;
         return PEKF_OK;
@@ -317,6 +463,7 @@ int pekf_comm_destroy(pekf_comm *c) {
 int pekf_comm_abort(pekf_comm *c) {
     if (!c) return PEKF_OK;
     abort_comm(c);
+    drop_events(c);
     delete c;
     return PEKF_OK;
 }
@@ -325,10 +472,12 @@ int pekf_comm_wait(pekf_comm *c, void *stream, double timeout_s) {
     PEKF_CHECK_ARG(c, "null communicator");
     PEKF_CHECK_ARG(c->nc, "communicator was aborted");
     const hipStream_t s = as_stream(stream);
-    const double deadline = deadline_after(timeout_s);
     for (;;) {
         const hipError_t q = hipStreamQuery(s);
-        if (q == hipSuccess) return PEKF_OK;
+        if (q == hipSuccess) {
+            retire(c);
+            return PEKF_OK;
+        }
         if (q != hipErrorNotReady) return hip_fail(q, "hipStreamQuery");
         ncclResult_t st = ncclSuccess;
         if (rccl().async_error(c->nc, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress) {
@@ -336,12 +485,31 @@ int pekf_comm_wait(pekf_comm *c, void *stream, double timeout_s) {
             return set_error(PEKF_ERR_COMM, "RCCL asynchronous error on rank %d of %d: %s (%d); communicator aborted",
                              c->rank, c->nranks, rccl().error_string(st), (int)st);
         }
-        if (deadline > 0 && now_s() > deadline) {
-            abort_comm(c);
-            return set_error(PEKF_ERR_TIMEOUT,
-                             "rank %d of %d: the stream's collectives did not complete within %.0f s (a peer rank "
-                             "gone?); communicator aborted",
-                             c->rank, c->nranks, timeout_s);
+        // the oldest collective of this stream that has not completed: is the stream at it yet?
+        pekf_comm::Pending *head = nullptr;
+        for (auto it = c->pending.begin(); it != c->pending.end();) {
+            if (it->stream != s) {
+                ++it;
+            } else if (hipEventQuery(it->post) == hipSuccess) {
+                release(c, *it);
+                it = c->pending.erase(it);
+            } else {
+                head = &*it;
+                break;
+            }
+        }
+        if (head && timeout_s > 0 && hipEventQuery(head->pre) == hipSuccess) {
+            const double t = now_s();
+            if (head->ready_at == 0.0) {
+                head->ready_at = t;
+            } else if (t - head->ready_at > timeout_s) {
+                const char *what = head->what;
+                abort_comm(c);
+                return set_error(PEKF_ERR_TIMEOUT,
+                                 "rank %d of %d: %s did not complete within %.0f s of its inputs being ready (a peer "
+                                 "rank gone?); communicator aborted",
+                                 c->rank, c->nranks, what, timeout_s);
+            }
         }
         std::this_thread::sleep_for(std::chrono::microseconds(100));
     }
@@ -361,8 +529,8 @@ int pekf_gather_dev(pekf_comm *c, const double *send, int64_t count, double *rec
     PEKF_CHECK_ARG(root >= 0 && root < c->nranks, "root out of range");
     PEKF_CHECK_ARG(c->rank != root || recv, "the root needs a receive buffer of nranks * count doubles");
     PEKF_CHECK_ARG(c->nc, "communicator was aborted");
-    return enqueued(c, rccl().gather(send, recv, (size_t)count, ncclFloat64, root, c->nc, as_stream(stream)),
-                    "ncclGather");
+    const hipStream_t s = as_stream(stream);
+    return tracked(c, s, "ncclGather", [&] { return rccl().gather(send, recv, (size_t)count, ncclFloat64, root, c->nc, s); });
 }
 
 int pekf_gather_multi_dev(int ndev, pekf_comm *const *comms, const double *const *send, int64_t count,
@@ -371,16 +539,33 @@ int pekf_gather_multi_dev(int ndev, pekf_comm *const *comms, const double *const
     PEKF_CHECK_ARG(count >= 0, "negative size");
     PEKF_CHECK_ARG(root >= 0 && root < ndev && recv, "root out of range or no receive buffer");
     for (int i = 0; i < ndev; ++i) PEKF_CHECK_ARG(comms[i] && comms[i]->nc, "null or aborted communicator");
-    PEKF_NCCL(rccl().group_start());
+    std::vector<hipEvent_t> pre(ndev);
+    for (int i = 0; i < ndev; ++i) pre[i] = mark(comms[i], as_stream(streams[i]));
+    const auto untrack = [&] {
+        for (int i = 0; i < ndev; ++i)
+            if (pre[i]) comms[i]->spare.push_back(pre[i]);
+    };
+    ncclResult_t e = rccl().group_start();
+    if (e != ncclSuccess) {
+        untrack();
+        return nccl_fail(e, "ncclGroupStart");
+    }
     for (int i = 0; i < ndev; ++i) {
-        const ncclResult_t e = rccl().gather(send[i], i == root ? recv : nullptr, (size_t)count, ncclFloat64, root,
-                                             comms[i]->nc, as_stream(streams[i]));
+        e = rccl().gather(send[i], i == root ? recv : nullptr, (size_t)count, ncclFloat64, root, comms[i]->nc,
+                          as_stream(streams[i]));
         if (e != ncclSuccess) {
             (void)rccl().group_end();
+            untrack();
             return nccl_fail(e, "ncclGather");
         }
     }
-    PEKF_NCCL(rccl().group_end());
+    e = rccl().group_end();
+    if (e != ncclSuccess) {
+        untrack();
+        return nccl_fail(e, "ncclGroupEnd");
+    }
+    for (int i = 0; i < ndev; ++i)
+        track(comms[i], as_stream(streams[i]), pre[i], mark(comms[i], as_stream(streams[i])), "ncclGather (grouped)");
     return PEKF_OK;
 }
 
@@ -388,8 +573,9 @@ int pekf_allreduce_max_dev(pekf_comm *c, double *buf, int64_t count, void *strea
     PEKF_CHECK_ARG(c && buf, "null pointer");
     PEKF_CHECK_ARG(count >= 0, "negative size");
     PEKF_CHECK_ARG(c->nc, "communicator was aborted");
-    return enqueued(c, rccl().all_reduce(buf, buf, (size_t)count, ncclFloat64, ncclMax, c->nc, as_stream(stream)),
-                    "ncclAllReduce");
+    const hipStream_t s = as_stream(stream);
+    return tracked(c, s, "ncclAllReduce",
+                   [&] { return rccl().all_reduce(buf, buf, (size_t)count, ncclFloat64, ncclMax, c->nc, s); });
 }
 
 }  // extern "C"

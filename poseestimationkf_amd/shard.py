@@ -82,11 +82,13 @@ class Communicator:
         return buf.raw
 
     @classmethod
-    def init_all(cls, devices):
-        """One communicator per device of this process (ncclCommInitAll), rank i on devices[i]."""
+    def init_all(cls, devices, timeout=None):
+        """One communicator per device of this process (ncclCommInitAll), rank i on devices[i], created
+        within `timeout` seconds (default comm_timeout()) or CommTimeoutError (then exit the process)."""
         devs = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
         hs = (ctypes.c_void_p * len(devices))()
-        check(lib.pekf_comm_init_all(len(devices), devs, hs))
+        check(lib.pekf_comm_init_all_timeout(len(devices), devs, comm_timeout() if timeout is None else float(timeout),
+                                             hs))
         return [cls(b"", 0, 0, _handle=hs[i]) for i in range(len(devices))]
 
     def gather(self, send_ptr, count, recv_ptr=None, root=0, stream=None):
@@ -97,8 +99,9 @@ class Communicator:
         check(self._lib.pekf_allreduce_max_dev(self.handle, buf_ptr, int(count), stream))
 
     def wait(self, stream=None, timeout=None):
-        """Drain `stream` (collectives of this communicator included) within the deadline (default
-        comm_timeout()); a peer that never arrives raises CommTimeoutError and aborts the communicator."""
+        """Drain `stream`, collectives of this communicator included.  Each of its collectives gets the
+        deadline (default comm_timeout()) from the moment the stream reaches it, so queued compute is never
+        charged; one a peer never joins raises CommTimeoutError and aborts the communicator."""
         check(self._lib.pekf_comm_wait(self.handle, stream, comm_timeout() if timeout is None else float(timeout)))
 
     def max_over_ranks_array(self, values, stream=None):
@@ -154,20 +157,38 @@ def _proc_start_ticks(pid):
         return 0
 
 
+def _launch_tag(env):
+    """What tells one launch of a job from a relaunch of it with the same key: torchrun's run id (when it
+    is not its "none" default), its restart count (elastic restarts reuse the agent, the ranks' parent)
+    and the master address / port -- those of them the launcher set, all equal on every rank of a launch."""
+    parts = []
+    run_id = env.get("TORCHELASTIC_RUN_ID")
+    if run_id and run_id != "none":
+        parts.append(run_id)
+    for k in ("TORCHELASTIC_RESTART_COUNT", "MASTER_ADDR", "MASTER_PORT"):
+        if env.get(k):
+            parts.append(env[k])
+    return "_".join(parts)
+
+
 class FileRendezvous:
     """Torch-free out-of-band channel for rank 0's 128-byte RCCL id, through a file on the node.
 
     A launcher such as torchrun starts every local rank as a child of one process, so the job's
-    key is (MASTER_ADDR, MASTER_PORT, the parent's pid and start time): unique among the jobs that
-    ever ran on the node, so a file left behind by another job is never read.  Rank 0 writes the id
-    atomically (temp file + rename); the others poll for it.  `key` / PEKF_RDZV_KEY override the key
-    for launchers whose ranks do not share a parent; PEKF_RDZV_DIR names the directory (it must be
-    shared by every rank, e.g. a network file system when ranks span nodes).  A job that spans nodes
-    must name its key: the default (the local parent) differs between nodes, so it is refused there.
+    key is (MASTER_ADDR, MASTER_PORT, the parent's pid and start time, the restart count): unique among
+    the launches that ever ran on the node, so a file left behind by another one is never read.  Rank 0
+    writes the id atomically (temp file + rename); the others poll for it.  `key` / PEKF_RDZV_KEY
+    override the key for launchers whose ranks do not share a parent; the launch tag (torchrun's run id
+    and restart count, MASTER_ADDR / MASTER_PORT, whichever are set) is appended to such a key too, so a
+    relaunch with the same key but a new port or run id never reads the previous launch's file.
+    PEKF_RDZV_DIR names the directory (it must be shared by every rank, e.g. a network file system when
+    ranks span nodes).  A job that spans nodes must name its key: the default (the local parent)
+    differs between nodes, so it is refused there.
     If rank 0 fails before it has an id, `fail(msg)` publishes the failure and the other ranks raise
     at once instead of waiting out `timeout` (PEKF_RDZV_TIMEOUT_S, default 300 s, as PEKF_COMM_TIMEOUT_S).
-    RCCL's communicator creation is itself collective, so after it returns on rank 0 every rank
-    has read the file and `done()` removes it."""
+    Rank 0 removes whatever an earlier launch left under its path when it is constructed (a failure
+    marker, an id whose job died), and `done()` removes its own file once the communicator exists (or
+    its creation failed): RCCL's communicator creation is collective, so every rank has read it by then."""
 
     def __init__(self, rank, world, key=None, directory=None, timeout=None, environ=None):
         env = os.environ if environ is None else environ
@@ -186,9 +207,16 @@ class FileRendezvous:
             ppid = os.getppid()
             key = "%s_%s_%d_%d" % (env.get("MASTER_ADDR", "local"), env.get("MASTER_PORT", "0"),
                                    ppid, _proc_start_ticks(ppid))
+            if env.get("TORCHELASTIC_RESTART_COUNT"):
+                key += "_r" + env["TORCHELASTIC_RESTART_COUNT"]
+        else:
+            tag = _launch_tag(env)
+            key = "%s_%s" % (key, tag) if tag else str(key)
         key = "".join(c if c.isalnum() or c in "-_." else "_" for c in str(key))
         directory = directory or env.get("PEKF_RDZV_DIR") or tempfile.gettempdir()
         self.path = os.path.join(directory, "pekf-rdzv-%s.id" % key)
+        if self.rank == 0 and self.world > 1:
+            self.done()   # a stale file of an earlier launch under this key
 
     def share_id(self, make_id=None):
         """Rank 0 creates the id (make_id(), default a new RCCL id) and publishes it; every rank returns it."""
@@ -253,9 +281,11 @@ def connect(rank, world, rendezvous=None):
     """The RCCL communicator of this process's rank on the current device: rank 0's id shared through
     `rendezvous` (default FileRendezvous(rank, world)), then ncclCommInitRank (collective)."""
     rdzv = rendezvous or FileRendezvous(rank, world)
-    comm = Communicator(rdzv.share_id(), world, rank)
-    rdzv.done()
-    return comm
+    uid = rdzv.share_id()
+    try:
+        return Communicator(uid, world, rank)
+    finally:
+        rdzv.done()   # rank 0: created or failed, the id is spent (a relaunch must not read it)
 
 
 def gather_quaternions(comm: Communicator, x_dev_ptr, batch_local, recv=None, root=0, stream=None):
@@ -275,7 +305,12 @@ class MultiDeviceEKF:
     """A batch of filters split over several GPUs of ONE process (SURVEY.md §8e's single-process
     form): device i holds filters [i*B_local, (i+1)*B_local) as its own IMUWindow + BatchedEKF,
     the launches run concurrently on per-device streams, and the final quaternions come back to
-    the root device with one grouped RCCL gather (pekf_gather_multi_dev)."""
+    the root device with one grouped RCCL gather (pekf_gather_multi_dev).
+
+    It fails instead of hanging, like the one-process-per-GPU path: the communicators are created
+    under the PEKF_COMM_TIMEOUT_S deadline, and sync() drains every device's stream through
+    pekf_comm_wait, so a grouped gather that does not complete within the deadline of its inputs
+    being ready (or an asynchronous RCCL error) aborts every communicator and raises."""
 
     def __init__(self, devices, batch_per_device, window, q=1.0, r=0.1, precision="f64"):
         from . import engine
@@ -326,13 +361,21 @@ class MultiDeviceEKF:
         engine.set_device(self.devices[0])
         return self._recv
 
-    def sync(self):
+    def sync(self, timeout=None):
+        """Drain every device's stream; each collective gets `timeout` (default comm_timeout()) from the
+        moment its device's stream reaches it.  On expiry or an RCCL error every communicator is aborted
+        (the grouped gather's other members would wait for the failed one forever) and the error raised."""
         from . import engine
 
-        for i, d in enumerate(self.devices):
-            engine.set_device(d)
-            self.streams[i].sync()
-        engine.set_device(self.devices[0])
+        try:
+            for i, d in enumerate(self.devices):
+                engine.set_device(d)
+                self.comms[i].wait(self.streams[i].handle, timeout)
+        except Exception:
+            self.abort()
+            raise
+        finally:
+            engine.set_device(self.devices[0])
 
     def gathered(self, root=0):
         """Host copy of the last gather: (n_dev * B_local, 4) float64, rows in filter order."""
@@ -347,3 +390,11 @@ class MultiDeviceEKF:
         for c in self.comms:
             c.close()
         self.comms = []
+
+    def abort(self):
+        """ncclCommAbort on every device's communicator (error paths)."""
+        for c in self.comms:
+            try:
+                c.abort()
+            except Exception:
+                pass

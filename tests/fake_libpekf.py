@@ -11,7 +11,11 @@ shard.py) runs unchanged, and only the ctypes library object is replaced.
   restatement of main_file.py:38-47), so parity against the oracle holds exactly;
 * collectives: pekf_comm_init_all's communicators live in one process (the grouped gather copies);
   pekf_comm_init's go through torch.distributed's gloo backend between processes (gloo stands in for
-  RCCL here, as in test_shard_gloo.py).
+  RCCL here, as in test_shard_gloo.py);
+* failure injection, for the "fail, don't hang" contract: `stuck_devices` -- a grouped gather enqueued
+  on one of these devices never completes, so pekf_comm_wait on it returns PEKF_ERR_TIMEOUT once its
+  deadline has passed (as libpekf's does for a collective whose inputs are ready); `init_all_stalls`
+  -- ncclCommInitAll never returns, so pekf_comm_init_all_timeout times out.
 
 install(monkeypatch_or_none, n_devices) swaps it into _lib / engine / shard.
 """
@@ -43,6 +47,9 @@ class FakeLib:
         self.gloo_port = gloo_port
         self.calls = []              # names of the entry points called, in order
         self.runs = []               # (device, batch, n_steps, step0) of every fused launch
+        self.last_err = b"fake libpekf"
+        self.stuck_devices = set()   # failure injection (module docstring)
+        self.init_all_stalls = False
 
     def _handle(self):
         self.next_handle += 1
@@ -59,7 +66,11 @@ class FakeLib:
         return 1
 
     def pekf_last_error(self):
-        return b"fake libpekf"
+        return self.last_err
+
+    def _fail(self, status, msg):
+        self.last_err = msg.encode()
+        return status
 
     def pekf_device_count(self, n):
         _set(n, self.n_devices)
@@ -173,13 +184,19 @@ class FakeLib:
         self.calls.append("pekf_comm_init")
         return 0
 
-    def pekf_comm_init_all(self, ndev, devs, out):
+    def pekf_comm_init_all_timeout(self, ndev, devs, timeout, out):
+        self.calls.append("pekf_comm_init_all")
+        if self.init_all_stalls:
+            time.sleep(max(0.0, timeout))
+            return self._fail(7, "fake: ncclCommInitAll not done within %.0f s; init abandoned" % timeout)
         for i in range(ndev):
             h = self._handle()
-            self.comms[h] = dict(rank=i, nranks=ndev, device=devs[i], gloo=False)
+            self.comms[h] = dict(rank=i, nranks=ndev, device=devs[i], gloo=False, pending=False)
             out[i] = h
-        self.calls.append("pekf_comm_init_all")
         return 0
+
+    def pekf_comm_init_all(self, ndev, devs, out):
+        return self.pekf_comm_init_all_timeout(ndev, devs, 300.0, out)
 
     def pekf_comm_rank(self, h, r, n, d):
         c = self.comms[h]
@@ -189,8 +206,8 @@ class FakeLib:
         return 0
 
     def pekf_comm_destroy(self, h):
-        c = self.comms.pop(h)
-        if c["gloo"]:
+        c = self.comms.pop(h, None)
+        if c is not None and c["gloo"]:
             import torch.distributed as dist
             dist.destroy_process_group()
         return 0
@@ -198,6 +215,14 @@ class FakeLib:
     pekf_comm_abort = pekf_comm_destroy
 
     def pekf_comm_wait(self, h, stream, timeout):
+        c = self.comms.get(h)
+        if c is None:
+            return self._fail(1, "fake: null or aborted communicator")
+        if c.get("pending") and c["device"] in self.stuck_devices:
+            time.sleep(max(0.0, timeout))
+            self.comms.pop(h)
+            return self._fail(7, "fake: rank %d of %d: ncclGather (grouped) did not complete within %.0f s of its "
+                                 "inputs being ready; communicator aborted" % (c["rank"], c["nranks"], timeout))
         return 0
 
     def pekf_gather_dev(self, h, send, count, recv, root, stream):
@@ -230,6 +255,7 @@ class FakeLib:
         for i in range(ndev):
             assert self.comms[comms[i]]["rank"] == i
             out[i] = self._view(send[i], 8 * count, np.float64)
+            self.comms[comms[i]]["pending"] = True
         self.calls.append("pekf_gather_multi_dev")
         return 0
 

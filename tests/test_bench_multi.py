@@ -7,7 +7,10 @@ code the driver's 8-GPU run executes:
   grouped gather per step);
 * one process per rank (`torchrun ... bench.py --gpus 2` and `--gpus 4`: FileRendezvous, RCCL init, per-step
   gather, max-over-ranks time, per-GPU timings exchanged by one all-reduce);
-* rank 0 failing before it has an RCCL id: the other rank stops waiting and exits 2 at once.
+* rank 0 failing before it has an RCCL id: the other rank stops waiting and exits 2 at once;
+* the one-process mode failing instead of hanging: a grouped gather that never completes on one of
+  the 8 devices, or an ncclCommInitAll that never returns, ends bench.py with status 2 within the
+  PEKF_COMM_TIMEOUT_S deadline, one stderr line and nothing on stdout.
 
 Filters are independent (PKF/ExtendedKalmanFilter.py:6-80), so each shard's rows must equal the
 oracle's run of those global filter ids (main_file.py:38-47's loop), wherever they were computed."""
@@ -58,7 +61,8 @@ def _check_line(d, world, batch=256):
     assert cpu is not None and cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["share_source"]
     assert len(d["kernel_ms_per_gpu"]) == world and all(v > 0 for v in d["kernel_ms_per_gpu"])
     assert len(d["gather_ms_per_gpu"]) == world and all(v >= 0 for v in d["gather_ms_per_gpu"])
-    assert d["roofline"]["kernel_ms"] == pytest.approx(float(np.mean(d["kernel_ms_per_gpu"])))
+    assert d["roofline"]["kernel_ms"] == pytest.approx(float(np.max(d["kernel_ms_per_gpu"])))
+    assert d["roofline"]["kernel_ms_mean_over_gpus"] == pytest.approx(float(np.mean(d["kernel_ms_per_gpu"])))
 
 
 def test_one_process_eight_devices(monkeypatch, capfd):
@@ -120,7 +124,7 @@ def _run_ranks(tmp_path, world, n_devices_of=lambda r: 1, timeout=240):
     return codes, texts, time.monotonic() - t0
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_ranks_one_process_each(tmp_path, world):
     """`torchrun --nproc-per-node N bench.py --gpus N`: N processes, rank 0 prints the one line."""
     codes, texts, _ = _run_ranks(tmp_path, world)
@@ -139,6 +143,62 @@ def test_rank0_failure_releases_the_other_ranks(tmp_path):
     assert codes == [2, 2], (codes, texts)
     assert texts == ["", ""]
     assert wall < 100
+
+
+def _plain_main(env, out_path, err_path, t_path, stuck_devices, init_all_stalls):
+    """`bench.py --gpus 8` launched plainly (one process over 8 fake devices) with a fault injected."""
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    os.environ.update(env)
+    sys.path.insert(0, ROOT)
+    from tests import fake_libpekf
+    fake = fake_libpekf.install(None, n_devices=8)
+    fake.stuck_devices = set(stuck_devices)
+    fake.init_all_stalls = init_all_stalls
+    for fd, path in ((1, out_path), (2, err_path)):
+        os.dup2(os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC), fd)
+    import bench
+    with open(t_path, "w") as fh:
+        fh.write(repr(time.monotonic()))
+    code = 0
+    try:
+        bench.main(["--gpus", "8", "--cpu-baseline", "none"] + SMALL)
+    except SystemExit as e:
+        code = e.code if isinstance(e.code, int) else 1
+    sys.stdout.flush()
+    os._exit(code)
+
+
+@pytest.mark.parametrize("fault", ["gather_on_device_5", "init_all"])
+def test_one_process_fails_instead_of_hanging(tmp_path, fault):
+    """The plain `bench.py --gpus 8` (MultiDeviceEKF) with a collective that never completes: a grouped
+    gather stuck on device 5 (MultiRun.sync -> MultiDeviceEKF.sync -> pekf_comm_wait per device), or an
+    ncclCommInitAll that never returns (pekf_comm_init_all_timeout).  bench.py exits 2 within the 2 s
+    PEKF_COMM_TIMEOUT_S deadline plus its own start-up, with one error line and nothing on stdout."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    out, err, tp = (str(tmp_path / n) for n in ("out", "err", "t0"))
+    p = ctx.Process(target=_plain_main, args=({"PEKF_COMM_TIMEOUT_S": "2"}, out, err, tp,
+                                              [5] if fault == "gather_on_device_5" else [], fault == "init_all"))
+    p.start()
+    p.join(timeout=120)
+    t_end = time.monotonic()
+    if p.exitcode is None:
+        p.kill()
+    with open(err) as fh:
+        err_text = fh.read()
+    assert p.exitcode == 2, err_text
+    with open(tp) as fh:
+        t0 = float(fh.read())
+    assert 2.0 <= t_end - t0 < 15, (t_end - t0, err_text)
+    with open(out) as fh:
+        assert fh.read() == ""
+    failed = [l for l in err_text.splitlines() if "collective failed" in l]
+    assert len(failed) == 1, err_text
+    if fault == "init_all":
+        assert "ncclCommInitAll not done within 2 s" in failed[0]
+    else:
+        assert "did not complete within 2 s" in failed[0] and "rank 5 of 8" in failed[0]
 
 
 def test_cpu_share_from_cgroup_v2(tmp_path):

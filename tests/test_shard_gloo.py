@@ -90,12 +90,14 @@ def test_default_key_is_shared_by_siblings_only(monkeypatch):
     monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
     monkeypatch.setenv("MASTER_PORT", "29999")
     monkeypatch.delenv("PEKF_RDZV_KEY", raising=False)
+    for k in ("TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT"):
+        monkeypatch.delenv(k, raising=False)
     a, b = shard.FileRendezvous(0, 2), shard.FileRendezvous(1, 2)
     assert a.path == b.path and str(os.getppid()) in a.path
     monkeypatch.setenv("MASTER_PORT", "29998")
     assert shard.FileRendezvous(1, 2).path != a.path
     monkeypatch.setenv("PEKF_RDZV_KEY", "k/../x")
-    assert os.path.basename(shard.FileRendezvous(1, 2).path) == "pekf-rdzv-k_.._x.id"
+    assert os.path.basename(shard.FileRendezvous(1, 2).path) == "pekf-rdzv-k_.._x_127.0.0.1_29998.id"
 
 
 def test_file_rendezvous_under_torchrun(tmp_path):
@@ -184,3 +186,42 @@ def test_rendezvous_multinode_needs_a_key_and_rank0_failure_is_published(tmp_pat
         r1.share_id()
     assert time.monotonic() - t0 < 5
     assert shard.FileRendezvous(0, 2, key="t", directory=str(tmp_path), environ={"PEKF_RDZV_TIMEOUT_S": "7"}).timeout == 7
+
+
+def test_rendezvous_relaunch_with_the_same_key_after_a_failure(tmp_path):
+    """A launch whose rank 0 failed leaves its failure marker behind.  A relaunch with the same
+    PEKF_RDZV_KEY never reads it: a new master port or torchrun run id / restart count gives the
+    launch its own file, and with everything equal the new rank 0 removes the stale file when it starts."""
+    d = str(tmp_path)
+    env1 = {"PEKF_RDZV_KEY": "job7", "MASTER_ADDR": "10.0.0.1", "MASTER_PORT": "29500",
+            "TORCHELASTIC_RUN_ID": "none", "TORCHELASTIC_RESTART_COUNT": "0"}
+    shard.FileRendezvous(0, 2, directory=d, environ=env1).fail("BenchError: no GPU")
+    stale = shard.FileRendezvous(1, 2, directory=d, environ=env1, timeout=0.2)
+    assert os.path.basename(stale.path) == "pekf-rdzv-job7_0_10.0.0.1_29500.id" and os.path.exists(stale.path)
+    for change in ({"MASTER_PORT": "29501"}, {"TORCHELASTIC_RESTART_COUNT": "1"}, {"TORCHELASTIC_RUN_ID": "abc"}):
+        r1 = shard.FileRendezvous(1, 2, directory=d, environ=dict(env1, **change), timeout=0.2)
+        assert r1.path != stale.path
+        with pytest.raises(TimeoutError):     # waits for its own launch's rank 0, not the stale marker
+            r1.share_id()
+    # the identical relaunch: its rank 0 removes the marker at start, then publishes a fresh id
+    r0 = shard.FileRendezvous(0, 2, directory=d, environ=env1)
+    assert not os.path.exists(stale.path)
+    assert r0.share_id(make_id=lambda: ID) == ID
+    assert shard.FileRendezvous(1, 2, directory=d, environ=env1, timeout=5).share_id() == ID
+
+
+def test_connect_removes_the_id_when_communicator_creation_fails(tmp_path, monkeypatch):
+    """Rank 0's published id is removed even when its communicator creation raises (an init timeout,
+    after which bench.py leaves with os._exit), so a relaunch cannot read a spent id."""
+    class Boom(RuntimeError):
+        pass
+
+    def failing_init(self, uid, nranks, rank, _handle=None):
+        raise Boom("init timed out")
+
+    monkeypatch.setattr(shard.Communicator, "__init__", failing_init)
+    r0 = shard.FileRendezvous(0, 2, key="jobC", directory=str(tmp_path), environ={})
+    monkeypatch.setattr(shard.Communicator, "unique_id", staticmethod(lambda: ID))
+    with pytest.raises(Boom):
+        shard.connect(0, 2, r0)
+    assert not os.path.exists(r0.path)
