@@ -26,6 +26,9 @@ typedef float nv4f __attribute__((ext_vector_type(4)));  // the native vector th
 #ifndef PEKF_INIT_NTL
 #define PEKF_INIT_NTL 1
 #endif
+// Queue depth: 10 rows = 25.6 KB of LDS per 64-lane block, tuned on gfx950's 160 KB of LDS per CU
+// (~6 blocks per CU); the library is built for gfx950 only (Makefile ARCH).  A 64 KB-LDS part would cap
+// this at 2 blocks per CU: re-measure the depth (or 0, the unstaged form) before building for one.
 #ifndef PEKF_FE_STAGE
 #define PEKF_FE_STAGE 10
 #endif
