@@ -239,6 +239,7 @@ int pekf_frontend_dev(int64_t batch, int64_t n_events, const void *ev_planes, co
  * event is skipped and the clock does not move, at no cost to the event loop). */
 #define PEKF_EV_TIME 3u
 #define PEKF_EV_TIME_EVENTS 0x1u
+#define PEKF_EV_F32_RECORDS 0x2u /* pekf_live_ext_dev: records rounded to the f32 stream record format */
 /* pekf_frontend_dev with time events (flags) and escaped records: a record whose dt does not fit the
  * dt word gets PEKF_DT_ESCAPE and its float64 dt in dt_ext[r_max][batch] (the window's dt side plane for
  * pekf_run_ext_dev; only escaped entries are written), and *dev_error |= 4 says some record was escaped.
@@ -254,15 +255,19 @@ int pekf_frontend_ext_dev(int64_t batch, int64_t n_events, const void *ev_planes
  * and refs as pekf_frontend_dev; X[batch*4], P[batch*16] (AoS, FP64) are the filters' state, read at
  * the start and written at the end (left untouched for a filter with no record, as for one whose init
  * is not finite: phase 2 never got ready); q, r as pekf_run_dev.
- * counts[b] receives the number of records filter b applied.  The final state equals pekf_frontend_dev
- * followed by pekf_run_dev with those counts, bit for bit.  A record whose dt does not fit the dt word
+ * counts[b] receives the number of records filter b applied.  A record's acc / mag reach the filter as
+ * the FP64 low-pass outputs, as the server hands them to its filter (KFS/KalmanFilter.cpp:279-303); with
+ * PEKF_EV_F32_RECORDS (pekf_live_ext_dev) they are rounded to f32 first, as in the 40 B stream record,
+ * and the final state then equals pekf_frontend_dev followed by pekf_run_dev with those counts, bit for
+ * bit.  A record whose dt does not fit the dt word
  * keeps its float64 dt beside it on the lane (as pekf_frontend_ext_dev + pekf_run_ext_dev would), so any
  * gap is applied; dev_error is kept for the ABI and never set by this kernel (no r_max either: there is
  * no record window). */
 int pekf_live_dev(int64_t batch, int64_t n_events, const void *ev_planes, const double *init,
                   const int64_t *t_init, double alpha, double *X, double *P, double q, double r,
                   int32_t *counts, double *refs, int *dev_error, void *stream);
-/* pekf_live_dev with flags (PEKF_EV_TIME_EVENTS: the planes hold time events). */
+/* pekf_live_dev with flags (PEKF_EV_TIME_EVENTS: the planes hold time events; PEKF_EV_F32_RECORDS: f32
+ * records, the split pipeline's). */
 int pekf_live_ext_dev(int64_t batch, int64_t n_events, const void *ev_planes, const double *init,
                       const int64_t *t_init, double alpha, double *X, double *P, double q, double r,
                       int32_t *counts, double *refs, uint32_t flags, int *dev_error, void *stream);

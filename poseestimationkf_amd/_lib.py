@@ -26,6 +26,7 @@ RUN_MIXED_PRECISION = 0x1
 RUN_STATE_SOA = 0x2
 DT_ESCAPE = 0x7FFFFFFF
 EV_TIME_EVENTS = 0x1
+EV_F32_RECORDS = 0x2
 
 
 class PekfError(RuntimeError):

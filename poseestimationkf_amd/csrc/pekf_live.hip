@@ -3,7 +3,11 @@
 // Parser::WriteKalmanFilterMeasurement / ExecuteKalmanFilter, KFS/Parser.cpp:148-267) -> Prediction +
 // Correction of each record (pekf_step.hpp, ExtendedKalmanFilter.py:58-80 as main_file.py:42-45 calls
 // them).  One lane per filter holds its front-end state, X and covariance in registers; records never
-// touch memory.  The split pipeline -- pekf_frontend_dev writing records to the stream planes, then
+// touch memory.  A record's acc / mag stay the FP64 low-pass outputs (the server's filter input,
+// KFS/KalmanFilter.cpp:279-303) in a 4-deep queue; PEKF_EV_F32_RECORDS rounds them to the f32 stream
+// record in a 6-deep queue instead -- the same 18 KB of LDS per wave -- and then equals the split
+// pipeline bit for bit.  FP64 costs +2.4-3.0 % (4.77 -> 4.88 ms at 1M filters x 1,024 events, same-box
+// ABBA, profiles/r5/live_records/): the shallower queue runs ~11 % more filter steps.  The split pipeline -- pekf_frontend_dev writing records to the stream planes, then
 // pekf_run_dev with counts reading them back -- pays a 40 B record write that scatters into 96 B of
 // sectors (each lane's record count drifts, so a wave's stores land in 64 different rows) plus the
 // 40 B read; here the only HBM traffic is the 16 B event.
@@ -18,7 +22,7 @@
 // last event (scripts/live_queue_sim.py: 0.79 of the lanes busy per step at 3 / 6 / 56 against 0.28
 // when every block drains).  Per lane the records apply in order with the same arithmetic as
 // pekf_run_dev's multi-record kernel (reference basis, N, omod), so the final state equals the split
-// pipeline's bit for bit.
+// pipeline's bit for bit (with f32 records; with FP64 ones, within FP64 rounding of the unrounded chain).
 #include "pekf_phase3.hpp"
 #include "pekf_step.hpp"
 
@@ -37,7 +41,10 @@ namespace pekf {
 #define PEKF_LIVE_NTL 1  // non-temporal event loads: each event is read once (-1.4 %, profiles/r4/ntload/)
 #endif
 #ifndef PEKF_LIVE_QUEUE
-#define PEKF_LIVE_QUEUE 6  // records a lane can hold (40 B of LDS each)
+#define PEKF_LIVE_QUEUE 6  // records a lane can hold (48 B of LDS each: the 40 B record + its escaped dt)
+#endif
+#ifndef PEKF_LIVE_QUEUE64
+#define PEKF_LIVE_QUEUE64 4  // the same with FP64 acc / mag (72 B each): the same 18 KB of LDS per wave
 #endif
 #ifndef PEKF_LIVE_QUORUM
 #define PEKF_LIVE_QUORUM 56  // lanes of 64 with a queued record that trigger a filter step
@@ -95,21 +102,30 @@ struct PendLds {
 // float64 dt in the slot's side entry dt[slot][lane], written and read only for such a record.
 template <int Q>
 struct LdsQueue {
+    static constexpr size_t kBytes = (sizeof(float4) * 2 + sizeof(float2) + sizeof(double)) * Q * kRunBlock;
     float4 (*gd)[kRunBlock];
     float4 (*am)[kRunBlock];
     float2 (*my)[kRunBlock];
     double (*dt)[kRunBlock];
     int head = 0, n = 0;
+    __device__ __forceinline__ void bind(unsigned char *lds) {
+        gd = reinterpret_cast<float4(*)[kRunBlock]>(lds);
+        am = reinterpret_cast<float4(*)[kRunBlock]>(lds + sizeof(float4) * Q * kRunBlock);
+        dt = reinterpret_cast<double(*)[kRunBlock]>(lds + 2 * sizeof(float4) * Q * kRunBlock);
+        my = reinterpret_cast<float2(*)[kRunBlock]>(lds + (2 * sizeof(float4) + sizeof(double)) * Q * kRunBlock);
+    }
+    __device__ __forceinline__ int tail() const { return head + n < Q ? head + n : head + n - Q; }
     __device__ __forceinline__ void push(const Rec &r, bool esc, double dtv) {
-        const int slot = head + n < Q ? head + n : head + n - Q;
+        const int slot = tail();
         gd[slot][threadIdx.x] = r.gd;
         am[slot][threadIdx.x] = r.am;
         my[slot][threadIdx.x] = r.my;
         if (esc) dt[slot][threadIdx.x] = dtv;
         ++n;
     }
+    using Slot = Rec;
     // the oldest record and its dt in ns
-    __device__ __forceinline__ Rec pop(double &dtv) {
+    __device__ __forceinline__ Slot pop(double &dtv) {
         const Rec r = {gd[head][threadIdx.x], am[head][threadIdx.x], my[head][threadIdx.x]};
         const uint32_t word = __float_as_uint(r.gd.w) & PEKF_DT_MASK;
         dtv = (double)word;
@@ -120,15 +136,82 @@ struct LdsQueue {
         }
         return r;
     }
+    static __device__ __forceinline__ void unpack(const Slot &r, double (&gy)[3], double (&acc)[3], double (&mag)[3]) {
+        gy[0] = r.gd.x; gy[1] = r.gd.y; gy[2] = r.gd.z;
+        acc[0] = r.am.x; acc[1] = r.am.y; acc[2] = r.am.z;
+        mag[0] = r.am.w; mag[1] = r.my.x; mag[2] = r.my.y;
+    }
+    // the popped record's acc / mag again (it stays in its slot, the one before head, until a later push)
+    __device__ __forceinline__ void reload(double *a, double *m) const {
+        const int slot = head == 0 ? Q - 1 : head - 1;
+        const float4 va = am[slot][threadIdx.x];
+        const float2 vm = my[slot][threadIdx.x];
+        a[0] = va.x; a[1] = va.y; a[2] = va.z;
+        m[0] = va.w; m[1] = vm.x; m[2] = vm.y;
+    }
 };
 
-// TE: the event planes may hold time events (Phase3::event).
-template <bool TE>
+// The queue with FP64 acc / mag: what the server's filter receives (KFS/KalmanFilter.cpp:279-303 hands
+// the double low-pass outputs to Prediction / Correction), not the f32 stream record.  Per slot the
+// gyro / dt word (16 B), acc and mag as three double2 planes (48 B) and the escaped dt (8 B).
+template <int Q>
+struct LdsQueue64 {
+    static constexpr size_t kBytes = (sizeof(float4) + 3 * sizeof(double2) + sizeof(double)) * Q * kRunBlock;
+    float4 (*gd)[kRunBlock];
+    double2 (*am)[3][kRunBlock];  // {acc.x, acc.y}, {acc.z, mag.x}, {mag.y, mag.z}
+    double (*dt)[kRunBlock];
+    int head = 0, n = 0;
+    __device__ __forceinline__ void bind(unsigned char *lds) {
+        am = reinterpret_cast<double2(*)[3][kRunBlock]>(lds);
+        gd = reinterpret_cast<float4(*)[kRunBlock]>(lds + 3 * sizeof(double2) * Q * kRunBlock);
+        dt = reinterpret_cast<double(*)[kRunBlock]>(lds + (3 * sizeof(double2) + sizeof(float4)) * Q * kRunBlock);
+    }
+    __device__ __forceinline__ void push(const float4 &g, const V3 &a, const V3 &m, bool esc, double dtv) {
+        const int slot = head + n < Q ? head + n : head + n - Q;
+        gd[slot][threadIdx.x] = g;
+        am[slot][0][threadIdx.x] = make_double2(a.x, a.y);
+        am[slot][1][threadIdx.x] = make_double2(a.z, m.x);
+        am[slot][2][threadIdx.x] = make_double2(m.y, m.z);
+        if (esc) dt[slot][threadIdx.x] = dtv;
+        ++n;
+    }
+    struct Slot {
+        float4 gd;
+        double2 v[3];
+    };
+    __device__ __forceinline__ Slot pop(double &dtv) {
+        const Slot r = {gd[head][threadIdx.x], {am[head][0][threadIdx.x], am[head][1][threadIdx.x], am[head][2][threadIdx.x]}};
+        const uint32_t word = __float_as_uint(r.gd.w) & PEKF_DT_MASK;
+        dtv = (double)word;
+        if (word == PEKF_DT_ESCAPE) dtv = dt[head][threadIdx.x];
+        if (n > 0) {
+            head = head + 1 < Q ? head + 1 : 0;
+            --n;
+        }
+        return r;
+    }
+    static __device__ __forceinline__ void unpack(const Slot &r, double (&gy)[3], double (&acc)[3], double (&mag)[3]) {
+        gy[0] = r.gd.x; gy[1] = r.gd.y; gy[2] = r.gd.z;
+        acc[0] = r.v[0].x; acc[1] = r.v[0].y; acc[2] = r.v[1].x;
+        mag[0] = r.v[1].y; mag[1] = r.v[2].x; mag[2] = r.v[2].y;
+    }
+    __device__ __forceinline__ void reload(double *a, double *m) const {
+        const int slot = head == 0 ? Q - 1 : head - 1;
+        const double2 v0 = am[slot][0][threadIdx.x], v1 = am[slot][1][threadIdx.x], v2 = am[slot][2][threadIdx.x];
+        a[0] = v0.x; a[1] = v0.y; a[2] = v1.x;
+        m[0] = v1.y; m[1] = v2.x; m[2] = v2.y;
+    }
+};
+
+// TE: the event planes may hold time events (Phase3::event).  R64: records keep their FP64 acc / mag
+// (LdsQueue64); otherwise they are the f32 stream records pekf_frontend_dev writes (LdsQueue).
+template <bool TE, bool R64>
 __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
     int64_t batch, int64_t n_events, const float4 *__restrict__ ev, const double *__restrict__ init,
     const int64_t *__restrict__ t_init, double alpha, double qs, double rs, double *__restrict__ Xio,
     double *__restrict__ Pio, int32_t *__restrict__ counts, double *__restrict__ refs) {
-    constexpr int kRing = PEKF_LIVE_RING, kFlush = 3, kQueue = PEKF_LIVE_QUEUE, kQuorum = PEKF_LIVE_QUORUM;
+    constexpr int kRing = PEKF_LIVE_RING, kFlush = 3, kQuorum = PEKF_LIVE_QUORUM;
+    constexpr int kQueue = R64 ? PEKF_LIVE_QUEUE64 : PEKF_LIVE_QUEUE;
     constexpr int kPush = kRing / kFlush;  // records a lane can complete within one block
     static_assert(kRing % kFlush == 0, "the ring depth must be a multiple of the emit period");
     static_assert(kQueue >= kPush, "the queue must hold a block's records");
@@ -161,11 +244,10 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
     }
     const StepK<double> kc = step_consts<double, true>(qs, rs);
 
-    __shared__ float4 q_gd[kQueue][kRunBlock], q_am[kQueue][kRunBlock];
-    __shared__ float2 q_my[kQueue][kRunBlock];
-    __shared__ double q_dt[kQueue][kRunBlock];
-    LdsQueue<kQueue> queue;
-    queue.gd = q_gd; queue.am = q_am; queue.my = q_my; queue.dt = q_dt;
+    using Queue = std::conditional_t<R64, LdsQueue64<kQueue>, LdsQueue<kQueue>>;
+    __shared__ __attribute__((aligned(16))) unsigned char q_lds[Queue::kBytes];
+    Queue queue;
+    queue.bind(q_lds);
     int32_t applied = 0;
     // One filter step for every lane with a queued record: its oldest, Prediction + Correction with
     // the multi-record kernel's arithmetic (the first record of the launch from the loaded |X|^2,
@@ -173,21 +255,13 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
     auto filter_step = [&]() {
         const bool has = queue.n > 0;
         double dt;
-        const Rec cur = queue.pop(dt);
-        auto reload = [&](double *a, double *m) {  // rare: the degenerate-Wahba fallback
-            // the popped record stays in its slot (the one before head) until a later push
-            const int slot = queue.head == 0 ? kQueue - 1 : queue.head - 1;
-            const float4 va = q_am[slot][threadIdx.x];
-            const float2 vm = q_my[slot][threadIdx.x];
-            a[0] = va.x; a[1] = va.y; a[2] = va.z;
-            m[0] = va.w; m[1] = vm.x; m[2] = vm.y;
-        };
+        const typename Queue::Slot cur = queue.pop(dt);
+        auto reload = [&](double *a, double *m) { queue.reload(a, m); };  // rare: the degenerate-Wahba fallback
         OmodMode mode;
         mode.enter();
         if (has) {
-            const double gy[3] = {cur.gd.x, cur.gd.y, cur.gd.z};
-            const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
-            const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
+            double gy[3], acc[3], mag[3];
+            Queue::unpack(cur, gy, acc, mag);
             constexpr bool kPin = PEKF_LIVE_PIN != 0;
             if (applied == 0)
                 ekf_record_step<double, true, false, true, kPin>(x, state_norm2(x), P, Wr, kc, gy, dt, false, acc, mag,
@@ -197,6 +271,17 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
             ++applied;
         }
         mode.leave();
+    };
+    // the pending record (captured by Phase3::event) into the queue
+    auto push_pending = [&](const RawRec &q) {
+        bool esc;
+        if constexpr (R64) {
+            const float4 g = fe.emit_lpf(q, esc);
+            if (ready) queue.push(g, fe.lpf_acc, fe.lpf_mag, esc, q.dt);
+        } else {
+            const Rec rc = fe.emit(q, esc);
+            if (ready) queue.push(rc, esc, q.dt);
+        }
     };
 #if PEKF_LIVE_PEND_LDS
     __shared__ float p_f[15][kRunBlock];
@@ -213,19 +298,15 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
     auto flush = [&]() {
         if (pend) {
             pend = false;
-            const RawRec q = pend_lds.get();
-            bool esc;
-            const Rec rc = fe.emit(q, esc);
-            if (ready) queue.push(rc, esc, q.dt);
+            push_pending(pend_lds.get());
         }
     };
 #else
     auto on_event = [&](const float4 v4) { fe.event<TE>(v4); };
     auto flush = [&]() {
         if (fe.pend) {
-            bool esc;
-            const Rec rc = fe.emit(esc);
-            if (ready) queue.push(rc, esc, fe.p.dt);
+            fe.pend = false;
+            push_pending(fe.p);
         }
     };
 #endif
@@ -298,7 +379,7 @@ extern "C" int pekf_live_ext_dev(int64_t batch, int64_t n_events, const void *ev
                                  const int64_t *t_init, double alpha, double *X, double *P, double q, double r,
                                  int32_t *counts, double *refs, uint32_t flags, int *dev_error, void *stream) {
     PEKF_CHECK_ARG(batch >= 0 && n_events >= 0, "negative size");
-    PEKF_CHECK_ARG((flags & ~PEKF_EV_TIME_EVENTS) == 0, "unknown flags");
+    PEKF_CHECK_ARG((flags & ~(PEKF_EV_TIME_EVENTS | PEKF_EV_F32_RECORDS)) == 0, "unknown flags");
     if (batch == 0) return PEKF_OK;
     PEKF_CHECK_ARG(batch < ((int64_t)1 << 28), "batch must be < 2^28 filters per launch");
     PEKF_CHECK_ARG(n_events < ((int64_t)1 << 30), "n_events must be < 2^30 per launch");
@@ -308,12 +389,15 @@ extern "C" int pekf_live_ext_dev(int64_t batch, int64_t n_events, const void *ev
     (void)dev_error;  // every record's dt is applied (escaped ones from the queue's side entries)
     const auto *ev = static_cast<const float4 *>(ev_planes);
     const dim3 grid(grid_for(batch, kRunBlock)), block(kRunBlock);
-    if (flags & PEKF_EV_TIME_EVENTS)
-        hipLaunchKernelGGL(k_live<true>, grid, block, 0, as_stream(stream), batch, n_events, ev, init, t_init, alpha, q,
-                           r, X, P, counts, refs);
+    const bool te = (flags & PEKF_EV_TIME_EVENTS) != 0, r64 = (flags & PEKF_EV_F32_RECORDS) == 0;
+    auto launch = [&](auto kernel) {
+        hipLaunchKernelGGL(kernel, grid, block, 0, as_stream(stream), batch, n_events, ev, init, t_init, alpha, q, r, X,
+                           P, counts, refs);
+    };
+    if (te)
+        r64 ? launch(k_live<true, true>) : launch(k_live<true, false>);
     else
-        hipLaunchKernelGGL(k_live<false>, grid, block, 0, as_stream(stream), batch, n_events, ev, init, t_init, alpha,
-                           q, r, X, P, counts, refs);
+        r64 ? launch(k_live<false, true>) : launch(k_live<false, false>);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_live");
     return PEKF_OK;

@@ -7,8 +7,9 @@
 // ExecuteKalmanFilter (Parser.cpp:229-257): acc / mag interpolated to the gyro time (:259-267),
 // normalised (:221-228), low-pass filtered (alpha, from a zero state: KalmanFilter.cpp:16-18,21-24,
 // 279-303), dt = gyro time - the previous record's (KalmanFilter.cpp:306-308).  FP64 arithmetic (one
-// reciprocal / rsqrt with a Newton step instead of IEEE divisions: ~1e-15 relative), records rounded
-// to f32 like every record of the stream.  The arithmetic is contracted as the compiler's default
+// reciprocal / rsqrt with a Newton step instead of IEEE divisions: ~1e-15 relative).  Records for the
+// stream planes are rounded to f32 like every record of the stream (emit); k_live can take the low-pass
+// outputs in FP64 instead (emit_lpf + lpf_acc / lpf_mag), as the server hands them to its filter.  The arithmetic is contracted as the compiler's default
 // (fp contract fast) whatever the including file is compiled with: every function with arithmetic
 // opens with that pragma, so k_live's records are k_frontend's.
 #pragma once
@@ -192,6 +193,11 @@ struct Phase3 {
         pend = false;
         return emit(p, esc);
     }
+    // the same with the low-pass outputs left in FP64 (lpf_acc / lpf_mag)
+    __device__ __forceinline__ float4 emit_lpf(bool &esc) {
+        pend = false;
+        return emit_lpf(p, esc);
+    }
 
     // The low-pass step l <- alpha x + beta l (KalmanFilter.cpp:285,298), rounded as fma(beta, l, alpha x)
     // -- the contraction the compiler chose for the expression -- but written into l's own register: the
@@ -202,10 +208,11 @@ struct Phase3 {
         asm("v_fma_f64 %0, %1, %0, %2" : "+v"(l) : "v"(beta), "v"(ax));
     }
 
-    // A captured record, in the order they complete: interpolation, normalisation, low-pass, f32
-    // packing.  esc: its dt does not fit the dt word (not in [0, 2^31 - 1) ns): the word is
-    // PEKF_DT_ESCAPE and the caller keeps q.dt beside the record (pekf.h).
-    __device__ __forceinline__ Rec emit(const RawRec &q, bool &esc) {
+    // A captured record, in the order they complete: interpolation, normalisation, low-pass (the FP64
+    // results stay in lpf_acc / lpf_mag), and the gyro / dt half of the record, which is returned.
+    // esc: its dt does not fit the dt word (not in [0, 2^31 - 1) ns): the word is PEKF_DT_ESCAPE and
+    // the caller keeps q.dt beside the record (pekf.h).
+    __device__ __forceinline__ float4 emit_lpf(const RawRec &q, bool &esc) {
 #pragma clang fp contract(fast)
         // Parser::LinearInterpolationSensor (:259-267): (y2 - y1) / (t2 - t1) * (t3 - t1) + y1, the
         // division taken as one reciprocal.  Timestamps are integer ns held in doubles (exact below
@@ -224,9 +231,14 @@ struct Phase3 {
         lpf_step(lpf_mag.x, m.x); lpf_step(lpf_mag.y, m.y); lpf_step(lpf_mag.z, m.z);
         lpf_step(lpf_acc.x, a.x); lpf_step(lpf_acc.y, a.y); lpf_step(lpf_acc.z, a.z);
         esc = !(q.dt >= 0.0 && q.dt < (double)PEKF_DT_ESCAPE);
-        Rec r;
-        r.gd = make_float4((float)q.gyro.x, (float)q.gyro.y, (float)q.gyro.z,
+        return make_float4((float)q.gyro.x, (float)q.gyro.y, (float)q.gyro.z,
                            __uint_as_float(esc ? PEKF_DT_ESCAPE : (uint32_t)q.dt));
+    }
+
+    // The 40 B stream record (acc / mag rounded to f32, as every record of the stream planes).
+    __device__ __forceinline__ Rec emit(const RawRec &q, bool &esc) {
+        Rec r;
+        r.gd = emit_lpf(q, esc);
         r.am = make_float4((float)lpf_acc.x, (float)lpf_acc.y, (float)lpf_acc.z, (float)lpf_mag.x);
         r.my = make_float2((float)lpf_mag.y, (float)lpf_mag.z);
         return r;

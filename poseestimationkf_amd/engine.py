@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 from . import synth
-from ._lib import EV_TIME_EVENTS, RUN_MIXED_PRECISION, RUN_STATE_SOA, check, dptr, f64, lib
+from ._lib import EV_F32_RECORDS, EV_TIME_EVENTS, RUN_MIXED_PRECISION, RUN_STATE_SOA, check, dptr, f64, lib
 
 
 # ------------------------------------------------------------------ device plumbing
@@ -335,12 +335,21 @@ def frontend_init(ev, n_avg=100, stats=True):
     return out
 
 
-def run_session(phase2, phase3, filters, n_avg=100, alpha=0.1):
+def _record_flags(records):
+    """pekf_live_ext_dev's record precision: "f64" (the low-pass acc / mag as the server's filter gets them,
+    KFS/KalmanFilter.cpp:279-303) or "f32" (the 40 B stream record, as the split pipeline's)."""
+    if records not in ("f64", "f32"):
+        raise ValueError("records must be 'f64' or 'f32'")
+    return EV_F32_RECORDS if records == "f32" else 0
+
+
+def run_session(phase2, phase3, filters, n_avg=100, alpha=0.1, records="f64"):
     """A whole client session of the server on the device (KFS/Parser.cpp:28-72): phase-2 events ->
     initial means and start time (pekf_frontend_init_dev) -> phase-3 events -> records -> the filters'
     state (pekf_live_dev), the phase-2 results handed over in device memory.  phase3's times continue
     phase2's (its first gap is taken from phase2's last event, the time phase 3 starts from).
-    filters: a BatchedEKF (FP64, AoS) whose state is advanced.  Returns dict(ready (K,) bool -- a filter
+    filters: a BatchedEKF (FP64, AoS) whose state is advanced; records as BatchedEKF.run_events.
+    Returns dict(ready (K,) bool -- a filter
     that never finished phase 2 has NaN references, applies no record and keeps its state --, counts
     (K,) records applied, refs (K, 6))."""
     K = filters.batch
@@ -353,7 +362,7 @@ def run_session(phase2, phase3, filters, n_avg=100, alpha=0.1):
     ib, tib, rb = DeviceBuffer(48 * K), DeviceBuffer(8 * K), DeviceBuffer(4 * K)
     check(lib.pekf_frontend_init_dev(K, E2, ev2.ptr, tsb.ptr, int(n_avg), ib.ptr, tib.ptr, None, rb.ptr, None))
     cnt, refs = DeviceBuffer(4 * K), DeviceBuffer(48 * K)
-    filters.run_events_async(ev3, E3, ib, tib, cnt, refs, alpha, flags=flags3)
+    filters.run_events_async(ev3, E3, ib, tib, cnt, refs, alpha, flags=flags3 | _record_flags(records))
     check(lib.pekf_device_sync())
     return dict(ready=rb.download((K,), np.int32).astype(bool), counts=cnt.download((K,), np.int32),
                 refs=refs.download((K, 6), np.float64))
@@ -455,24 +464,27 @@ class BatchedEKF:
     def run_events_async(self, ev_planes, n_events, init, t_init, counts, refs, alpha=0.1, stream=None, flags=0):
         """Enqueue pekf_live_ext_dev: device event planes [n_events][batch][4] f32 (synth.pack_events), init
         (batch, 6), t_init (batch,) int64; counts (batch,) int32 and refs (batch, 6) outputs -- DeviceBuffers;
-        flags: EV_TIME_EVENTS if the planes hold time events."""
+        flags: EV_TIME_EVENTS if the planes hold time events, EV_F32_RECORDS for f32 records."""
         if self.layout != "aos" or self.flags & RUN_MIXED_PRECISION:
             raise ValueError("the fused front-end + filter kernel runs the FP64 filter on AoS state")
         check(lib.pekf_live_ext_dev(self.batch, int(n_events), ev_planes.ptr, init.ptr, t_init.ptr, float(alpha),
                                     self.X.ptr, self.P.ptr, self.q, self.r, counts.ptr, refs.ptr, int(flags), None,
                                     stream))
 
-    def run_events(self, ev, alpha=0.1):
+    def run_events(self, ev, alpha=0.1, records="f64"):
         """Raw phone events (synth.generate_events layout) -> front-end -> filter, fused in one launch
         (pekf_live_ext_dev).  Returns (counts (batch,) int32 records applied, refs (batch, 6)
-        the filters' acc0 / mag0).  Any event gap and any record dt is applied (time events, escapes)."""
+        the filters' acc0 / mag0).  Any event gap and any record dt is applied (time events, escapes).
+        records: "f64" (default) feeds the filter the FP64 low-pass acc / mag, as the server does
+        (KFS/KalmanFilter.cpp:279-303); "f32" rounds them to the 40 B stream record first, which makes the
+        result equal run_frontend + run bit for bit."""
         assert np.asarray(ev["types"]).shape[1] == self.batch
         evb, E, flags = _event_planes(ev)
         init = DeviceBuffer(48 * self.batch).upload(
             np.concatenate([ev["init_acc"], ev["init_mag"]], axis=1).astype(np.float64))
         tib = DeviceBuffer(8 * self.batch).upload(np.ascontiguousarray(ev["t_init"], np.int64))
         cnt, refs = DeviceBuffer(4 * self.batch), DeviceBuffer(48 * self.batch)
-        self.run_events_async(evb, E, init, tib, cnt, refs, alpha, flags=flags)
+        self.run_events_async(evb, E, init, tib, cnt, refs, alpha, flags=flags | _record_flags(records))
         check(lib.pekf_device_sync())
         return cnt.download((self.batch,), np.int32), refs.download((self.batch, 6), np.float64)
 

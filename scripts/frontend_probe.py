@@ -5,7 +5,8 @@
 phase 2 (pekf_frontend_init_dev, the means / variances of the first 100 samples; --init-means: the
 means alone, no stats, as engine.run_session calls it).
 
-usage: python3 scripts/frontend_probe.py [reps] [--live | --init | --init-means]
+usage: python3 scripts/frontend_probe.py [reps] [--live [--f64 | --f32] | --init | --init-means]
+(--live: the records' acc / mag in FP64, the default, or as f32 stream records with --f32)
 """
 from __future__ import annotations
 
@@ -18,12 +19,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from poseestimationkf_amd import engine, synth  # noqa: E402
-from poseestimationkf_amd._lib import check, lib  # noqa: E402
+from poseestimationkf_amd._lib import EV_F32_RECORDS, check, lib  # noqa: E402
 
 
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     live = "--live" in sys.argv
+    rec_flags = EV_F32_RECORDS if "--f32" in sys.argv else 0
     means_only = "--init-means" in sys.argv
     phase2 = "--init" in sys.argv or means_only
     reps = int(args[0]) if args else 3
@@ -54,7 +56,7 @@ def main():
             check(lib.pekf_frontend_init_dev(K, E, evb.ptr, tb.ptr, 100, ob.ptr, tob.ptr,
                                              None if means_only else sb.ptr, rb.ptr, s))
         elif live:
-            f.run_events_async(evb, E, ib, tb, cnt, win.refs, 0.1, s)
+            f.run_events_async(evb, E, ib, tb, cnt, win.refs, 0.1, s, flags=rec_flags)
         else:
             check(lib.pekf_frontend_dev(K, E, evb.ptr, ib.ptr, tb.ptr, 0.1, r_max, win.gd.ptr, win.am.ptr,
                                         win.my.ptr, cnt.ptr, win.refs.ptr, err.ptr, s))
@@ -70,8 +72,13 @@ def main():
                  digest, ["%.3f" % t for t in times]))
         return
     recs = int(cnt.download((K,), np.int32).sum())
-    print("frontend_probe%s: %d filters x %d events, %d records, ms %s"
-          % (" --live" if live else "", K, E, recs, ["%.3f" % t for t in times]))
+    digest = ""
+    if live:
+        X, _ = f.get_state()
+        digest = " X digest %.17g" % float(np.sum(X * np.arange(1, 5)))
+    print("frontend_probe%s: %d filters x %d events, %d records,%s ms %s"
+          % (" --live" + (" --f32" if rec_flags else " (f64 records)") if live else "", K, E, recs, digest,
+             ["%.3f" % t for t in times]))
 
 
 if __name__ == "__main__":

@@ -120,7 +120,7 @@ def fused(case):
     f = engine.BatchedEKF(case["K"])
     if case["X0"] is not None:
         f.set_state(case["X0"], case["P0"])
-    counts, refs = f.run_events(case["ev"])
+    counts, refs = f.run_events(case["ev"], records="f32")   # the split pipeline's records
     X, P = f.get_state()
     return X, P, counts, refs
 

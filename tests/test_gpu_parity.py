@@ -354,7 +354,10 @@ def test_fused_run_on_native_parsed_c1_log(eng, tmp_path):
     want = np.load(os.path.join(GOLDEN, "c1_xk.npy"))[1:]
     err = _maxerr(tr[:, 0], want)
     print("C1 via native log ingest + fused kernel: max |dq| = %.3e (inputs rounded to f32)" % err)
-    assert err < ATOL_Q
+    # the batched stream path stores the log's float64 samples as f32 (the 40 B record): measured 5.4e-8
+    # against the reference's own X_k (NumPy restatement on the same f32-rounded records: 5.380e-8), so
+    # the bound is that rounding, not the north_star's 1e-5 (the drop-in loop keeps FP64: 1.1e-13)
+    assert err < 1e-7
     assert np.array_equal(tr[:, 0], tr[:, 1])
 
 

@@ -1,9 +1,14 @@
 """The front-end fused into the filter (pekf_live_dev): raw phone events -> records ->
 Prediction + Correction in one launch, no record window.
 
-Checked two ways: bit for bit against the split pipeline it replaces (pekf_frontend_dev writing the
-records, pekf_run_dev with counts applying them), and against the oracle chain (oracle/frontend_numpy.py
-records -> the C oracle filter), whose front-end half is partly pinned (see tests/test_frontend.py)."""
+Two record precisions (pekf_live_ext_dev's PEKF_EV_F32_RECORDS):
+* f32 records (the 40 B stream record): bit for bit against the split pipeline it replaces
+  (pekf_frontend_dev writing the records, pekf_run_dev with counts applying them), and against the
+  oracle chain on f32-rounded records (oracle/frontend_numpy.py -> the C oracle filter);
+* FP64 records (the default, what the server's filter receives: KFS/KalmanFilter.cpp:279-303) against
+  the unrounded oracle chain (oracle/frontend_numpy.py float64 records -> oracle/ekf_numpy.py, the
+  reference's own arithmetic), where the f32 records' rounding shows as ~1e-8 (measured, asserted).
+The oracle's front-end half is partly pinned (see tests/test_frontend.py)."""
 import numpy as np
 import pytest
 
@@ -33,11 +38,12 @@ def _split(eng, ev, K, X0=None, P0=None):
     return X, P, counts, win.refs.download((K, 6), np.float64)
 
 
-def _fused(eng, ev, K, X0=None, P0=None):
+def _fused(eng, ev, K, X0=None, P0=None, records="f32"):
+    """pekf_live_ext_dev; f32 records by default here: the split pipeline's, for bit-for-bit checks."""
     f = eng.BatchedEKF(K)
     if X0 is not None:
         f.set_state(X0, P0)
-    counts, refs = f.run_events(ev)
+    counts, refs = f.run_events(ev, records=records)
     X, P = f.get_state()
     return X, P, counts, refs
 
@@ -70,12 +76,34 @@ def test_live_continues_from_a_given_state(eng):
     _same(_fused(eng, ev, K, X0, P0), _split(eng, ev, K, X0, P0))
 
 
+def _oracle_chain_f64(ev, k, refs, X0=None, P0=None):
+    """Filter k's float64 records from the front-end restatement, through the NumPy restatement of
+    main_file.py's loop (bit-identical to the reference) with the device's reference pair."""
+    from oracle import ekf_numpy
+    g, dt, a, m = _oracle_records(ev, k)
+    X, _, _ = ekf_numpy.run_filter(g, dt.astype(np.float64), a, m, refs[k, :3], refs[k, 3:], X0=X0, P0=P0,
+                                   record=False)
+    return X, len(dt)
+
+
+# FP64 records vs the unrounded oracle chain: the fused kernel's FP64 arithmetic (reference basis,
+# closed-form polar Wahba) against the reference's (SVD), ~1e-14 measured over ~100 records
+ATOL_F64_CHAIN = 1e-12
+# f32 records vs the same unrounded chain: the records' f32 rounding (measured 1.4e-8 on seed 25's
+# sampled filters, 5.3e-8 on 24 filters in round 4's review), within the north_star's 1e-5
+ATOL_F32_ROUNDING = 1e-7
+
+
 def test_live_vs_oracle_chain(eng, oracle_c):
-    """Each filter's own records (ragged) through the oracle front-end and the C oracle filter."""
+    """Each filter's own records (ragged) through the oracle front-end and the oracle filter: f32 records
+    against the C oracle on the same f32-rounded records (1e-9), and against the unrounded chain (the
+    rounding, <= ATOL_F32_ROUNDING); FP64 records against the unrounded chain (<= ATOL_F64_CHAIN)."""
     K, E = 256, 1200
     ev = synth.generate_events(np.arange(K), E, seed=25)
-    X, _, counts, refs = _fused(eng, ev, K)
-    worst = 0.0
+    X, _, counts, refs = _fused(eng, ev, K, records="f32")
+    X64, _, counts64, refs64 = _fused(eng, ev, K, records="f64")
+    assert np.array_equal(counts, counts64) and np.array_equal(refs, refs64)
+    worst = worst_round = worst64 = 0.0
     for k in range(0, K, 23):
         g, dt, a, m = _oracle_records(ev, k)
         assert counts[k] == len(dt)
@@ -84,8 +112,58 @@ def test_live_vs_oracle_chain(eng, oracle_c):
                             refs[k:k + 1, :3], refs[k:k + 1, 3:])
         Xo, _, _ = oracle_c.run(rec)
         worst = max(worst, float(np.abs(X[k] - Xo[0]).max()))
-    print("fused events -> filter vs oracle chain: max |dq| = %.3e" % worst)
+        Xu, _ = _oracle_chain_f64(ev, k, refs)
+        worst_round = max(worst_round, float(np.abs(X[k] - Xu).max()))
+        worst64 = max(worst64, float(np.abs(X64[k] - Xu).max()))
+    print("fused events -> filter: f32 records vs the f32 oracle chain %.3e, vs the unrounded chain %.3e; "
+          "FP64 records vs the unrounded chain %.3e" % (worst, worst_round, worst64))
     assert worst < 1e-9
+    assert worst_round < ATOL_F32_ROUNDING
+    assert worst64 < ATOL_F64_CHAIN
+
+
+def test_live_f64_records_full_batch_sampled(eng):
+    """FP64 records at full scale (1,048,576 filters x 192 events, 16,384 streams tiled x64): sampled
+    filters against the unrounded oracle chain, and every filter within the f32 rounding of the f32-record
+    run (same counts and reference pairs)."""
+    K0, E, tile = 16384, 192, 64
+    ev0 = synth.generate_events(np.arange(K0), E, seed=26)
+    ev = dict(types=np.tile(ev0["types"], (1, tile)), values=np.tile(ev0["values"], (1, tile, 1)),
+              times=np.tile(ev0["times"], (1, tile)), init_acc=np.tile(ev0["init_acc"], (tile, 1)),
+              init_mag=np.tile(ev0["init_mag"], (tile, 1)), t_init=np.tile(ev0["t_init"], tile))
+    K = K0 * tile
+    X64, _, c64, r64 = _fused(eng, ev, K, records="f64")
+    X32, _, c32, r32 = _fused(eng, ev, K, records="f32")
+    assert np.array_equal(c64, c32) and np.array_equal(r64, r32) and c64.sum() > 10 * K
+    assert np.isfinite(X64).all() and float(np.abs(X64 - X32).max()) < ATOL_F32_ROUNDING
+    worst = 0.0
+    for k in (0, 1, 4095, K0 - 1, K0, 7 * K0 + 77, K - 1):
+        Xu, n = _oracle_chain_f64(ev0, k % K0, r64)      # tiled: filter k runs stream k % K0
+        assert c64[k] == n
+        worst = max(worst, float(np.abs(X64[k] - Xu).max()))
+    print("FP64 records, 1M filters: sampled vs the unrounded chain %.3e" % worst)
+    assert worst < ATOL_F64_CHAIN
+
+
+def test_live_f64_records_across_escaped_gaps(eng):
+    """FP64 records whose dt does not fit the dt word (3 x (2^30 - 1) ns apart: escaped, the float64 dt
+    in the LdsQueue64 side entry), from a resumed state, against the unrounded oracle chain."""
+    K = 64
+    g = (1 << 30) - 1
+    spec = [(synth.EV_GYRO, g), (synth.EV_GYRO, g), (synth.EV_GYRO, g), (synth.EV_ACC, 10), (synth.EV_MAG, 10)] * 5
+    ev = _events(K, spec)
+    rng = np.random.default_rng(9)
+    X0 = rng.standard_normal((K, 4))
+    X0 /= np.linalg.norm(X0, axis=1, keepdims=True)
+    P0 = np.tile(np.eye(4) * 0.4, (K, 1, 1))
+    X, _, counts, refs = _fused(eng, ev, K, X0, P0, records="f64")
+    assert np.all(counts == 5)
+    worst = 0.0
+    for k in range(0, K, 7):
+        Xu, _ = _oracle_chain_f64(ev, k, refs, X0[k], P0[k])
+        worst = max(worst, float(np.abs(X[k] - Xu).max()))
+    print("FP64 records across escaped gaps vs the unrounded chain: %.3e" % worst)
+    assert worst < ATOL_F64_CHAIN
 
 
 def test_live_streams_without_records_leave_the_state(eng):
@@ -147,13 +225,18 @@ def test_session_phase2_then_fused_phase3(eng):
     ph3 = synth.generate_events(np.arange(K), 500, seed=34)
     ph3 = dict(ph3, times=ph3["times"] - ph3["t_init"][None, :] + ph2["times"][-1][None, :])
     f = eng.BatchedEKF(K)
-    got = eng.run_session(ph2, ph3, f)
+    got = eng.run_session(ph2, ph3, f, records="f32")
     assert got["ready"].all()
     ini = eng.frontend_init(ph2)
     assert np.array_equal(ini["t_init"], ph2["times"][-1])
-    split = _split(eng, dict(ph3, t_init=ini["t_init"], init_acc=ini["init"][:, :3], init_mag=ini["init"][:, 3:]), K)
+    ev3 = dict(ph3, t_init=ini["t_init"], init_acc=ini["init"][:, :3], init_mag=ini["init"][:, 3:])
+    split = _split(eng, ev3, K)
     X, P = f.get_state()
     _same((X, P, got["counts"], got["refs"]), split)
+    # the default FP64 records: the session equals the fused launch on the same phase-2 results
+    f64 = eng.BatchedEKF(K)
+    got64 = eng.run_session(ph2, ph3, f64)
+    _same(f64.get_state() + (got64["counts"], got64["refs"]), _fused(eng, ev3, K, records="f64"))
 
 
 def test_session_leaves_filters_that_never_got_ready(eng):
@@ -170,7 +253,7 @@ def test_session_leaves_filters_that_never_got_ready(eng):
     P0 = np.tile(np.eye(4) * 0.3, (K, 1, 1))
     f = eng.BatchedEKF(K)
     f.set_state(X0, P0)
-    got = eng.run_session(ph2, ph3, f)
+    got = eng.run_session(ph2, ph3, f, records="f32")
     ready = got["ready"]
     assert 0 < ready.sum() < K
     X, P = f.get_state()

@@ -296,6 +296,13 @@ def test_live_and_split_pipelines_across_pauses(eng, oracle_c):
         worst = max(worst, _err(X[k], Xo[0]))
     print("events with pauses / clock steps -> filter vs oracle chain: max |dq| = %.3e" % worst)
     assert worst < 1e-9
+    # FP64 records (the default) across the same pauses, against the unrounded oracle chain
+    from .test_live import ATOL_F64_CHAIN, _oracle_chain_f64
+    X64, _, c64, r64 = _fused(eng, ev, K, records="f64")
+    assert np.array_equal(c64, counts) and np.array_equal(r64, refs)
+    worst64 = max(float(np.abs(X64[k] - _oracle_chain_f64(ev, k, refs)[0]).max()) for k in range(0, K, 9))
+    print("FP64 records across pauses vs the unrounded chain: %.3e" % worst64)
+    assert worst64 < ATOL_F64_CHAIN
 
 
 @pytest.mark.gpu
