@@ -628,6 +628,59 @@ struct NoPin {
 // solves Wahba by wahba_current_rank1_quat with the reference's weights |acc_z|, 1 - |acc_z|
 // (ExtendedKalmanFilter.py:71).  The caller re-reads them (memory, LDS) instead of holding six doubles
 // in registers through the Wahba chain.
+// wahba_quat_toward (below) in two halves, for ekf_record_step's HOIST schedule (the same arithmetic;
+// the one-piece form is kept for every other kernel, whose schedule it fixes).
+// The state-independent half: Wahba's rotation R' of the current frame in the reference basis (it
+// depends on the record's samples only, not on the prediction z).
+template <int F = 1, class RW, std::enable_if_t<RW::kRefBasis, int> = 0>
+PEKF_DEV void wahba_rotation_ref(const RW &W, const Frame &V, double ka, double km, double *R) {
+    const double kw = km * W.b2W, kb = km * W.b1W;
+    double p = ka * W.aW * V.alpha + kb * V.beta1 + kw * V.beta2;
+    double s = kw * V.beta1 - kb * V.beta2;
+    const double ih = rsqrt<F>(p * p + s * s);
+    p *= ih;
+    s *= ih;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        R[j] = p * V.e1[j] - s * V.e2[j];
+        R[3 + j] = s * V.e1[j] + p * V.e2[j];
+        R[6 + j] = V.u3[j];
+    }
+}
+
+// The z-dependent half: Q4 of R' flipped toward z, with the fallbacks.
+template <int F = 1, class RW, class Reload, class Pin = NoPin, std::enable_if_t<RW::kRefBasis, int> = 0>
+PEKF_DEV void wahba_toward_from_rotation(const RW &W, const double *R, const double *z, double *v, double &sc,
+                                         const Reload &reload, const Pin &pin = Pin()) {
+    double nv, t0;
+    q4_times(R, z, v, nv, t0);
+    sc = rsqrt<F>(nv);
+    pin();
+    if (PEKF_TAKEN(!(nv >= 1.0), false)) {  // (nv < 1, or NaN)
+        double Fw[9], Rw[9], zw[4], vw[4], qw[4];
+        W.quat(qw);
+        quat_to_rotm(qw, Fw);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) Rw[3 * i + j] = Fw[3 * i] * R[j] + Fw[3 * i + 1] * R[3 + j] + Fw[3 * i + 2] * R[6 + j];
+        qmul_left<false>(qw, z, zw);
+        rotm_to_quat_flip_reference(Rw, zw, vw, sc);
+        qmul_left<true>(qw, vw, v);
+        // NaN: a degenerate current frame.  In this basis B' = Fw^T B pairs acc, mag with the reference
+        // pair's own coordinates (aW, 0, 0), (b1W, b2W, 0); its shortest-arc attitude, flipped toward z
+        // as ExtendedKalmanFilter.py:73-75 flips, replaces the NaN one.
+        if (!(nv == nv)) {  // (it overwrites v and sc in place)
+            double acc[3], mag[3];
+            reload(acc, mag);
+            const double a0[3] = {W.aW, 0.0, 0.0}, m0[3] = {W.b1W, W.b2W, 0.0}, kr = fabs(acc[2]);
+            wahba_current_rank1_quat<1>(a0, m0, acc, mag, kr, 1.0 - kr, v);
+            sc = v[0] * z[0] + v[1] * z[1] + v[2] * z[2] + v[3] * z[3] < 0.0 ? -1.0 : 1.0;
+        }
+    }
+    (void)t0;
+}
+
 template <int F = 1, class RW, class Reload, class Pin = NoPin, std::enable_if_t<RW::kRefBasis, int> = 0>
 PEKF_DEV void wahba_quat_toward(const RW &W, const Frame &V, double ka, double km, const double *z, double *v,
                                 double &sc, const Reload &reload, const Pin &pin = Pin()) {

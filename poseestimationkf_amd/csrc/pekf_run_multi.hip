@@ -20,13 +20,35 @@ static bool pin_schedule() {
     return !(e && e[0] == '0');
 }
 
+// The HOIST schedule (ekf_record_step) for launches of at most one wave per SIMD (batch <= CUs x 4 x 64:
+// config 2's 65,536 filters on 256 CUs), where the record's dependency chain is exposed; more waves fill
+// the stalls themselves and pay for the longer block's registers (profiles/r5/ab_hoist/).
+// PEKF_RUN_HOIST=0 / 1 forces it off / on (A/B runs, tests).
+static bool hoist_schedule(int64_t batch) {
+    const char *e = getenv("PEKF_RUN_HOIST");
+    if (e && e[0] == '0') return false;
+    if (e && e[0] == '1') return true;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        return false;
+    return batch <= (int64_t)cus * 4 * kWave;
+}
+
 int launch_run_multi(int64_t batch, int64_t n_steps, int64_t window, int64_t step0, const float4 *gd,
                      const float4 *am, const float2 *my, const double *dtx, const double *refs, double *X,
                      double *P, double q, double r, double *traj, const int32_t *counts, bool mixed, bool soa,
                      hipStream_t stream) {
     const dim3 grid(grid_for(batch, kRunBlock)), block(kRunBlock);
     if (!traj && !mixed && !counts && !dtx && pin_schedule()) {
-        if (soa)
+        if (hoist_schedule(batch)) {
+            if (soa)
+                hipLaunchKernelGGL((k_run<false, false, true, false, false, true, false, true>), grid, block, 0, stream,
+                                   batch, n_steps, window, step0, gd, am, my, refs, X, P, q, r, traj, counts, dtx);
+            else
+                hipLaunchKernelGGL((k_run<false, false, false, false, false, true, false, true>), grid, block, 0, stream,
+                                   batch, n_steps, window, step0, gd, am, my, refs, X, P, q, r, traj, counts, dtx);
+        } else if (soa)
             hipLaunchKernelGGL((k_run<false, false, true, false, false, true>), grid, block, 0, stream, batch, n_steps,
                                window, step0, gd, am, my, refs, X, P, q, r, traj, counts, dtx);
         else

@@ -196,12 +196,66 @@ __device__ __forceinline__ StepK<PT> step_consts(double qs, double rs) {
 // same values bit for bit.
 // reload(acc, mag) re-reads the record's samples for the rare degenerate-Wahba fallback
 // (wahba_quat_toward); it is not called on the common path.
-template <typename PT, bool MC = false, bool LAZY = false, bool OM = false, bool PIN = false, typename Ref,
-          typename Reload>
+// Wahba-skip: no Correction for this record (X = z, P = P- = S - rI)
+template <typename PT, bool MC>
+__device__ __forceinline__ void record_skip(double *x, const double *z, Sym4T<PT> &P, const Sym4T<PT> &S2,
+                                            const StepK<PT> &k) {
+    x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
+    const PT hf = PT(0.5);
+    if (MC)  // D N D = (S - 2r I) / beta = S^/2 - rb I
+        P = {fma(hf, S2.a00, -k.r2), hf * S2.a01, -hf * S2.a02, -hf * S2.a03, fma(hf, S2.a11, -k.r2),
+             -hf * S2.a12, -hf * S2.a13, fma(hf, S2.a22, -k.r2), hf * S2.a23, fma(hf, S2.a33, -k.r2)};
+    else
+        P = {fma(hf, S2.a00, -k.rp), hf * S2.a01, hf * S2.a02, hf * S2.a03, fma(hf, S2.a11, -k.rp),
+             hf * S2.a12, hf * S2.a13, fma(hf, S2.a22, -k.rp), hf * S2.a23, fma(hf, S2.a33, -k.rp)};
+}
+
+// ---- Correction (ExtendedKalmanFilter.py:70-80) from S^-1 (Si) and Wahba's Y = v sc ----
+template <typename PT, bool MC>
+__device__ __forceinline__ void record_correct(double *x, const double *z, Sym4T<PT> &P, const Sym4T<PT> &Si,
+                                               const double *v, double sc, const StepK<PT> &k) {
+    // e = Y - z (MC: D e, whose last two components are z - Y)
+    const PT e0 = (PT)fma_sub(v[0], sc, z[0]), e1 = (PT)fma_sub(v[1], sc, z[1]);
+    const PT e2 = (PT)(MC ? fma_rsub(v[2], sc, z[2]) : fma_sub(v[2], sc, z[2]));
+    const PT e3 = (PT)(MC ? fma_rsub(v[3], sc, z[3]) : fma_sub(v[3], sc, z[3]));
+    // X = z + K e = Y - r S^-1 e (:77), normalised (:79): X ~ Y / (2r) - S^-1 e / 2, or (MC,
+    // S^-1 = -(2/beta) D Si D) X ~ Y / sqrt(2) + D Si D e
+    const double u0 = Si.a00 * e0 + Si.a01 * e1 + Si.a02 * e2 + Si.a03 * e3;
+    const double u1 = Si.a01 * e0 + Si.a11 * e1 + Si.a12 * e2 + Si.a13 * e3;
+    const double u2 = Si.a02 * e0 + Si.a12 * e1 + Si.a22 * e2 + Si.a23 * e3;
+    const double u3 = Si.a03 * e0 + Si.a13 * e1 + Si.a23 * e2 + Si.a33 * e3;
+    const double sr = sc * k.sy;
+    const double x0 = fma(v[0], sr, MC ? u0 : -u0), x1 = fma(v[1], sr, MC ? u1 : -u1);
+    const double x2 = fma(v[2], sr, -u2), x3 = fma(v[3], sr, -u3);
+    if (MC) {
+        x[0] = x0; x[1] = x1; x[2] = x2; x[3] = x3;
+    } else {
+        const double in = rsqrt<true>(x0 * x0 + x1 * x1 + x2 * x2 + x3 * x3);
+        x[0] = x0 * in; x[1] = x1 * in; x[2] = x2 * in; x[3] = x3 * in;
+    }
+    // P = P- - K P- = r K = r I - r^2 S^-1 = r I - (2 r^2) Si (:78)
+    if (MC) {
+        P = Si;  // P = rI + beta D N D: nothing to compute
+    } else {
+        const PT rp = k.rp, rr = k.rr;
+        P = {rp - rr * Si.a00, -rr * Si.a01, -rr * Si.a02, -rr * Si.a03, rp - rr * Si.a11,
+             -rr * Si.a12, -rr * Si.a13, rp - rr * Si.a22, -rr * Si.a23, rp - rr * Si.a33};
+    }
+}
+
+// HOIST (the FP64 multi-record loop only): the Correction's state-independent half -- S^-1, the
+// current frame and Wahba's rotation R' -- is formed ahead of the missing-magnetometer branch, in the
+// Prediction's basic block (held there by an empty asm), so one block carries two independent
+// dependency chains (the Prediction's and the record's own); only Q4 z, its flip and the update stay
+// behind the branch.  For launches of at most one wave per SIMD (config 2), where nothing else fills
+// the chain's stalls (launch_run_multi selects it).  The same arithmetic, bit for bit.
+template <typename PT, bool MC = false, bool LAZY = false, bool OM = false, bool PIN = false, bool HOIST = false,
+          typename Ref, typename Reload>
 __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> &P, const Ref &Wf, const StepK<PT> &k,
                                                 const double *gy, double dt_ns, bool missing,
                                                 const double *acc, const double *mag, const Reload &reload) {
     static_assert(!OM || (MC && std::is_same<PT, double>::value), "omod form: FP64 multi-record loop only");
+    static_assert(!HOIST || OM, "hoisted form: FP64 multi-record loop only");
     constexpr int F = OM ? 2 : 1;  // rsqrt form
     // ---- Prediction (ExtendedKalmanFilter.py:58-68) ----
     const double n2x = LAZY ? x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3] : n2;
@@ -229,6 +283,25 @@ __device__ __forceinline__ void ekf_record_step(double *x, double n2, Sym4T<PT> 
                 : innovation_cov2<PT>(P, hp, wp, (PT)th2, xp, n2p, k.g2, k.r2, g2x);
     }
 
+    if constexpr (HOIST) {
+        const Sym4T<PT> Si = spd_inverse_schur<PT, true, MC>(S2);
+        const double ka = fabs(acc[2]);              // (:71)
+        Frame Vf;
+        make_frame<F>(acc, mag, Vf, 1.0 - ka);
+        double R[9];
+        wahba_rotation_ref<F>(Wf, Vf, ka, 1.0 - ka, R);
+        asm volatile("" ::"v"(Si.a00), "v"(Si.a01), "v"(Si.a02), "v"(Si.a03), "v"(Si.a11), "v"(Si.a12),
+                     "v"(Si.a13), "v"(Si.a22), "v"(Si.a23), "v"(Si.a33), "v"(R[0]), "v"(R[1]), "v"(R[2]),
+                     "v"(R[3]), "v"(R[4]), "v"(R[5]), "v"(R[6]), "v"(R[7]), "v"(R[8]));
+        if (missing) {
+            record_skip<PT, MC>(x, z, P, S2, k);
+        } else {
+            double v[4], sc;
+            wahba_toward_from_rotation<F>(Wf, R, z, v, sc, reload);  // Wahba.py:8-47 + the flip of :73-75
+            record_correct<PT, MC>(x, z, P, Si, v, sc, k);
+        }
+        return;
+    }
     if (missing) {
         // Wahba-skip: no Correction for this record (X = z, P = P- = S - rI)
         x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
@@ -344,7 +417,9 @@ __device__ __forceinline__ void from_ref_basis(const RW &Wr, double *x, Sym4T<PT
 // PEKF_DT_ESCAPE takes its dt from there -- gaps of 2^31 ns or more, negative or fractional ones, any
 // T - previousT the reference accepts (ExtendedKalmanFilter.py:62).  A separate instantiation, so the
 // windows without escapes (every synthetic and front-end stream but the rare long pause) pay nothing.
-template <bool TRAJ, bool MIXED, bool SOA, bool COUNTS, bool ONE, bool PIN = false, bool LONGDT = false>
+// HOIST: the Correction's state-independent half ahead of the missing branch (ekf_record_step).
+template <bool TRAJ, bool MIXED, bool SOA, bool COUNTS, bool ONE, bool PIN = false, bool LONGDT = false,
+          bool HOIST = false>
 __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run(int64_t batch, int64_t n_steps, int64_t window,
                                                    int64_t step0, const float4 *__restrict__ gd,
                                                    const float4 *__restrict__ am,
@@ -472,7 +547,7 @@ __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run(int64_t batch, 
                 a[0] = va.x; a[1] = va.y; a[2] = va.z;
                 m[0] = va.w; m[1] = vm.x; m[2] = vm.y;
             };
-            ekf_record_step<PT, MC, decltype(lazy)::value, MC && !MIXED, PIN>(
+            ekf_record_step<PT, MC, decltype(lazy)::value, MC && !MIXED, PIN, HOIST && MC && !MIXED>(
                 x, n2, P, ref, step_consts<PT, MC>(qs, rs), gy, dtn, (word & PEKF_MISSING_MAG_BIT) != 0, acc, mag,
                 reload);
         }
