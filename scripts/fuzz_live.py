@@ -12,6 +12,13 @@ timestamps: the interpolation divides 0 by 0 as the C++ server does), 1-4 ms, or
 of 2^30 ns and more or a clock stepping back (time events, escaped record dts), filters that never got
 ready (NaN phase-2 means) and a random initial state.
 
+The default FP64-record form (pekf_live_ext_dev without PEKF_EV_F32_RECORDS: the low-pass acc / mag
+reach the filter unrounded, as in the server) is run on every case too: its counts and reference pairs
+must equal the f32 form's, and the four filters' final X must agree with the unrounded oracle chain
+(the restatement's float64 records -> oracle/ekf_numpy.py, the reference's own arithmetic) within
+F64_TOL; NaN where the chain's SVD raises (a NaN record: duplicate timestamps interpolate 0/0).
+check_f64 says which filters the reference's own ill-conditioning exempts.
+
 usage: python3 scripts/fuzz_live.py [--cases N] [--seed S]   (exit status 1 on any difference)
 """
 from __future__ import annotations
@@ -26,10 +33,11 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from oracle import frontend_numpy  # noqa: E402  (the checker)
+from oracle import ekf_numpy, frontend_numpy  # noqa: E402  (the checkers)
 from poseestimationkf_amd import engine, synth  # noqa: E402
 
 KINDS = np.array([synth.EV_ACC, synth.EV_GYRO, synth.EV_MAG], np.uint32)
+F64_TOL = 1e-9   # FP64 records vs the unrounded chain (tests/test_live.py asserts 1e-12 on smooth streams)
 
 
 def draw_case(rng):
@@ -116,13 +124,81 @@ def split(case, cols=None):
     return X, P, counts, win.refs.download((case["K"], 6), np.float64)
 
 
-def fused(case):
+def fused(case, records="f32"):
     f = engine.BatchedEKF(case["K"])
     if case["X0"] is not None:
         f.set_state(case["X0"], case["P0"])
-    counts, refs = f.run_events(case["ev"], records="f32")   # the split pipeline's records
+    counts, refs = f.run_events(case["ev"], records=records)   # f32: the split pipeline's records
     X, P = f.get_state()
     return X, P, counts, refs
+
+
+def _chain(g, dt, a, m, refs_k, X0, P0):
+    """The unrounded oracle chain's final X: NaN-filled if its SVD raises on a NaN record."""
+    try:
+        with np.errstate(all="ignore"):
+            X, _, _ = ekf_numpy.run_filter(g, dt, a, m, refs_k[:3], refs_k[3:], X0=X0, P0=P0, record=False)
+        return X, False
+    except np.linalg.LinAlgError:
+        return np.full(4, np.nan), True
+
+
+def check_f64(case, got, cols, tally):
+    """(problems, worst |dq|) of the FP64-record run's filters cols against the unrounded oracle chain.
+
+    Two kinds of filter are not held to F64_TOL, each counted in `tally`: where the reference itself
+    returns NaN from finite records (its RotationMatrix2Quart at an exactly-identity rotation takes a
+    square root of -2e-16 -- the first record after duplicate timestamps interpolates to the phase-2
+    means exactly; the kernel returns the well-conditioned value), and where the chain
+    is ill-conditioned: rounding its records to f32 moves its answer by more than 1e-6 (a Comparator
+    sign at q.z ~ 0, ExtendedKalmanFilter.py:73-75: either sign is the reference's answer).  A filter
+    off by more than F64_TOL is held to 4x the spread of the reference's own answer under 1-ulp
+    input noise instead (near-identity rotations) and counted as ulp-sensitive."""
+    ev, out, worst = case["ev"], [], 0.0
+    X, _, counts, refs = got
+    for k in cols:
+        if not np.isfinite(ev["init_acc"][k]).all():
+            continue
+        g, dt, a, m = frontend_numpy.run_frontend(ev["types"][:, k], ev["values"][:, k].astype(np.float64),
+                                                  ev["times"][:, k], ev["init_acc"][k], ev["init_mag"][k],
+                                                  ev["t_init"][k])
+        if len(dt) == 0:
+            continue
+        X0 = None if case["X0"] is None else case["X0"][k]
+        P0 = None if case["P0"] is None else case["P0"][k]
+        dt = dt.astype(np.float64)
+        Xo, raised = _chain(g, dt, a, m, refs[k], X0, P0)
+        if raised or np.isnan(X[k]).any():
+            if not (raised and np.isnan(X[k]).all()):
+                out.append("filter %d: NaN in one of kernel / chain (chain raised: %s)" % (k, raised))
+            continue
+        if np.isnan(Xo).any():
+            tally["reference_nan"] += 1
+            continue
+        r32 = lambda v: v.astype(np.float32).astype(np.float64)  # noqa: E731
+        X32, _ = _chain(r32(g), dt, r32(a), r32(m), refs[k], X0, P0)
+        if not float(np.abs(X32 - Xo).max()) < 1e-6:
+            tally["ill_conditioned"] += 1
+            continue
+        d = float(np.abs(X[k] - Xo).max())
+        if d > F64_TOL:
+            # near an identity Wahba rotation the reference's R->q divides rounding noise by the angle
+            # (DESIGN.md §4.1): its own answer then moves by ~d under 1-ulp input noise.  Such a filter
+            # is held to four times that spread (a 16-sample estimate), and counted.
+            pr = np.random.default_rng(k)
+            spread = 0.0
+            for _ in range(16):
+                u = lambda v: v * (1 + 2.2e-16 * pr.standard_normal(np.shape(v)))  # noqa: E731
+                Xn, _ = _chain(u(g), dt, u(a), u(m), u(refs[k]), X0, P0)
+                spread = max(spread, float(np.abs(Xn - Xo).max()))
+            if d <= 4 * spread:
+                tally["ulp_sensitive"] += 1
+                continue
+        worst = max(worst, d)
+        tally["checked"] += 1
+        if d > F64_TOL:
+            out.append("filter %d: FP64 records vs the unrounded chain %.3e" % (k, d))
+    return out, worst
 
 
 def main(argv=None):
@@ -131,10 +207,12 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=1)
     a = ap.parse_args(argv)
     rng = np.random.default_rng(a.seed)
-    fails, records, t0 = 0, 0, time.time()
+    fails, records, t0, worst64 = 0, 0, time.time(), 0.0
+    tally = dict(checked=0, reference_nan=0, ill_conditioned=0, ulp_sensitive=0)
     for i in range(a.cases):
         if i and i % 25 == 0:
-            print("%d cases, %d differ, %d records applied, %.0f s" % (i, fails, records, time.time() - t0), flush=True)
+            print("%d cases, %d differ, %d records applied, FP64 records vs the unrounded chain <= %.3e, %.0f s"
+                  % (i, fails, records, worst64, time.time() - t0), flush=True)
         case = draw_case(rng)
         cols = rng.choice(case["K"], size=min(4, case["K"]), replace=False)
         u, v = fused(case), split(case, cols)
@@ -143,6 +221,15 @@ def main(argv=None):
             print("RECORDS case %d: %s  K=%d E=%d mix=%s" % (i, "; ".join(case["record_problems"][:4]), case["K"],
                                                             case["E"], case["mix"]), flush=True)
         records += int(u[2].sum())
+        w = fused(case, "f64")
+        probs, d64 = check_f64(case, w, cols, tally)
+        worst64 = max(worst64, d64)
+        if not (np.array_equal(w[2], u[2]) and np.array_equal(w[3], u[3], equal_nan=True)):
+            probs.append("counts / refs differ from the f32 form")
+        if probs:
+            fails += 1
+            print("F64 case %d: %s  K=%d E=%d mix=%s" % (i, "; ".join(probs[:4]), case["K"], case["E"], case["mix"]),
+                  flush=True)
         same = all(np.array_equal(x, y, equal_nan=True) for x, y in zip(u, v))
         if not same:
             fails += 1
@@ -150,7 +237,11 @@ def main(argv=None):
                      for n, x, y in zip(("X", "P", "counts", "refs"), u, v) if not np.array_equal(x, y, equal_nan=True)]
             print("DIFFERENT case %d: %s  K=%d E=%d mix=%s X0=%s" % (i, ", ".join(names), case["K"], case["E"],
                                                                      case["mix"], case["X0"] is not None), flush=True)
-    print("done: %d cases, %d differ, %d records applied" % (a.cases, fails, records))
+    print("done: %d cases, %d differ, %d records applied; FP64 records vs the unrounded chain <= %.3e over %d "
+          "filters (%d where the reference returns NaN from finite records, %d ill-conditioned: not held to it; "
+          "%d within 4x the reference's own spread under 1-ulp input noise)"
+          % (a.cases, fails, records, worst64, tally["checked"], tally["reference_nan"], tally["ill_conditioned"],
+             tally["ulp_sensitive"]))
     return 1 if fails else 0
 
 
