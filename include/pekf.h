@@ -177,6 +177,19 @@ int pekf_run_ext_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t ste
                      const void *plane_gd, const void *plane_am, const void *plane_my, const double *dt_ext,
                      const double *refs, double *X, double *P, double q, double r, double *traj,
                      const int32_t *counts, uint32_t flags, void *stream);
+/* The same launch over FP64 records, for inputs that are float64 to begin with (recorded logs, which the
+ * reference parses into float64, ReadFile.py:14-21): 80 B per filter-record in three
+ * filter-minor planes,
+ *   plane_gd : double4 [window][batch] {gyro x, y, z, dt_ns} -- dt the float64 T - previousT itself
+ *              (ExtendedKalmanFilter.py:62): any pause, clock step or fraction
+ *   plane_am : double4 [window][batch] {acc x, y, z, mag x}
+ *   plane_my : double2 [window][batch] {mag y, z}
+ * Every record is a full record (no missing-magnetometer flag).  refs, X, P, q, r, traj, counts as
+ * pekf_run_dev (AoS FP64 state); always the multi-record arithmetic, so a window of f32-representable
+ * values gives pekf_run_dev's state (n_steps >= 2) bit for bit. */
+int pekf_run_rec64_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0, const void *plane_gd,
+                       const void *plane_am, const void *plane_my, const double *refs, double *X, double *P,
+                       double q, double r, double *traj, const int32_t *counts, void *stream);
 /* AoS state (X[batch][4], P[batch][4][4]) <-> SoA state (X[4][batch], P[10][batch] holding
  * P00 P01 P02 P03 P11 P12 P13 P22 P23 P33).  to_soa != 0: AoS -> SoA, else SoA -> AoS. */
 int pekf_state_layout_dev(int64_t batch, double *X_aos, double *P_aos, double *X_soa, double *P_soa,
@@ -213,6 +226,10 @@ int pekf_log_read(const char *path, int64_t n_records, float *gyro, float *acc, 
                   double *acc0, double *mag0, double *t0);
 int pekf_log_read_ext(const char *path, int64_t n_records, float *gyro, float *acc, float *mag, uint32_t *dtw,
                       double *dt_ext, int64_t *n_escaped, double *acc0, double *mag0, double *t0);
+/* The log's records as parsed, float64 (the records of pekf_run_rec64_dev): gyro/acc/mag[n*3], dt_ns[n] =
+ * T[i+1] - T[i] (any value), acc0/mag0[3], t0 (may be NULL). */
+int pekf_log_read64(const char *path, int64_t n_records, double *gyro, double *acc, double *mag, double *dt_ns,
+                    double *acc0, double *mag0, double *t0);
 
 /* ---------------- server front-end: raw phone events -> records ----------------
  * Device kernel.  Per filter, the phase-3 state machine of Parser::WriteKalmanFilterMeasurement

@@ -89,6 +89,7 @@ SIGNATURES = {
     "pekf_wahba_quaternion": [_i64] + [_vp] * 7,
     "pekf_rotmat_to_quat": [_i64, _vp, _vp],
     "pekf_run_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp, _u32, _vp],
+    "pekf_run_rec64_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp, _vp],
     "pekf_run_ext_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp, _u32,
                          _vp],
     "pekf_reset_state_dev": [_i64, _vp, _vp, _vp],
@@ -116,6 +117,7 @@ SIGNATURES = {
     "pekf_log_scan": [ctypes.c_char_p, ctypes.POINTER(_i64)],
     "pekf_log_read": [ctypes.c_char_p, _i64, _vp, _vp, _vp, _vp, _dp, _dp, _dp],
     "pekf_log_read_ext": [ctypes.c_char_p, _i64, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_i64), _dp, _dp, _dp],
+    "pekf_log_read64": [ctypes.c_char_p, _i64, _vp, _vp, _vp, _vp, _dp, _dp, _dp],
     "pekf_quat_to_rpy_dev": [_i64, _vp, _vp, _vp],
     "pekf_synth_dev": [_i64, _i64, _i64, _u32, _int, _dp, _dbl, _vp, _vp, _vp, _vp, _vp],
     "pekf_comm_version": [_ip],

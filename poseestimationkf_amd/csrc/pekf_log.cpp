@@ -158,6 +158,33 @@ int pekf_log_read_ext(const char *path, int64_t n_records, float *gyro, float *a
     return PEKF_OK;
 }
 
+int pekf_log_read64(const char *path, int64_t n_records, double *gyro, double *acc, double *mag, double *dt_ns,
+                    double *acc0, double *mag0, double *t0) {
+    if (!path || !gyro || !acc || !mag || !dt_ns || !acc0 || !mag0)
+        return pekf::set_error(PEKF_ERR_INVALID, "null pointer");
+    LogColumns c;
+    if (int st = parse(path, c)) return st;
+    int64_t n = 0;
+    if (int st = validate(path, c, &n)) return st;
+    if (n_records > n)
+        return pekf::set_error(PEKF_ERR_INVALID, "%s has %lld records, %lld requested", path, (long long)n,
+                               (long long)n_records);
+    for (int k = 0; k < 3; ++k) {
+        acc0[k] = c.acc0[k];
+        mag0[k] = c.mag0[k];
+    }
+    if (t0) *t0 = c.T[0];
+    for (int64_t i = 0; i < n_records; ++i) {
+        for (int k = 0; k < 3; ++k) {
+            gyro[3 * i + k] = c.gyro[3 * i + k];
+            acc[3 * i + k] = c.acc1[3 * i + k];
+            mag[3 * i + k] = c.mag1[3 * i + k];
+        }
+        dt_ns[i] = c.T[i + 1] - c.T[i];  // T - previousT as the reference forms it (ExtendedKalmanFilter.py:62)
+    }
+    return PEKF_OK;
+}
+
 int pekf_log_read(const char *path, int64_t n_records, float *gyro, float *acc, float *mag, uint32_t *dtw,
                   double *acc0, double *mag0, double *t0) {
     return pekf_log_read_ext(path, n_records, gyro, acc, mag, dtw, nullptr, nullptr, acc0, mag0, t0);

@@ -265,6 +265,74 @@ class IMUWindow:
         return synth.unpack_planes(gd, am, my, refs[:, :3], refs[:, 3:], dtx)
 
 
+class RecordWindow64:
+    """`window` steps x `batch` filters of FP64 records (80 B per filter-record, pekf_run_rec64_dev), for
+    inputs that are float64 to begin with: recorded logs, parsed into float64 as the reference parses
+    them (ReadFile.py:14-21), where IMUWindow's 40 B record would round them to f32.
+
+    Planes [window][batch]: gd double4 {gyro xyz, dt_ns}, am double4 {acc xyz, mag x}, my double2
+    {mag yz}; dt is the float64 T - previousT itself (any pause, clock step or fraction).  Every record
+    is a full record (no missing-magnetometer flag).  BatchedEKF.run / run_async take it like an
+    IMUWindow (FP64 AoS state)."""
+
+    def __init__(self, batch, window):
+        self.batch, self.window = int(batch), int(window)
+        n = self.batch * self.window
+        self.gd = DeviceBuffer(32 * n)
+        self.am = DeviceBuffer(32 * n)
+        self.my = DeviceBuffer(16 * n)
+        self.refs = DeviceBuffer(48 * self.batch)
+        self.counts = None  # per-filter valid record counts when filters are ragged (logs)
+
+    @property
+    def nbytes(self):
+        return self.gd.nbytes + self.am.nbytes + self.my.nbytes
+
+    @classmethod
+    def from_arrays(cls, gyro, dt_ns, acc, mag, acc0, mag0):
+        """gyro / acc / mag (W, K, 3), dt_ns (W, K) float64 (the reference's T - previousT); acc0 / mag0
+        (K, 3) the reference pairs (KalmanFilter(T0, mag_0, acc_0))."""
+        gyro, acc, mag = (np.asarray(a, np.float64) for a in (gyro, acc, mag))
+        W, K = gyro.shape[:2]
+        dt = np.asarray(dt_ns, np.float64).reshape(W, K)
+        win = cls(K, W)
+        win.gd.upload(np.ascontiguousarray(np.concatenate([gyro, dt[..., None]], axis=2)))
+        win.am.upload(np.ascontiguousarray(np.concatenate([acc, mag[..., :1]], axis=2)))
+        win.my.upload(np.ascontiguousarray(mag[..., 1:]))
+        win.refs.upload(synth.refs_array(np.asarray(acc0, np.float64).reshape(K, 3),
+                                         np.asarray(mag0, np.float64).reshape(K, 3)))
+        return win
+
+    @classmethod
+    def from_logs(cls, paths, n_records=None):
+        """One filter per server log, parsed natively into float64 (pekf_log_read64); ragged logs as
+        IMUWindow.from_logs (zero-padded, win.counts = each filter's own record count)."""
+        cols = []
+        for p in paths:
+            bpath = os.fsencode(p)
+            n = ctypes.c_int64()
+            check(lib.pekf_log_scan(bpath, ctypes.byref(n)))
+            g, a, m = (np.empty((n.value, 3)) for _ in range(3))
+            dt = np.empty(n.value)
+            a0, m0, t0 = np.empty(3), np.empty(3), ctypes.c_double()
+            check(lib.pekf_log_read64(bpath, n.value, g.ctypes.data, a.ctypes.data, m.ctypes.data, dt.ctypes.data,
+                                      dptr(a0), dptr(m0), ctypes.byref(t0)))
+            cols.append((g, dt, a, m, a0, m0))
+        lens = np.array([c[1].shape[0] for c in cols], np.int64)
+        W = int(lens.max()) if n_records is None else int(n_records)
+
+        def stack(i, shape):
+            out = np.zeros((W, len(cols)) + shape)
+            for k, c in enumerate(cols):
+                m = min(W, c[i].shape[0])
+                out[:m, k] = c[i][:m]
+            return out
+        win = cls.from_arrays(stack(0, (3,)), stack(1, ()), stack(2, (3,)), stack(3, (3,)),
+                              np.stack([c[4] for c in cols]), np.stack([c[5] for c in cols]))
+        win.counts = np.minimum(lens, W).astype(np.int32)
+        return win
+
+
 # ------------------------------------------------------------------ server front-end (raw events)
 
 def _event_planes(ev):
@@ -430,10 +498,17 @@ class BatchedEKF:
     def run_async(self, win: IMUWindow, n_steps, step0=0, stream=None, traj=None, counts=None):
         """Enqueue one fused launch; traj: optional DeviceBuffer of n_steps*batch*32 bytes;
         counts: optional DeviceBuffer of batch int32 (filter b applies its first counts[b] records).
-        A window with a dt side plane (escaped records) runs pekf_run_ext_dev with it."""
+        A window with a dt side plane (escaped records) runs pekf_run_ext_dev with it; a RecordWindow64
+        (FP64 records) runs pekf_run_rec64_dev."""
         assert win.batch == self.batch
         tr, cn = traj.ptr if traj is not None else None, counts.ptr if counts is not None else None
-        if win.dtx is None:
+        if isinstance(win, RecordWindow64):
+            if self.layout != "aos" or self.flags & RUN_MIXED_PRECISION:
+                raise ValueError("FP64-record windows run the FP64 filter on AoS state")
+            check(lib.pekf_run_rec64_dev(self.batch, int(n_steps), win.window, int(step0), win.gd.ptr, win.am.ptr,
+                                         win.my.ptr, win.refs.ptr, self.X.ptr, self.P.ptr, self.q, self.r, tr, cn,
+                                         stream))
+        elif win.dtx is None:
             check(lib.pekf_run_dev(self.batch, int(n_steps), win.window, int(step0), win.gd.ptr, win.am.ptr,
                                    win.my.ptr, win.refs.ptr, self.X.ptr, self.P.ptr, self.q, self.r, tr, cn,
                                    self.flags, stream))

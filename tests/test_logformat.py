@@ -127,3 +127,38 @@ def test_native_ingest_takes_lines_of_any_length(tmp_path):
     gp, dt_py, ap, mp, _, _ = logformat.log_to_arrays(logformat.read_log(str(path)))
     assert got.dtw.shape == (6, 1) and np.array_equal(got.dt_ns[:, 0], dt_py)
     assert np.array_equal(got.gyro[:, 0], gp.astype(np.float32)) and got.gyro[0, 0].tolist() == [0.25, -0.5, 0.125]
+
+
+def _read64(path):
+    import ctypes
+
+    from poseestimationkf_amd import _lib
+    bpath = os.fsencode(path)
+    n = ctypes.c_int64()
+    _lib.check(_lib.lib.pekf_log_scan(bpath, ctypes.byref(n)))
+    g, a, m = (np.empty((n.value, 3)) for _ in range(3))
+    dt, a0, m0, t0 = np.empty(n.value), np.empty(3), np.empty(3), ctypes.c_double()
+    _lib.check(_lib.lib.pekf_log_read64(bpath, n.value, g.ctypes.data, a.ctypes.data, m.ctypes.data, dt.ctypes.data,
+                                        _lib.dptr(a0), _lib.dptr(m0), ctypes.byref(t0)))
+    return g, dt, a, m, a0, m0, t0.value
+
+
+def test_native_ingest_float64_matches_python_reader(c1_log, tmp_path):
+    """pekf_log_read64 (the FP64 records of pekf_run_rec64_dev): the log's values exactly as the Python
+    reader (ReadFile.py:14-21's float64) parses them, dt = T[i+1] - T[i] as the reference forms it --
+    on config 1's log and on a log with pauses and a clock stepping back."""
+    g, dt, a, m, a0, m0, _ = _read64(c1_log)
+    want = logformat.log_to_arrays(logformat.read_log(c1_log))
+    for got, w in zip((g, dt, a, m, a0, m0), want):
+        assert np.array_equal(got, w)
+    rng = np.random.default_rng(4)
+    n = 40
+    ts = 1e15 + np.cumsum(rng.choice([1e7, 3.5e9, -2e6, 1234.0], size=n + 1))
+    path = tmp_path / "odd.txt"
+    logformat.write_log(str(path), ts, rng.normal(size=(n, 3)), rng.normal(size=(n, 3)) + [0, 0, 9.8],
+                        rng.normal(size=(n, 3)) * 30, [0.1, 0.2, 9.8], [20.0, 1.0, -40.0])
+    got = _read64(str(path))
+    want = logformat.log_to_arrays(logformat.read_log(str(path)))
+    for x, w in zip(got[:6], want):
+        assert np.array_equal(x, w)
+    assert (got[1] < 0).any() and got[1].max() > 2 ** 31   # (the writer's "T : %d" keeps integer ns)
