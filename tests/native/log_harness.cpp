@@ -1,7 +1,7 @@
 // Host-only harness for the native log reader (csrc/pekf_log.cpp) under AddressSanitizer and
 // UndefinedBehaviorSanitizer (tests/test_log_sanitizers.py builds and runs it; no GPU, no HIP).
-// Each argument is a log path: scan it, then read it with and without the dt side plane and with one
-// record too many.  pekf::set_error (pekf_capi.hip in the library) is replaced by a printing stub.
+// Each argument is a log path: scan it, then read it with and without the dt side plane, as float64
+// records, and with one record too many.  pekf::set_error (pekf_capi.hip in the library) is replaced by a printing stub.
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -37,7 +37,12 @@ int main(int argc, char **argv) {
             const int plain = pekf_log_read(argv[i], n, g.data(), a.data(), m.data(), dtw.data(), acc0, mag0, &t0);
             const int over = pekf_log_read_ext(argv[i], n + 1, g.data(), a.data(), m.data(), dtw.data(), dtx.data(),
                                                &esc, acc0, mag0, &t0);
-            printf(" ext=%d escaped=%lld plain=%d over=%d", ext, (long long)esc, plain, over);
+            std::vector<double> g64(3 * n), a64(3 * n), m64(3 * n), dt64(n);
+            const int r64 = pekf_log_read64(argv[i], n, g64.data(), a64.data(), m64.data(), dt64.data(), acc0, mag0, &t0);
+            const int over64 =
+                pekf_log_read64(argv[i], n + 1, g64.data(), a64.data(), m64.data(), dt64.data(), acc0, mag0, &t0);
+            printf(" ext=%d escaped=%lld plain=%d over=%d r64=%d over64=%d", ext, (long long)esc, plain, over, r64,
+                   over64);
         }
         printf("\n");
     }
