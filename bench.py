@@ -3,8 +3,9 @@
 
 One bench "step" = one fused launch (pekf_run_dev) per GPU that advances every filter of that
 GPU's shard by --records IMU records (config 3 of BASELINE.json: 1,048,576 filters, 10,000
-records), followed, when more than one GPU takes part, by ONE RCCL gather of the final
-quaternions to the root.  Inputs are a resident window of --window records per filter (40 B per
+records).  When more than one GPU takes part, the timed run ends with ONE RCCL gather of the final
+quaternions to the root (the north_star's single gather; the shards exchange nothing per step, so
+the GPUs run their steps independently).  Inputs are a resident window of --window records per filter (40 B per
 filter-record, 43 GB at config 3 -- far beyond the 256 MB Infinity Cache), generated on the device
 by the Philox generator before timing and replayed cyclically, so every record is read from HBM.
 
@@ -18,12 +19,12 @@ Either way each GPU owns an equal contiguous shard of filters (weak scaling), an
 non-zero when fewer than N GPUs are visible.
 
 Prints ONE JSON line on rank 0.  `value` = filter-steps/s over all GPUs (the slowest rank's wall
-clock, gather included).  `roofline` is the fused kernel's achieved algorithmic HBM read rate per
+clock, the final gather included).  `roofline` is the fused kernel's achieved algorithmic HBM read rate per
 GPU (40 B x filters x records / kernel time, HIP events on the launch stream) against the 8 TB/s
 peak; `valu_roofline` is the resource that binds it, FP64 VALU issue; `cpu_baseline` times the
 NumPy restatement of the reference loop on the job's host cores (rank 0, at every N, a bounded
 sample, before any GPU work; the core count comes from the cgroup's CPU quota / cpuset);
-`kernel_ms_per_gpu` / `gather_ms_per_gpu` attribute each GPU's share of the step.
+`kernel_ms_per_gpu` / `gather_ms_per_gpu` attribute each GPU's time to its launches and the gather.
 A rank that never joins or dies mid-run fails the job within PEKF_COMM_TIMEOUT_S (status 2).
 """
 from __future__ import annotations
@@ -290,7 +291,7 @@ def c_oracle_rate(seed, missing, n_filters=64, n_rec=1000):
 # ----------------------------------------------------------------------------------- the runs
 class RankRun:
     """One process = one GPU (modes "single" and "ranks"): this rank's shard as an IMUWindow +
-    BatchedEKF on device `dev`; with a communicator, each step ends with the RCCL gather to rank 0."""
+    BatchedEKF on device `dev`; with a communicator, gather() sends its final quaternions to rank 0."""
 
     def __init__(self, args, plan, rdzv=None):
         import numpy as np
@@ -319,8 +320,11 @@ class RankRun:
         self.ev = []
 
     def prepare(self, n_steps):
-        """ev[k] = (kernel start, kernel end, gather end) HIP events of step k on this rank's stream."""
-        self.ev = [tuple(self.engine.Event() for _ in range(3)) for _ in range(n_steps)]
+        """ev[k] = (kernel start, kernel end) HIP events of step k on this rank's stream; gev = (start,
+        end) of the last gather."""
+        self.ev = [tuple(self.engine.Event() for _ in range(2)) for _ in range(n_steps)]
+        self.gev = (self.engine.Event(), self.engine.Event())
+        self.gathered = False
 
     def sync(self):
         if self.comm is not None:  # drains the stream's collectives too, against PEKF_COMM_TIMEOUT_S
@@ -333,28 +337,36 @@ class RankRun:
             self.comm.barrier(self.stream)
 
     def step(self, k, n_rec, row0):
-        e0, e1, e2 = self.ev[k]
+        e0, e1 = self.ev[k]
         e0.record(self.stream)
         self.filt.run_async(self.win, n_rec, row0, self.stream)
         e1.record(self.stream)
-        if self.comm is not None:  # ONE RCCL gather of the final quaternions to rank 0 (pekf_gather_dev)
-            self.shard.gather_quaternions(self.comm, self.filt.X.ptr, self.B, self.recv, 0, self.stream)
-        e2.record(self.stream)
+
+    def gather(self):
+        """ONE RCCL gather of the current quaternions to rank 0 (pekf_gather_dev), enqueued after the
+        launches; its time includes waiting for the slowest peer's last launch."""
+        if self.comm is None:
+            return
+        g0, g1 = self.gev
+        g0.record(self.stream)
+        self.shard.gather_quaternions(self.comm, self.filt.X.ptr, self.B, self.recv, 0, self.stream)
+        g1.record(self.stream)
+        self.gathered = True
 
     def kernel_ms(self, k):
         return self.ev[k][0].elapsed_ms(self.ev[k][1])
 
-    def gather_ms(self, k):
-        return self.ev[k][1].elapsed_ms(self.ev[k][2])
+    def gather_ms(self):
+        return self.gev[0].elapsed_ms(self.gev[1]) if self.gathered else 0.0
 
     def slowest(self, elapsed):
         return self.comm.max_over_ranks(elapsed, self.stream) if self.comm is not None else elapsed
 
     def per_gpu(self, steps):
-        """(kernel ms, gather ms) per GPU in rank order, each the mean over `steps`: every rank's own
-        HIP-event times, exchanged with one RCCL all-reduce (collective: all ranks call it)."""
-        mine = [float(self.np.mean([self.kernel_ms(k) for k in steps])),
-                float(self.np.mean([self.gather_ms(k) for k in steps]))]
+        """(kernel ms, gather ms) per GPU in rank order -- the mean launch time over `steps` and the final
+        gather's time: every rank's own HIP-event times, exchanged with one RCCL all-reduce (collective:
+        all ranks call it)."""
+        mine = [float(self.np.mean([self.kernel_ms(k) for k in steps])), float(self.gather_ms())]
         if self.comm is None:
             return [mine[0]], [mine[1]]
         allv = self.comm.all_values(mine, self.stream)
@@ -379,8 +391,8 @@ class RankRun:
 
 
 class MultiRun:
-    """One process drives GPUs 0..N-1 (mode "multi"): shard.MultiDeviceEKF, one grouped RCCL gather
-    per step.  Kernel times are per-device HIP events on each device's own stream."""
+    """One process drives GPUs 0..N-1 (mode "multi"): shard.MultiDeviceEKF, the final quaternions
+    collected by one grouped RCCL gather.  Times are per-device HIP events on each device's own stream."""
 
     def __init__(self, args, plan):
         from poseestimationkf_amd import engine, shard
@@ -395,15 +407,21 @@ class MultiRun:
         self.ev = []
 
     def prepare(self, n_steps):
-        """HIP events are per device: ev[k][i] = (kernel start, kernel end, gather end) of step k on device i."""
+        """HIP events are per device: ev[k][i] = (kernel start, kernel end) of step k on device i, gev[i] =
+        (start, end) of the last gather on device i."""
         self.ev = []
         for _ in range(n_steps):
-            trip = []
+            pair = []
             for d in self.devices:
                 self.engine.set_device(d)
-                trip.append(tuple(self.engine.Event() for _ in range(3)))
-            self.ev.append(trip)
+                pair.append(tuple(self.engine.Event() for _ in range(2)))
+            self.ev.append(pair)
+        self.gev = []
+        for d in self.devices:
+            self.engine.set_device(d)
+            self.gev.append((self.engine.Event(), self.engine.Event()))
         self.engine.set_device(self.devices[0])
+        self.gathered = False
 
     def sync(self):
         self.m.sync()
@@ -414,25 +432,35 @@ class MultiRun:
     def step(self, k, n_rec, row0):
         for i, d in enumerate(self.devices):
             self.engine.set_device(d)
-            e0, e1, _ = self.ev[k][i]
+            e0, e1 = self.ev[k][i]
             s = self.m.streams[i].handle
             e0.record(s)
             self.m.filts[i].run_async(self.m.wins[i], n_rec, row0, s)
             e1.record(s)
         self.engine.set_device(self.devices[0])
+
+    def gather(self):
+        """The final quaternions of every device to device 0: one grouped RCCL gather."""
+        for i, d in enumerate(self.devices):
+            self.engine.set_device(d)
+            self.gev[i][0].record(self.m.streams[i].handle)
+        self.engine.set_device(self.devices[0])
         self.m.gather_async()
         for i, d in enumerate(self.devices):
             self.engine.set_device(d)
-            self.ev[k][i][2].record(self.m.streams[i].handle)
+            self.gev[i][1].record(self.m.streams[i].handle)
         self.engine.set_device(self.devices[0])
+        self.gathered = True
 
     def kernel_ms(self, k, device_index=None):
         """The slowest device's kernel time of step k (or one device's)."""
         t = [e[0].elapsed_ms(e[1]) for e in self.ev[k]]
         return max(t) if device_index is None else t[device_index]
 
-    def gather_ms(self, k, device_index=None):
-        t = [e[1].elapsed_ms(e[2]) for e in self.ev[k]]
+    def gather_ms(self, device_index=None):
+        if not self.gathered:
+            return 0.0
+        t = [g[0].elapsed_ms(g[1]) for g in self.gev]
         return max(t) if device_index is None else t[device_index]
 
     def slowest(self, elapsed):
@@ -440,8 +468,8 @@ class MultiRun:
 
     def per_gpu(self, steps):
         n = len(self.devices)
-        mean = lambda f: [sum(f(k, i) for k in steps) / len(steps) for i in range(n)]  # noqa: E731
-        return mean(self.kernel_ms), mean(self.gather_ms)
+        return ([sum(self.kernel_ms(k, i) for k in steps) / len(steps) for i in range(n)],
+                [self.gather_ms(i) for i in range(n)])
 
     def final_rows(self):
         return 0, self.m.gathered()
@@ -564,14 +592,18 @@ def _main(argv=None):
 
     for k in range(args.warmup):
         run.step(k, N, (k * N) % W)
+        if k == args.warmup - 1:
+            run.gather()   # the communicator's first collective pays RCCL's connection setup: not timed
         run.sync()
-        log("warmup %d: kernel %.1f ms, gather %.3f ms" % (k, run.kernel_ms(k), run.gather_ms(k)))
+        log("warmup %d: kernel %.1f ms%s" % (k, run.kernel_ms(k), ", gather %.3f ms" % run.gather_ms()
+                                            if k == args.warmup - 1 else ""))
 
     run.sync()
     run.barrier()
     t0 = time.perf_counter()
     for k in range(args.warmup, total):
         run.step(k, N, (k * N) % W)
+    run.gather()           # ONE gather of the final quaternions, inside the timed region
     run.sync()
     run.barrier()
     elapsed = run.slowest(time.perf_counter() - t0)
@@ -636,7 +668,7 @@ def result_line(args, plan, elapsed, kms, cpu, parity, per_gpu=None):
                    "window_records": args.window,
                    "first_filter": plan["first_shard"] * B if plan["mode"] == "single" else 0,
                    "parallelism": "dp%d (filter-batch shards%s)" % (
-                       world, ", 1 RCCL gather of final quaternions per step"
+                       world, ", no per-step exchange, 1 RCCL gather of the final quaternions"
                        if world > 1 or args.dist or plan["mode"] == "multi" else ""),
                    "launch": launch},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -669,8 +701,9 @@ def result_line(args, plan, elapsed, kms, cpu, parity, per_gpu=None):
         "parity": parity,
         "kernel_ms_per_gpu": per_gpu[0],
         "gather_ms_per_gpu": per_gpu[1],
-        "timing_note": "per GPU, in rank order: the fused launch's and the RCCL gather's mean HIP-event time "
-                       "over the timed steps on that GPU's stream (gather 0 when nothing is gathered); "
+        "timing_note": "per GPU, in rank order: the fused launch's mean HIP-event time over the timed steps and "
+                       "the final RCCL gather's time on that GPU's stream (it includes waiting for the slowest "
+                       "peer's last launch; 0 when nothing is gathered); "
                        "ms_per_step is the slowest rank's wall clock",
     }
 

@@ -4,8 +4,8 @@ RCCL between processes).  Everything above the C ABI -- bench.py, engine.py, sha
 code the driver's 8-GPU run executes:
 
 * one process over 8 devices (`bench.py --gpus 8`: shard.MultiDeviceEKF, ncclCommInitAll, one
-  grouped gather per step);
-* one process per rank (`torchrun ... bench.py --gpus 2` and `--gpus 4`: FileRendezvous, RCCL init, per-step
+  grouped gather of the final quaternions);
+* one process per rank (`torchrun ... bench.py --gpus 2`, `4` and `8`: FileRendezvous, RCCL init, the final
   gather, max-over-ranks time, per-GPU timings exchanged by one all-reduce);
 * rank 0 failing before it has an RCCL id: the other rank stops waiting and exits 2 at once;
 * the one-process mode failing instead of hanging: a grouped gather that never completes on one of
@@ -78,7 +78,7 @@ def test_one_process_eight_devices(monkeypatch, capfd):
     _check_line(d, 8)
     assert "ncclCommInitAll" in d["config"]["launch"] and d["config"]["workload"].startswith("custom")
     assert fake.calls.count("pekf_comm_init_all") == 1
-    assert fake.calls.count("pekf_gather_multi_dev") == 3          # warmup + 2 timed steps
+    assert fake.calls.count("pekf_gather_multi_dev") == 2          # after the warmup + ONE after the timed steps
     assert sorted({r[0] for r in fake.runs}) == list(range(8))     # every device ran its shard
     assert all(r[1:] == (256, 16, (k // 8) * 16 % 8) for k, r in enumerate(fake.runs))
 
