@@ -35,6 +35,17 @@ typedef float nv4f __attribute__((ext_vector_type(4)));  // the native vector th
 #ifndef PEKF_FE_STAGE_THR
 #define PEKF_FE_STAGE_THR 56
 #endif
+// Lanes that share the queue's base row: 64 = the whole wave (round 4); 8 = each group of 8 lanes keeps
+// its own base (a row of 8 lanes is one 128 B line of the gd / am planes), writes its row once all its
+// ready lanes hold it (GROUP_THR), and drifts apart from the other groups: WRITE_SIZE 1.72x -> 1.59x
+// the record bytes, -0.8 % time at the same LDS (profiles/r5/frontend_group/; deeper queues reach 1.27x
+// but lose a third of the waves per CU and 20 % of the time).
+#ifndef PEKF_FE_GROUP
+#define PEKF_FE_GROUP 8
+#endif
+#ifndef PEKF_FE_GROUP_THR
+#define PEKF_FE_GROUP_THR (PEKF_FE_GROUP == 64 ? PEKF_FE_STAGE_THR : PEKF_FE_GROUP)
+#endif
 
 // The staged form's LDS: each lane's queued records, one row per slot (row % S), lane-minor so a
 // lane's accesses are its own column (no other lane reads them: no barrier).
@@ -89,7 +100,10 @@ __global__ __launch_bounds__(STG ? 64 : kFeBlock) void k_frontend(int64_t batch,
     constexpr int kS = STG ? STG : 1;
     __shared__ FeStage<kS> st;
     const int col = threadIdx.x & 63;
-    int32_t base = 0;   // STG: the oldest row the wave's queue holds (wave-uniform)
+    constexpr int kG = PEKF_FE_GROUP;
+    static_assert(kG == 8 || kG == 16 || kG == 32 || kG == 64, "lane groups of 8, 16, 32 or 64");
+    // STG: the oldest row the queue holds -- wave-uniform for kG = 64, else the same in each group of kG lanes
+    int32_t base = 0;
     uint32_t held = 0;  // STG: bit row % STG = this lane's record for that row is queued
     // the pending record (Phase3::pend) is emitted every kFlush events; a lane never has two
     constexpr int kFlush = 3;
@@ -121,22 +135,48 @@ __global__ __launch_bounds__(STG ? 64 : kFeBlock) void k_frontend(int64_t batch,
     // STG: write out queued rows -- while few enough ready lanes still lack row base, or (all) until
     // no lane holds any
     auto drain = [&](bool all) {
-        for (;;) {
-            if (all) {
-                if (!__any(held != 0)) break;
-            } else {
-                const int behind = __popcll(__ballot(ready && r <= base && r < rmax));
-                if (behind > 64 - PEKF_FE_STAGE_THR || !__any(held != 0)) break;
+        if constexpr (kG == 64) {
+            for (;;) {
+                if (all) {
+                    if (!__any(held != 0)) break;
+                } else {
+                    const int behind = __popcll(__ballot(ready && r <= base && r < rmax));
+                    if (behind > 64 - PEKF_FE_STAGE_THR || !__any(held != 0)) break;
+                }
+                const int sl = base % kS;
+                if (held & (1u << sl)) {
+                    const int64_t o = (int64_t)base * batch + b;
+                    gd[o] = st.gd[sl][col];
+                    am[o] = st.am[sl][col];
+                    my[o] = st.my[sl][col];
+                    held &= ~(1u << sl);
+                }
+                ++base;
             }
-            const int sl = base % kS;
-            if (held & (1u << sl)) {
-                const int64_t o = (int64_t)base * batch + b;
-                gd[o] = st.gd[sl][col];
-                am[o] = st.am[sl][col];
-                my[o] = st.my[sl][col];
-                held &= ~(1u << sl);
+        } else {
+            // this lane's group's bits of a wave ballot
+            const int shift = col & ~(kG - 1);
+            constexpr uint64_t kMask = kG == 64 ? ~0ull : (1ull << (kG & 63)) - 1;
+            for (;;) {
+                const uint64_t anyheld = (__ballot(held != 0) >> shift) & kMask;
+                bool go = anyheld != 0;
+                if (!all) {
+                    const uint64_t behind = (__ballot(ready && r <= base && r < rmax) >> shift) & kMask;
+                    go = go && __popcll(behind) <= kG - PEKF_FE_GROUP_THR;
+                }
+                if (!__any(go)) break;
+                if (go) {
+                    const int sl = base % kS;
+                    if (held & (1u << sl)) {
+                        const int64_t o = (int64_t)base * batch + b;
+                        gd[o] = st.gd[sl][col];
+                        am[o] = st.am[sl][col];
+                        my[o] = st.my[sl][col];
+                        held &= ~(1u << sl);
+                    }
+                    ++base;
+                }
             }
-            ++base;
         }
     };
 
