@@ -110,3 +110,27 @@ def test_rec64_ragged_logs_in_one_launch(eng, tmp_path):
         g, dt, a, m, a0, m0 = logformat.log_to_arrays(logformat.read_log(p))
         Xo, _, _ = npo.run_filter(g, dt, a, m, a0, m0, record=False)
         assert float(np.abs(X[k] - Xo).max()) < ATOL_F64, k
+
+
+def test_rec64_nan_record_poisons_only_its_filter(eng):
+    """A NaN sample, where the reference's SVD raises LinAlgError (Wahba.py:14): inside a batch the filter
+    cannot raise, so that filter's state turns NaN (pekf.h, as pekf_run_dev) and every other filter is
+    unaffected -- equal to the same launch without the bad filter."""
+    K, W = 128, 40
+    rng = np.random.default_rng(21)
+    g = rng.normal(scale=0.5, size=(W, K, 3))
+    a = rng.normal(scale=0.3, size=(W, K, 3)) + [0.0, 0.0, 9.8]
+    m = rng.normal(scale=2.0, size=(W, K, 3)) + [20.0, 1.0, -40.0]
+    dt = np.full((W, K), 1.0e7)
+    a0 = np.tile([0.1, 0.2, 9.8], (K, 1))
+    m0 = np.tile([20.0, 1.0, -40.0], (K, 1))
+    bad = a.copy()
+    bad[17, 77, 1] = np.nan
+    out = []
+    for acc in (a, bad):
+        f = eng.BatchedEKF(K)
+        f.run(eng.RecordWindow64.from_arrays(g, dt, acc, m, a0, m0))
+        out.append(f.get_state()[0])
+    assert np.isnan(out[1][77]).all()
+    keep = np.arange(K) != 77
+    assert np.array_equal(out[0][keep], out[1][keep]) and np.isfinite(out[0]).all()
