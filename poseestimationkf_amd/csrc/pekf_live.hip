@@ -4,10 +4,10 @@
 // Correction of each record (pekf_step.hpp, ExtendedKalmanFilter.py:58-80 as main_file.py:42-45 calls
 // them).  One lane per filter holds its front-end state, X and covariance in registers; records never
 // touch memory.  A record's acc / mag stay the FP64 low-pass outputs (the server's filter input,
-// KFS/KalmanFilter.cpp:279-303) in a 4-deep queue; PEKF_EV_F32_RECORDS rounds them to the f32 stream
-// record in a 6-deep queue instead -- the same 18 KB of LDS per wave -- and then equals the split
-// pipeline bit for bit.  FP64 costs +2.4-3.0 % (4.77 -> 4.88 ms at 1M filters x 1,024 events, same-box
-// ABBA, profiles/r5/live_records/): the shallower queue runs ~11 % more filter steps.  The split pipeline -- pekf_frontend_dev writing records to the stream planes, then
+// KFS/KalmanFilter.cpp:279-303) in a 5-deep queue (20 KB per wave); PEKF_EV_F32_RECORDS rounds them to
+// the f32 stream record in a 6-deep queue instead (18 KB) and then equals the split pipeline bit for
+// bit.  FP64 costs +1.5-1.8 % at 1M filters x 1,024 events (same-box ABBA, profiles/r5/live_q5/): the
+// shallower queue runs more filter steps with fewer lanes busy.  The split pipeline -- pekf_frontend_dev writing records to the stream planes, then
 // pekf_run_dev with counts reading them back -- pays a 40 B record write that scatters into 96 B of
 // sectors (each lane's record count drifts, so a wave's stores land in 64 different rows) plus the
 // 40 B read; here the only HBM traffic is the 16 B event.
@@ -44,7 +44,7 @@ namespace pekf {
 #define PEKF_LIVE_QUEUE 6  // records a lane can hold (48 B of LDS each: the 40 B record + its escaped dt)
 #endif
 #ifndef PEKF_LIVE_QUEUE64
-#define PEKF_LIVE_QUEUE64 4  // the same with FP64 acc / mag (72 B each): the same 18 KB of LDS per wave
+#define PEKF_LIVE_QUEUE64 5  // the same with FP64 acc / mag (64 B each): 20 KB of LDS per wave, all of it
 #endif
 #ifndef PEKF_LIVE_QUORUM
 #define PEKF_LIVE_QUORUM 56  // lanes of 64 with a queued record that trigger a filter step
@@ -115,6 +115,7 @@ struct LdsQueue {
         my = reinterpret_cast<float2(*)[kRunBlock]>(lds + (2 * sizeof(float4) + sizeof(double)) * Q * kRunBlock);
     }
     __device__ __forceinline__ int tail() const { return head + n < Q ? head + n : head + n - Q; }
+    __device__ __forceinline__ bool esc_queued() const { return false; }  // escaped dts live in the dt plane
     __device__ __forceinline__ void push(const Rec &r, bool esc, double dtv) {
         const int slot = tail();
         gd[slot][threadIdx.x] = r.gd;
@@ -153,26 +154,31 @@ struct LdsQueue {
 
 // The queue with FP64 acc / mag: what the server's filter receives (KFS/KalmanFilter.cpp:279-303 hands
 // the double low-pass outputs to Prediction / Correction), not the f32 stream record.  Per slot the
-// gyro / dt word (16 B), acc and mag as three double2 planes (48 B) and the escaped dt (8 B).
+// gyro / dt word (16 B) and acc and mag as three double2 planes (48 B): 5 slots x 64 B x 64 lanes is
+// 20 KB per wave, exactly the CU's 160 KB at 2 waves per SIMD, so there is no room for an escaped-dt
+// plane.  A record whose dt does not fit the dt word keeps its float64 dt in a register instead
+// (esc_dt), one per lane: k_live steps a wave while any lane still has such a record queued, so a lane
+// never holds two (escapes are pauses of 2.1 s or more: rare, and cheap to drain for).
 template <int Q>
 struct LdsQueue64 {
-    static constexpr size_t kBytes = (sizeof(float4) + 3 * sizeof(double2) + sizeof(double)) * Q * kRunBlock;
+    static constexpr size_t kBytes = (sizeof(float4) + 3 * sizeof(double2)) * Q * kRunBlock;
     float4 (*gd)[kRunBlock];
     double2 (*am)[3][kRunBlock];  // {acc.x, acc.y}, {acc.z, mag.x}, {mag.y, mag.z}
-    double (*dt)[kRunBlock];
+    double esc_dt = __builtin_nan("");  // the queued escaped record's dt (NaN: none queued)
     int head = 0, n = 0;
     __device__ __forceinline__ void bind(unsigned char *lds) {
         am = reinterpret_cast<double2(*)[3][kRunBlock]>(lds);
         gd = reinterpret_cast<float4(*)[kRunBlock]>(lds + 3 * sizeof(double2) * Q * kRunBlock);
-        dt = reinterpret_cast<double(*)[kRunBlock]>(lds + (3 * sizeof(double2) + sizeof(float4)) * Q * kRunBlock);
     }
+    // a lane has an escaped record queued (k_live then steps until it is applied)
+    __device__ __forceinline__ bool esc_queued() const { return esc_dt == esc_dt; }
     __device__ __forceinline__ void push(const float4 &g, const V3 &a, const V3 &m, bool esc, double dtv) {
         const int slot = head + n < Q ? head + n : head + n - Q;
         gd[slot][threadIdx.x] = g;
         am[slot][0][threadIdx.x] = make_double2(a.x, a.y);
         am[slot][1][threadIdx.x] = make_double2(a.z, m.x);
         am[slot][2][threadIdx.x] = make_double2(m.y, m.z);
-        if (esc) dt[slot][threadIdx.x] = dtv;
+        if (esc) esc_dt = dtv;
         ++n;
     }
     struct Slot {
@@ -183,7 +189,10 @@ struct LdsQueue64 {
         const Slot r = {gd[head][threadIdx.x], {am[head][0][threadIdx.x], am[head][1][threadIdx.x], am[head][2][threadIdx.x]}};
         const uint32_t word = __float_as_uint(r.gd.w) & PEKF_DT_MASK;
         dtv = (double)word;
-        if (word == PEKF_DT_ESCAPE) dtv = dt[head][threadIdx.x];
+        if (n > 0 && word == PEKF_DT_ESCAPE) {
+            dtv = esc_dt;
+            esc_dt = __builtin_nan("");
+        }
         if (n > 0) {
             head = head + 1 < Q ? head + 1 : 0;
             --n;
@@ -328,10 +337,12 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
 #endif
     };
     // wave-uniform: a step while some lane could overflow in the next block, then one more if a quorum
-    // of lanes has a record; after the last event until every queue is empty
+    // of lanes has a record; after the last event until every queue is empty; (R64) while some lane
+    // still has an escaped record queued, so the next block cannot queue a second one on that lane
     auto want_step = [&](bool last) {
         const uint64_t queued = __ballot(queue.n > 0);
-        return queued != 0 && (last || __any(queue.n > kQueue - kPush) || __popcll(queued) >= kQuorum);
+        return queued != 0 && (last || __any(queue.n > kQueue - kPush) || __popcll(queued) >= kQuorum ||
+                               (R64 && __any(queue.esc_queued())));
     };
     auto steps = [&](bool last) {
         // tested before the loop, so a block that runs no step does not pass the loop's header
