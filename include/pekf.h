@@ -209,6 +209,14 @@ int pekf_gyro_chain_ext_dev(int64_t batch, int64_t n_steps, int64_t window, int6
 int pekf_wahba_stream_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,
                           const void *plane_am, const void *plane_my, const double *refs, double k_acc,
                           double k_mag, double *out, void *stream);
+/* The pure-gyro chain and the pure-Wahba stream over FP64 records (pekf_run_rec64_dev's planes: the gd
+ * plane double4 {gyro xyz, dt_ns}, am double4 {acc xyz, mag x}, my double2 {mag yz}); the same arithmetic as
+ * the two above, dt the float64 itself. */
+int pekf_gyro_chain_rec64_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0, const void *plane_gd,
+                              double *q_gyro, double *traj, void *stream);
+int pekf_wahba_stream_rec64_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0, const void *plane_am,
+                                const void *plane_my, const double *refs, double k_acc, double k_mag, double *out,
+                                void *stream);
 /* UtilityFunctions.Quart2RPY(q), UtilityFunctions.py:3-14: q[n*4] -> rpy[n*3] in degrees. */
 int pekf_quat_to_rpy(int64_t n, const double *q, double *rpy);
 int pekf_quat_to_rpy_dev(int64_t n, const double *q, double *rpy, void *stream);

@@ -109,6 +109,8 @@ SIGNATURES = {
     "pekf_gyro_chain_ext_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp],
     "pekf_wahba_stream_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp],
     "pekf_quat_to_rpy": [_i64, _vp, _vp],
+    "pekf_gyro_chain_rec64_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
+    "pekf_wahba_stream_rec64_dev": [_i64, _i64, _i64, _i64, _vp, _vp, _vp, _dbl, _dbl, _vp, _vp],
     "pekf_frontend_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "pekf_frontend_ext_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp],
     "pekf_frontend_init_dev": [_i64, _i64, _vp, _vp, _int, _vp, _vp, _vp, _vp, _vp],

@@ -146,6 +146,113 @@ __global__ __launch_bounds__(kSideBlock) void k_wahba_stream(int64_t batch, int6
     }
 }
 
+// The same two side outputs over FP64 records (pekf_run_rec64_dev's planes: gd double4 {gyro xyz, dt_ns},
+// am double4 {acc xyz, mag x}, my double2 {mag yz}), so a log replayed in FP64 gets its q_gyro / Wahba
+// attitudes from the values as parsed.  The arithmetic is the 40 B-record kernels' line for line (on
+// f32-representable values the results are bit-identical); dt is the float64 itself.  Shallower rings:
+// a record is 32-48 B of registers here.
+constexpr int kDepth64 = 4;
+
+__global__ __launch_bounds__(kSideBlock) void k_gyro_chain64(int64_t batch, int64_t n_steps, int64_t window,
+                                                             int64_t step0, const double4 *__restrict__ gd,
+                                                             double *__restrict__ q, double *__restrict__ traj) {
+    const int64_t b = (int64_t)blockIdx.x * kSideBlock + threadIdx.x;
+    if (b >= batch) return;
+    const int32_t n = (int32_t)n_steps, W = (int32_t)window;
+    double x[4] = {q[4 * b], q[4 * b + 1], q[4 * b + 2], q[4 * b + 3]};
+    double4 ring[kDepth64];
+    int32_t pf = (int32_t)(step0 % window);
+#pragma unroll
+    for (int k = 0; k < kDepth64; ++k) {
+        ring[k] = gd[(int64_t)pf * batch + b];
+        pf = next_row(pf, W);
+    }
+    auto one = [&](int k, int32_t t) {
+        const double4 r = ring[k];
+        ring[k] = gd[(int64_t)pf * batch + b];
+        pf = next_row(pf, W);
+        const double hw[3] = {0.5 * r.x, 0.5 * r.y, 0.5 * r.z};
+        double z[4];
+        rk4_closed(x, x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3], r.w, hw, z);
+        x[0] = z[0]; x[1] = z[1]; x[2] = z[2]; x[3] = z[3];
+        if (traj) {
+            double2 *o = reinterpret_cast<double2 *>(traj + (int64_t)t * batch * 4) + 2 * b;
+            o[0] = make_double2(x[0], x[1]);
+            o[1] = make_double2(x[2], x[3]);
+        }
+    };
+    const int32_t n_full = n - n % kDepth64;
+    int32_t t0 = 0;
+    for (; t0 < n_full; t0 += kDepth64) {
+#pragma unroll
+        for (int k = 0; k < kDepth64; ++k) one(k, t0 + k);
+    }
+#pragma unroll
+    for (int k = 0; k < kDepth64; ++k) {
+        if (t0 + k >= n) break;  // uniform
+        one(k, t0 + k);
+    }
+    q[4 * b] = x[0]; q[4 * b + 1] = x[1]; q[4 * b + 2] = x[2]; q[4 * b + 3] = x[3];
+}
+
+__global__ __launch_bounds__(kSideBlock) void k_wahba_stream64(int64_t batch, int64_t n_steps, int64_t window,
+                                                               int64_t step0, const double4 *__restrict__ am,
+                                                               const double2 *__restrict__ my,
+                                                               const double *__restrict__ refs, double ka,
+                                                               double km, double *__restrict__ out) {
+    const int64_t b = (int64_t)blockIdx.x * kSideBlock + threadIdx.x;
+    if (b >= batch) return;
+    const int32_t n = (int32_t)n_steps, W = (int32_t)window;
+    Frame Wf;
+    {
+        const double a0[3] = {refs[6 * b + 0], refs[6 * b + 1], refs[6 * b + 2]};
+        const double m0[3] = {refs[6 * b + 3], refs[6 * b + 4], refs[6 * b + 5]};
+        make_frame<true>(a0, m0, Wf);
+    }
+    const double sg = wahba_sign(ka, km);
+    double4 ra[kDepth64];
+    double2 rm[kDepth64];
+    int32_t pf = (int32_t)(step0 % window);
+#pragma unroll
+    for (int k = 0; k < kDepth64; ++k) {
+        ra[k] = am[(int64_t)pf * batch + b];
+        rm[k] = my[(int64_t)pf * batch + b];
+        pf = next_row(pf, W);
+    }
+    auto one = [&](int k, int32_t t) {
+        const double4 a = ra[k];
+        const double2 m = rm[k];
+        ra[k] = am[(int64_t)pf * batch + b];
+        rm[k] = my[(int64_t)pf * batch + b];
+        pf = next_row(pf, W);
+        const double acc[3] = {a.x, a.y, a.z}, mag[3] = {a.w, m.x, m.y};
+        Frame Vf;
+        make_frame<true>(acc, mag, Vf, sg);
+        double R[9], y[4];
+        wahba_rotation<true>(Wf, Vf, ka, km, R);
+        if (frame_degenerate(Vf)) {  // a zero sample or acc parallel to mag: B has rank 1 (pekf_math.hpp)
+            double a0[3], m0[3];
+            frame_pair(Wf, a0, m0);
+            wahba_current_rank1<1>(a0, m0, acc, mag, ka, km, R);
+        }
+        rotm_to_quat_fast(R, y);  // keeps the reference's branch / sign convention
+        double2 *o = reinterpret_cast<double2 *>(out + (int64_t)t * batch * 4) + 2 * b;
+        o[0] = make_double2(y[0], y[1]);
+        o[1] = make_double2(y[2], y[3]);
+    };
+    const int32_t n_full = n - n % kDepth64;
+    int32_t t0 = 0;
+    for (; t0 < n_full; t0 += kDepth64) {
+#pragma unroll
+        for (int k = 0; k < kDepth64; ++k) one(k, t0 + k);
+    }
+#pragma unroll
+    for (int k = 0; k < kDepth64; ++k) {
+        if (t0 + k >= n) break;  // uniform
+        one(k, t0 + k);
+    }
+}
+
 // UtilityFunctions.Quart2RPY: roll = atan2(2(q0q1+q2q3), 1-2(q1^2+q2^2)), pitch = asin(2(q0q2-q3q1)),
 // yaw = atan2(2(q0q3+q1q2), 1-2(q2^2+q3^2)), times 180/pi
 __device__ __forceinline__ void d_rpy(int64_t i, const double *__restrict__ q, double *__restrict__ rpy) {
@@ -198,6 +305,39 @@ int pekf_gyro_chain_ext_dev(int64_t batch, int64_t n_steps, int64_t window, int6
         hipLaunchKernelGGL(k_gyro_chain<false>, grid, block, 0, as_stream(stream), batch, n_steps, window, step0, gd,
                            nullptr, q_gyro, traj);
     return launched("k_gyro_chain");
+}
+
+int pekf_gyro_chain_rec64_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0, const void *plane_gd,
+                              double *q_gyro, double *traj, void *stream) {
+    PEKF_CHECK_ARG(batch >= 0 && n_steps >= 0, "negative size");
+    if (batch == 0 || n_steps == 0) return PEKF_OK;
+    PEKF_CHECK_ARG(window > 0 && step0 >= 0, "window must be > 0 and step0 >= 0");
+    PEKF_CHECK_ARG(batch < ((int64_t)1 << 28), "batch must be < 2^28 filters per launch");
+    PEKF_CHECK_ARG(plane_gd && q_gyro, "null pointer");
+    PEKF_CHECK_ARG((uintptr_t)plane_gd % 32 == 0 && (uintptr_t)traj % 16 == 0, "misaligned plane / traj pointer");
+    PEKF_CHECK_ARG(n_steps < ((int64_t)1 << 31) && window < ((int64_t)1 << 31), "n_steps and window must be < 2^31");
+    const dim3 grid(grid_for(batch, kSideBlock)), block(kSideBlock);
+    hipLaunchKernelGGL(k_gyro_chain64, grid, block, 0, as_stream(stream), batch, n_steps, window, step0,
+                       static_cast<const double4 *>(plane_gd), q_gyro, traj);
+    return launched("k_gyro_chain64");
+}
+
+int pekf_wahba_stream_rec64_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0, const void *plane_am,
+                                const void *plane_my, const double *refs, double k_acc, double k_mag, double *out,
+                                void *stream) {
+    PEKF_CHECK_ARG(batch >= 0 && n_steps >= 0, "negative size");
+    if (batch == 0 || n_steps == 0) return PEKF_OK;
+    PEKF_CHECK_ARG(window > 0 && step0 >= 0, "window must be > 0 and step0 >= 0");
+    PEKF_CHECK_ARG(batch < ((int64_t)1 << 28), "batch must be < 2^28 filters per launch");
+    PEKF_CHECK_ARG(plane_am && plane_my && refs && out, "null pointer");
+    PEKF_CHECK_ARG((uintptr_t)plane_am % 32 == 0 && (uintptr_t)plane_my % 16 == 0 && (uintptr_t)out % 16 == 0,
+                   "misaligned plane / out pointer");
+    PEKF_CHECK_ARG(n_steps < ((int64_t)1 << 31) && window < ((int64_t)1 << 31), "n_steps and window must be < 2^31");
+    const dim3 grid(grid_for(batch, kSideBlock)), block(kSideBlock);
+    hipLaunchKernelGGL(k_wahba_stream64, grid, block, 0, as_stream(stream), batch, n_steps, window, step0,
+                       static_cast<const double4 *>(plane_am), static_cast<const double2 *>(plane_my), refs, k_acc,
+                       k_mag, out);
+    return launched("k_wahba_stream64");
 }
 
 int pekf_gyro_chain_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0,

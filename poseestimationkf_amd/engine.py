@@ -332,6 +332,28 @@ class RecordWindow64:
         win.counts = np.minimum(lens, W).astype(np.int32)
         return win
 
+    def wahba_quaternions(self, n_steps=None, step0=0, k_acc=0.5, k_mag=0.5):
+        """Pure-Wahba attitude of every record with fixed weights (main_file.py:40): (n_steps, batch, 4)."""
+        n_steps = self.window if n_steps is None else int(n_steps)
+        out = DeviceBuffer(32 * n_steps * self.batch)
+        check(lib.pekf_wahba_stream_rec64_dev(self.batch, n_steps, self.window, int(step0), self.am.ptr, self.my.ptr,
+                                              self.refs.ptr, float(k_acc), float(k_mag), out.ptr, None))
+        check(lib.pekf_device_sync())
+        return out.download((n_steps, self.batch, 4), np.float64)
+
+    def gyro_chain(self, q0=None, n_steps=None, step0=0, want_traj=False):
+        """Pure-gyro attitude (RK4 of the gyro records alone, KFS/KalmanFilter.cpp:149) from q0 (default
+        [1,0,0,0]); returns (q_final (batch,4), traj (n_steps,batch,4) or None)."""
+        n_steps = self.window if n_steps is None else int(n_steps)
+        q = np.tile([1.0, 0.0, 0.0, 0.0], (self.batch, 1)) if q0 is None else f64(q0, (self.batch, 4))
+        qb = DeviceBuffer(32 * self.batch).upload(q)
+        tb = DeviceBuffer(32 * n_steps * self.batch) if want_traj else None
+        check(lib.pekf_gyro_chain_rec64_dev(self.batch, n_steps, self.window, int(step0), self.gd.ptr, qb.ptr,
+                                            tb.ptr if tb is not None else None, None))
+        check(lib.pekf_device_sync())
+        return (qb.download((self.batch, 4), np.float64),
+                tb.download((n_steps, self.batch, 4), np.float64) if want_traj else None)
+
 
 # ------------------------------------------------------------------ server front-end (raw events)
 

@@ -134,3 +134,38 @@ def test_rec64_nan_record_poisons_only_its_filter(eng):
     assert np.isnan(out[1][77]).all()
     keep = np.arange(K) != 77
     assert np.array_equal(out[0][keep], out[1][keep]) and np.isfinite(out[0]).all()
+
+
+def test_rec64_side_outputs(eng):
+    """The pure-gyro chain and the per-record 0.5/0.5 Wahba (main_file.py:40) over FP64 records: bit for bit
+    the 40 B-record kernels on f32-representable values, and against the NumPy restatement
+    (RungeKutta4 chained, Wahba.getQuarternion) on float64 records with odd time differences."""
+    K, W = 130, 48
+    rec = synth.generate(np.arange(K), W, seed=43)
+    w32, w64 = eng.IMUWindow.from_records(rec), _rec64_of(eng, rec)
+    for a, b in zip(w32.gyro_chain(n_steps=70, step0=3, want_traj=True),
+                    w64.gyro_chain(n_steps=70, step0=3, want_traj=True)):
+        assert np.array_equal(a, b)
+    assert np.array_equal(w32.wahba_quaternions(n_steps=60, step0=9), w64.wahba_quaternions(n_steps=60, step0=9))
+
+    rng = np.random.default_rng(44)
+    K, W = 40, 50
+    g = rng.normal(scale=0.5, size=(W, K, 3))
+    a = rng.normal(scale=0.3, size=(W, K, 3)) + [0.0, 0.0, 9.8]
+    m = rng.normal(scale=2.0, size=(W, K, 3)) + [20.0, 1.0, -40.0]
+    dt = rng.choice([1.0e7, 2.5e7 + 0.25, 3.2e9, -4.0e6], p=[0.7, 0.2, 0.05, 0.05], size=(W, K))
+    a0 = rng.normal(scale=0.3, size=(K, 3)) + [0.0, 0.0, 9.8]
+    m0 = rng.normal(scale=2.0, size=(K, 3)) + [20.0, 1.0, -40.0]
+    win = eng.RecordWindow64.from_arrays(g, dt, a, m, a0, m0)
+    qf, tr = win.gyro_chain(want_traj=True)
+    wq = win.wahba_quaternions()
+    eg = ew = 0.0
+    for k in range(0, K, 3):
+        q = np.array([1.0, 0, 0, 0])
+        for i in range(W):
+            q = npo.rk4(q, dt[i, k], g[i, k])
+            eg = max(eg, float(np.abs(tr[i, k] - q).max()))
+            ew = max(ew, float(np.abs(wq[i, k] - npo.wahba_quat(a0[k], m0[k], a[i, k], m[i, k], 0.5, 0.5)).max()))
+    print("FP64 records: gyro chain %.3e, 0.5/0.5 Wahba %.3e vs the NumPy restatement" % (eg, ew))
+    assert eg < 1e-12 and ew < 1e-10
+    assert np.array_equal(qf, tr[-1])
