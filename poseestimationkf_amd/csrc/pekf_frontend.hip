@@ -47,6 +47,20 @@ typedef float nv4f __attribute__((ext_vector_type(4)));  // the native vector th
 #define PEKF_FE_GROUP_THR (PEKF_FE_GROUP == 64 ? PEKF_FE_STAGE_THR : PEKF_FE_GROUP)
 #endif
 
+// Pooled queue (PEKF_FE_POOL > 0 slots per group of PEKF_FE_GROUP lanes; 0 = the per-lane rows of
+// PEKF_FE_STAGE above): a group's lanes share one pool of record slots instead of owning STG rows
+// each, so a lane running ahead of its group may queue up to PEKF_FE_POOL_ROWS rows past the group's
+// base while the lanes near the base use few -- the per-lane rows overflow when the LEAD lane is STG
+// rows ahead, the pool only when the group's queued records together fill it.  64 slots x 8 groups +
+// the slot table = 23 KB per wave, 7 waves per CU: WRITE_SIZE 1.58x -> 1.25x the record bytes, -5 %
+// time against the 10 per-lane rows (profiles/r5/frontend_pool/; 56-78 slots, 16 / 32 rows swept).
+#ifndef PEKF_FE_POOL
+#define PEKF_FE_POOL 64
+#endif
+#ifndef PEKF_FE_POOL_ROWS
+#define PEKF_FE_POOL_ROWS 32
+#endif
+
 // The staged form's LDS: each lane's queued records, one row per slot (row % S), lane-minor so a
 // lane's accesses are its own column (no other lane reads them: no barrier).
 template <int S>
@@ -54,6 +68,18 @@ struct FeStage {
     float4 gd[S][64];
     float4 am[S][64];
     float2 my[S][64];
+};
+// The pooled form's LDS (one wave per block, so no barrier: a wave's LDS accesses complete in
+// order): per group, P record slots and the ring of its free slot numbers; per lane, the slot of its
+// record for each row base .. base + ROWS - 1 (row % ROWS).
+template <int P, int NG, int ROWS>
+struct FePool {
+    static_assert(P <= 255, "slot numbers are bytes");
+    float4 gd[NG][P];
+    float4 am[NG][P];
+    float2 my[NG][P];
+    uint8_t ring[NG][P];
+    uint8_t slot[ROWS][64];
 };
 #ifndef PEKF_FE_RING
 #define PEKF_FE_RING 9
@@ -71,7 +97,12 @@ struct FeStage {
 // coalesced row, once at most 64 - THR ready lanes still lack it, and the queue drains after the last
 // event.  The records and their rows are unchanged; only the order of the stores differs.  10 rows:
 // 1.7x the record bytes written, -20 % time (profiles/r4/frontend_stage/).
-template <bool TE, int STG>
+//
+// POOL > 0 (with STG > 0 and PEKF_FE_GROUP < 64): the pooled queue.  A lane's record for a row in
+// [base, base + PEKF_FE_POOL_ROWS) takes a free slot of its group's pool (the group's lanes that
+// queue in one flush take consecutive entries of the free ring, in lane order), or is stored
+// directly when the pool is empty; a written row's slots go back to the ring.
+template <bool TE, int STG, int POOL = 0>
 __global__ __launch_bounds__(STG ? 64 : kFeBlock) void k_frontend(int64_t batch, int64_t n_events,
                                                        const float4 *__restrict__ ev,
                                                        const double *__restrict__ init,
@@ -98,13 +129,29 @@ __global__ __launch_bounds__(STG ? 64 : kFeBlock) void k_frontend(int64_t batch,
     int bad = 0;
     static_assert(STG >= 0 && STG <= 32, "the queue's rows are bits of one 32-bit mask");
     constexpr int kS = STG ? STG : 1;
-    __shared__ FeStage<kS> st;
-    const int col = threadIdx.x & 63;
     constexpr int kG = PEKF_FE_GROUP;
     static_assert(kG == 8 || kG == 16 || kG == 32 || kG == 64, "lane groups of 8, 16, 32 or 64");
+    constexpr int kRows = PEKF_FE_POOL_ROWS;
+    static_assert(POOL == 0 || (STG > 0 && kG < 64 && kRows > 0 && kRows <= 32 && (kRows & (kRows - 1)) == 0),
+                  "the pooled queue: staged, lane groups, a power-of-two row span of at most 32");
+    using Stage = typename std::conditional<(POOL > 0), FePool<(POOL > 0 ? POOL : 1), 64 / kG, kRows>,
+                                            FeStage<kS>>::type;
+    __shared__ Stage st;
+    const int col = threadIdx.x & 63;
     // STG: the oldest row the queue holds -- wave-uniform for kG = 64, else the same in each group of kG lanes
     int32_t base = 0;
-    uint32_t held = 0;  // STG: bit row % STG = this lane's record for that row is queued
+    uint32_t held = 0;  // STG: bit row % STG (POOL: row % kRows) = this lane's record for that row is queued
+    // this lane's group's bits of a wave ballot
+    const int shift = col & ~(kG - 1);
+    constexpr uint64_t kMask = kG == 64 ? ~0ull : (1ull << (kG & 63)) - 1;
+    const int grp = col / kG;                       // POOL: the group's pool
+    const uint64_t below = (1ull << (col & (kG - 1))) - 1;  // the group's lanes before this one
+    int head = 0, nfree = POOL;                     // POOL: the free ring's first entry and length (group-uniform)
+    if constexpr (POOL > 0) {  // the ring holds every slot; a group cut short by the batch's end has fewer lanes
+        const uint64_t act = (__ballot(true) >> shift) & kMask;
+        const int na = __popcll(act);
+        for (int i = __popcll(act & below); i < POOL; i += na) st.ring[grp][i] = (uint8_t)i;
+    }
     // the pending record (Phase3::pend) is emitted every kFlush events; a lane never has two
     constexpr int kFlush = 3;
     auto flush = [&]() {
@@ -154,9 +201,6 @@ __global__ __launch_bounds__(STG ? 64 : kFeBlock) void k_frontend(int64_t batch,
                 ++base;
             }
         } else {
-            // this lane's group's bits of a wave ballot
-            const int shift = col & ~(kG - 1);
-            constexpr uint64_t kMask = kG == 64 ? ~0ull : (1ull << (kG & 63)) - 1;
             for (;;) {
                 const uint64_t anyheld = (__ballot(held != 0) >> shift) & kMask;
                 bool go = anyheld != 0;
@@ -178,6 +222,76 @@ __global__ __launch_bounds__(STG ? 64 : kFeBlock) void k_frontend(int64_t batch,
                 }
             }
         }
+    };
+    // POOL: flush with every lane active (the group's queueing lanes are ranked by a ballot)
+    auto flush_pool = [&]() {
+      if constexpr (POOL > 0) {
+        const bool has = fe.pend;
+        bool esc = false;
+        Rec rc{};
+        if (has) rc = fe.emit(esc);
+        const bool live = has && ready;
+        if (live && esc) bad |= dtx ? 4 : 1;
+        const bool in = live && r < rmax;
+        if (live && !in) bad |= 2;  // more records than the output window holds
+        const bool want = in && r >= base && r < base + kRows;
+        const uint64_t req = (__ballot(want) >> shift) & kMask;
+        const int j = __popcll(req & below), k = __popcll(req);
+        const int64_t o = (int64_t)r * batch + b;
+        if (want && j < nfree) {
+            int i = head + j;
+            if (i >= POOL) i -= POOL;
+            const int s = st.ring[grp][i];
+            st.gd[grp][s] = rc.gd;
+            st.am[grp][s] = rc.am;
+            st.my[grp][s] = rc.my;
+            const uint32_t sl = (uint32_t)r % kRows;
+            st.slot[sl][col] = (uint8_t)s;
+            held |= 1u << sl;
+        } else if (in) {
+            gd[o] = rc.gd;
+            am[o] = rc.am;
+            my[o] = rc.my;
+        }
+        if (in && esc && dtx) dtx[o] = fe.p.dt;
+        const int t = k < nfree ? k : nfree;
+        head += t;
+        if (head >= POOL) head -= POOL;
+        nfree -= t;
+        if (live) ++r;
+      }
+    };
+    // POOL: write out row base while every ready lane of the group has made it (or, all, until no lane
+    // holds any); its slots go back to the free ring
+    auto drain_pool = [&](bool all) {
+      if constexpr (POOL > 0) {
+        for (;;) {
+            bool go = ((__ballot(held != 0) >> shift) & kMask) != 0;
+            if (!all) {
+                const uint64_t behind = (__ballot(ready && r <= base && r < rmax) >> shift) & kMask;
+                go = go && __popcll(behind) <= kG - PEKF_FE_GROUP_THR;
+            }
+            if (!__any(go)) break;
+            const uint32_t sl = (uint32_t)base % kRows;
+            const bool mine = go && (held & (1u << sl));
+            const uint64_t fm = (__ballot(mine) >> shift) & kMask;
+            if (mine) {
+                const int s = st.slot[sl][col];
+                const int64_t o = (int64_t)base * batch + b;
+                gd[o] = st.gd[grp][s];
+                am[o] = st.am[grp][s];
+                my[o] = st.my[grp][s];
+                int i = head + nfree + __popcll(fm & below);
+                if (i >= POOL) i -= POOL;
+                st.ring[grp][i] = (uint8_t)s;
+                held &= ~(1u << sl);
+            }
+            if (go) {
+                nfree += __popcll(fm);
+                ++base;
+            }
+        }
+      }
     };
 
     // Events stream through a register ring of kRing records loaded kRing events ahead (the loop is
@@ -215,13 +329,21 @@ __global__ __launch_bounds__(STG ? 64 : kFeBlock) void k_frontend(int64_t batch,
                 ring[k] = load(e0 + k + kRing);
                 fe.event<TE>(v4);
                 if ((k + 1) % kFlush == 0) {
-                    flush();
-                    if constexpr (STG > 0) drain(false);
+                    if constexpr (POOL > 0) {
+                        flush_pool();
+                        drain_pool(false);
+                    } else {
+                        flush();
+                        if constexpr (STG > 0) drain(false);
+                    }
                 }
             }
         }
     }
-    if constexpr (STG > 0) drain(true);
+    if constexpr (POOL > 0)
+        drain_pool(true);
+    else if constexpr (STG > 0)
+        drain(true);
     counts[b] = r < rmax ? r : rmax;
     if (bad && err) atomicOr(err, bad);
 }
@@ -389,14 +511,15 @@ extern "C" int pekf_frontend_ext_dev(int64_t batch, int64_t n_events, const void
     auto *am = static_cast<float4 *>(plane_am);
     auto *my = static_cast<float2 *>(plane_my);
     constexpr int kStg = PEKF_FE_STAGE;
+    constexpr int kPool = PEKF_FE_POOL;
     constexpr int kBlock = kStg ? 64 : kFeBlock;
     const dim3 grid(grid_for(batch, kBlock)), block(kBlock);
     if (flags & PEKF_EV_TIME_EVENTS)
-        hipLaunchKernelGGL((k_frontend<true, kStg>), grid, block, 0, as_stream(stream), batch, n_events, ev, init,
-                           t_init, alpha, r_max, gd, am, my, dt_ext, counts, refs, dev_error);
+        hipLaunchKernelGGL((k_frontend<true, kStg, kPool>), grid, block, 0, as_stream(stream), batch, n_events, ev,
+                           init, t_init, alpha, r_max, gd, am, my, dt_ext, counts, refs, dev_error);
     else
-        hipLaunchKernelGGL((k_frontend<false, kStg>), grid, block, 0, as_stream(stream), batch, n_events, ev, init,
-                           t_init, alpha, r_max, gd, am, my, dt_ext, counts, refs, dev_error);
+        hipLaunchKernelGGL((k_frontend<false, kStg, kPool>), grid, block, 0, as_stream(stream), batch, n_events, ev,
+                           init, t_init, alpha, r_max, gd, am, my, dt_ext, counts, refs, dev_error);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_frontend");
     return PEKF_OK;
