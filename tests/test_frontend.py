@@ -128,10 +128,12 @@ def _events(K, spec):
 
 @pytest.mark.gpu
 def test_frontend_row_queue_with_drifting_lanes(eng):
-    """k_frontend stages a wave's records in a 10-row LDS queue and writes whole rows; records of
-    lanes too far behind or ahead of the queue are stored directly.  Lanes drifting 0-12 rows apart
-    (acc-only lead-ins), a slow lane (a record per 5 events), a late lane, one with no records, one
-    never ready, and a partial last wave: every record of every filter equals the restatement's."""
+    """k_frontend queues each 8-lane group's records in a shared pool of LDS slots and writes whole
+    rows; records more than 32 rows ahead of the group's base, or met by an empty pool, are stored
+    directly.  Lanes drifting 0-12 rows apart (acc-only lead-ins), a slow lane (a record per 5
+    events), a late lane, one with no records (its group's base never moves, so the pool runs dry),
+    one never ready, and a partial last wave (a group of 5 lanes): every record of every filter
+    equals the restatement's."""
     A, G, M = synth.EV_ACC, synth.EV_GYRO, synth.EV_MAG
     K, E = 64 * 2 + 5, 600
     types = np.empty((E, K), np.uint32)
