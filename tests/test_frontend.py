@@ -178,6 +178,25 @@ def test_frontend_row_queue_with_drifting_lanes(eng):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("K", [1, 2, 3, 5, 7, 8, 9, 15, 17, 70])
+def test_frontend_partial_lane_groups(eng, K):
+    """Batches that end inside an 8-lane group (the pooled queue's unit): the group's ring of free
+    slots is filled by the lanes it has, and every record of every filter equals the restatement's."""
+    E = 240
+    ev = synth.generate_events(np.arange(K), E, seed=100 + K)
+    win, counts = eng.run_frontend(ev)
+    rec = win.download_filters(np.arange(K))
+    for k in range(K):
+        g, dt, a, m = _oracle_records(ev, k)
+        r = len(dt)
+        assert counts[k] == r
+        assert np.array_equal(rec.gyro[:r, k], g.astype(np.float32))
+        assert np.array_equal(rec.dtw[:r, k], dt.astype(np.uint32))
+        assert _f32_ulps(rec.acc[:r, k], a) <= 1
+        assert _f32_ulps(rec.mag[:r, k], m) <= 1
+
+
+@pytest.mark.gpu
 def test_frontend_streams_without_records(eng):
     K = 70
     for spec in ([], [(synth.EV_ACC, 10), (synth.EV_MAG, 10)] * 5,            # nothing, or no gyro at all
