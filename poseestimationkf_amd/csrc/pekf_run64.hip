@@ -11,8 +11,10 @@
 // The arithmetic is k_run's multi-record loop step for step -- reference-frame basis, covariance as
 // N, lazy |X|, omod halvings (ekf_record_step<double, MC, LAZY, OM, PIN>, pekf_step.hpp) -- so a
 // window of f32-representable values gives k_run's state bit for bit (tests/test_rec64.py).  Compiled
-// with the same flags as pekf_run_multi.hip (Makefile RUNMULTIFLAGS).  Loads are plain global loads
-// of the next record, one row ahead: at 80 B per record a log replay at scale is as much HBM as VALU.
+// with the same flags as pekf_run_multi.hip (Makefile RUNMULTIFLAGS), and k_run's loop: rows through
+// scalar-offset buffer descriptors (RowCursor64), the next record in flight one row ahead, unrolled by
+// two so no record is copied between steps.  At 80 B per record a log replay at scale is as much HBM
+// as VALU.
 #include "pekf_step.hpp"
 
 namespace pekf {
@@ -20,6 +22,60 @@ namespace pekf {
 struct Rec64 {
     double4 gd, am;
     double2 my;
+};
+
+// k_run's RowCursor for the 80 B record: rows of batch x 32 B (gd, am) and batch x 16 B (my), read
+// through buffer descriptors of a chunk of rows with the row's offset in the scalar offset, so the
+// next row is two scalar adds and a compare and no vector address arithmetic is kept per record
+// (the lane offsets are 32-bit: batch < 2^27, checked on the host).  A double4 is two 16 B loads
+// (the second at the instruction's immediate offset).
+struct RowCursor64 {
+    const char *g, *a, *m;
+    uint32_t row32, row16;
+    int32_t window, chunk_rows;
+    int32_t row = 0, end = 0;
+    uint32_t s32 = 0, s16 = 0;
+    __amdgpu_buffer_rsrc_t rg, ra, rm;
+
+    __device__ __forceinline__ RowCursor64(const double4 *gd, const double4 *am, const double2 *my, int64_t batch,
+                                           int64_t win)
+        : g(reinterpret_cast<const char *>(gd)), a(reinterpret_cast<const char *>(am)),
+          m(reinterpret_cast<const char *>(my)), row32((uint32_t)batch * 32u), row16((uint32_t)batch * 16u),
+          window((int32_t)win) {
+        const uint32_t c = (1u << 31) / row32;
+        chunk_rows = c ? (int32_t)c : 1;
+    }
+    __device__ __forceinline__ void start(int32_t r) {
+        row = r;
+        end = (window - r < chunk_rows) ? window : r + chunk_rows;
+        const uint64_t n = (uint64_t)(end - r);
+        rg = row_rsrc(g + (uint64_t)r * row32, (int64_t)(n * row32));
+        ra = row_rsrc(a + (uint64_t)r * row32, (int64_t)(n * row32));
+        rm = row_rsrc(m + (uint64_t)r * row16, (int64_t)(n * row16));
+        s32 = 0;
+        s16 = 0;
+    }
+    __device__ __forceinline__ void advance() {
+        if (++row == end) {
+            start(row == window ? 0 : row);
+        } else {
+            s32 += row32;
+            s16 += row16;
+        }
+    }
+    template <int AUX>
+    static __device__ __forceinline__ double4 load4(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t so) {
+        const double2 lo = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, off, so, AUX));
+        const double2 hi = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16u, so, AUX));
+        return make_double4(lo.x, lo.y, hi.x, hi.y);
+    }
+    __device__ __forceinline__ Rec64 load(uint32_t off32, uint32_t off16) const {
+        Rec64 v;
+        v.gd = load4<PEKF_REC_AUX>(rg, off32, s32);
+        v.am = load4<PEKF_REC_AUX>(ra, off32, s32);
+        v.my = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rm, off16, s16, PEKF_REC_AUX));
+        return v;
+    }
 };
 
 template <bool TRAJ, bool COUNTS>
@@ -42,6 +98,13 @@ __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run64(
     double x[4];
     Sym4T<double> P;
     load_state<false>(Xio, Pio, b, batch, x, P);
+
+    const uint32_t lane = (uint32_t)b;
+    const uint32_t off32 = lane * 32u, off16 = lane * 16u;
+    RowCursor64 rows(gd, am, my, batch, window);
+    rows.start((int32_t)(step0 % window));
+    Rec64 ra = rows.load(off32, off16), rb;
+
     using RW = typename std::conditional<TRAJ, RefW, RefWLazy>::type;
     RW Wr;
     Wr.aW = Wf.alpha; Wr.b1W = Wf.beta1; Wr.b2W = Wf.beta2;
@@ -58,34 +121,27 @@ __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run64(
     }
     const StepK<double> kc = step_consts<double, true>(qs, rs);
 
-    auto load = [&](int64_t row) -> Rec64 {
-        const int64_t i = row * batch + b;
-        return {gd[i], am[i], my[i]};
-    };
-    int64_t row = step0 % window;
-    Rec64 cur = load(row);
-    OmodMode mode;
-    mode.enter();
-    for (int32_t t = 0; t < n32; ++t) {
-        const int64_t next = row + 1 == window ? 0 : row + 1;
-        const Rec64 nxt = load(next);  // in flight while this record is applied
+    // One record (main_file.py:42-45) on (x, P) in registers; lazy: X arrives unnormalised (every
+    // record after the launch's first)
+    auto step = [&](const Rec64 &cur, int32_t t, auto lazy) {
         if (!COUNTS || t < my_steps) {
             const double gy[3] = {cur.gd.x, cur.gd.y, cur.gd.z};
             const double acc[3] = {cur.am.x, cur.am.y, cur.am.z};
             const double mag[3] = {cur.am.w, cur.my.x, cur.my.y};
-            const int64_t r = row;
-            auto reload = [&](double *a, double *m) {  // rare: the degenerate-Wahba fallback
-                const double4 va = am[r * batch + b];
-                const double2 vm = my[r * batch + b];
+            auto reload = [&](double *a, double *m) {  // rare: the degenerate-Wahba fallback; the cursor is a row ahead
+                const int32_t r = rows.row == 0 ? rows.window - 1 : rows.row - 1;
+                const double4 va = RowCursor64::load4<0>(row_rsrc(rows.a + (uint64_t)r * rows.row32, rows.row32), off32, 0);
+                const double2 vm = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(
+                    row_rsrc(rows.m + (uint64_t)r * rows.row16, rows.row16), off16, 0, 0));
                 a[0] = va.x; a[1] = va.y; a[2] = va.z;
                 m[0] = va.w; m[1] = vm.x; m[2] = vm.y;
             };
-            if (t == 0)
-                ekf_record_step<double, true, false, true, true>(x, state_norm2(x), P, Wr, kc, gy, cur.gd.w, false, acc,
-                                                                 mag, reload);
-            else
+            if constexpr (decltype(lazy)::value)
                 ekf_record_step<double, true, true, true, true>(x, 1.0, P, Wr, kc, gy, cur.gd.w, false, acc, mag,
                                                                 reload);
+            else
+                ekf_record_step<double, true, false, true, true>(x, state_norm2(x), P, Wr, kc, gy, cur.gd.w, false, acc,
+                                                                 mag, reload);
         }
         if constexpr (TRAJ) {
             double xo[4] = {x[0], x[1], x[2], x[3]};
@@ -100,8 +156,26 @@ __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run64(
             o[0] = make_double2(xo[0], xo[1]);
             o[1] = make_double2(xo[2], xo[3]);
         }
-        cur = nxt;
-        row = next;
+    };
+    using eager = std::false_type;
+    using lazy = std::true_type;
+
+    // k_run's time loop: unrolled by two with ping-pong records, the next row always in flight and no
+    // record copied between steps; the prefetch wraps inside the window, so it is always a valid row
+    rows.advance();
+    rb = rows.load(off32, off16);
+    OmodMode mode;
+    mode.enter();
+    step(ra, 0, eager{});
+    for (int32_t t = 1; t < n32;) {
+        rows.advance();
+        ra = rows.load(off32, off16);
+        step(rb, t, lazy{});
+        if (++t == n32) break;
+        rows.advance();
+        rb = rows.load(off32, off16);
+        step(ra, t, lazy{});
+        ++t;
     }
     mode.leave();
     if (COUNTS && my_steps == 0) return;
@@ -120,7 +194,7 @@ extern "C" int pekf_run_rec64_dev(int64_t batch, int64_t n_steps, int64_t window
     PEKF_CHECK_ARG(batch >= 0 && n_steps >= 0, "negative size");
     if (batch == 0 || n_steps == 0) return PEKF_OK;
     PEKF_CHECK_ARG(window > 0 && step0 >= 0, "window must be > 0 and step0 >= 0");
-    PEKF_CHECK_ARG(batch < ((int64_t)1 << 28), "batch must be < 2^28 filters per launch");
+    PEKF_CHECK_ARG(batch < ((int64_t)1 << 27), "batch must be < 2^27 filters per launch (32-bit lane offsets of 32 B)");
     PEKF_CHECK_ARG(n_steps < ((int64_t)1 << 31), "n_steps must be < 2^31 records per launch");
     PEKF_CHECK_ARG(plane_gd && plane_am && plane_my && refs && X && P, "null pointer");
     PEKF_CHECK_ARG(((uintptr_t)plane_gd % 32 == 0) && ((uintptr_t)plane_am % 32 == 0) &&
