@@ -186,7 +186,8 @@ int pekf_run_ext_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t ste
  *   plane_my : double2 [window][batch] {mag y, z}
  * Every record is a full record (no missing-magnetometer flag).  refs, X, P, q, r, traj, counts as
  * pekf_run_dev (AoS FP64 state); always the multi-record arithmetic, so a window of f32-representable
- * values gives pekf_run_dev's state (n_steps >= 2) bit for bit. */
+ * values gives pekf_run_dev's state (n_steps >= 2) bit for bit.  batch < 2^27 (32-bit lane offsets of
+ * the 32 B planes); planes 32 B aligned (my: 16 B). */
 int pekf_run_rec64_dev(int64_t batch, int64_t n_steps, int64_t window, int64_t step0, const void *plane_gd,
                        const void *plane_am, const void *plane_my, const double *refs, double *X, double *P,
                        double q, double r, double *traj, const int32_t *counts, void *stream);
