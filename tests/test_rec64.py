@@ -169,3 +169,26 @@ def test_rec64_side_outputs(eng):
     print("FP64 records: gyro chain %.3e, 0.5/0.5 Wahba %.3e vs the NumPy restatement" % (eg, ew))
     assert eg < 1e-12 and ew < 1e-10
     assert np.array_equal(qf, tr[-1])
+
+
+def test_rec64_fallback_branch_bit_identical(eng):
+    """The rare fallback branch, which re-reads the record from memory (k_run64's reload, one row behind
+    the cursor, wrapping at the window's start): degenerate samples (zero acc / mag, a parallel pair)
+    and filters started at random attitudes (measurements far from the prediction), over a window
+    replayed twice from a mid-window start -- bit for bit the 40 B-record launch on the same values."""
+    from .test_degenerate_samples import _degenerate_stream
+    rec, _ = _degenerate_stream(K=8, W=120, seed=9)
+    K, W = 8, 120
+    rng = np.random.default_rng(3)
+    X0 = rng.normal(size=(K, 4))
+    X0 /= np.linalg.norm(X0, axis=1, keepdims=True)
+    P0 = np.broadcast_to(np.identity(4), (K, 4, 4)).copy()
+    out = []
+    for win in (eng.IMUWindow.from_records(rec), _rec64_of(eng, rec)):
+        f = eng.BatchedEKF(K)
+        f.set_state(X0, P0)
+        tr = f.run(win, n_steps=2 * W + 7, step0=W - 3, want_traj=True)
+        out.append(f.get_state() + (tr,))
+    for a, b in zip(*out):
+        assert np.array_equal(a, b, equal_nan=True)
+    assert np.isfinite(out[1][2]).all()
