@@ -400,7 +400,14 @@ int pekf_comm_abort(pekf_comm *c);
  * stream reaches it -- the work queued before it has finished -- so compute ahead of a collective, however
  * long, is never charged to it.  On expiry or error c is aborted (it must then only be destroyed) and
  * PEKF_ERR_TIMEOUT / PEKF_ERR_COMM returned: a peer that died turns into an error here instead of a host
- * thread stuck in hipStreamSynchronize. */
+ * thread stuck in hipStreamSynchronize.
+ * The clock starts when THIS rank's inputs are ready, so it also runs while slower peers finish the compute
+ * queued ahead of the collective on their side: the deadline must exceed the ranks' skew at the
+ * collective (bench.py's final gather follows the whole timed run; size PEKF_COMM_TIMEOUT_S to the run).
+ * Every collective is tracked: at most 1,024 incomplete ones per communicator, one more is refused with
+ * PEKF_ERR_COMM and not enqueued.  If a collective could not be tracked after it was enqueued (its
+ * completion event could not be recorded), the drain of that stream is bounded by timeout_s from the
+ * wait call instead, compute included. */
 int pekf_comm_wait(pekf_comm *c, void *stream, double timeout_s);
 int pekf_comm_rank(const pekf_comm *c, int *rank, int *nranks, int *device); /* outputs may be NULL */
 /* recv[nranks * count] on the root (rows in rank order) <- every rank's send[count]; device

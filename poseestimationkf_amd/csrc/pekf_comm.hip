@@ -184,6 +184,10 @@ struct pekf_comm {
     };
     std::deque<Pending> pending{};
     std::vector<hipEvent_t> spare{};  // events of retired entries, for reuse (on `device`)
+    // Streams holding a collective that was enqueued but could not be tracked (its completion event
+    // could not be recorded): pekf_comm_wait bounds a drain of such a stream by a wall-clock deadline
+    // from the wait call instead, until the stream has drained once.
+    std::vector<hipStream_t> lost{};
 };
 
 namespace pekf {
@@ -201,7 +205,10 @@ struct DeviceScope {
     }
 };
 
-constexpr size_t kMaxPending = 1024;  // beyond this the oldest collective goes untracked (never waited on)
+// Collectives a communicator tracks at once.  One more is refused (PEKF_ERR_COMM) rather than enqueued
+// untracked: an untracked collective that a peer never joins would stall the stream with no deadline
+// running (the next tracked one's inputs would never be ready).
+constexpr size_t kMaxPending = 1024;
 
 void release(pekf_comm *c, const pekf_comm::Pending &p) {
     c->spare.push_back(p.pre);
@@ -233,24 +240,40 @@ hipEvent_t mark(pekf_comm *c, hipStream_t s) {
     return ev;
 }
 
+bool is_lost(const pekf_comm *c, hipStream_t s) {
+    for (hipStream_t x : c->lost)
+        if (x == s) return true;
+    return false;
+}
+
+// Tracks a collective just enqueued on s between pre (recorded before it) and post.  Without post the
+// collective cannot be tracked: s is marked lost (pekf_comm_wait then bounds its drain by wall clock).
+// The caller has checked room() before enqueueing, so nothing is ever evicted.
 void track(pekf_comm *c, hipStream_t s, hipEvent_t pre, hipEvent_t post, const char *what) {
-    if (!pre || !post) {
+    if (!post || c->pending.size() >= kMaxPending) {
         if (pre) c->spare.push_back(pre);
         if (post) c->spare.push_back(post);
+        if (!is_lost(c, s)) c->lost.push_back(s);
         return;
     }
-    retire(c);
-    if (c->pending.size() >= kMaxPending) {
-        release(c, c->pending.front());
-        c->pending.pop_front();
-    }
     c->pending.push_back({pre, post, s, what, 0.0});
+}
+
+// Room to track one more collective on c (after dropping the completed ones), else PEKF_ERR_COMM.
+int room(pekf_comm *c) {
+    retire(c);
+    if (c->pending.size() < kMaxPending) return PEKF_OK;
+    return set_error(PEKF_ERR_COMM,
+                     "rank %d of %d: %zu collectives already in flight on this communicator (the most it tracks "
+                     "for pekf_comm_wait's deadline); wait for them before enqueueing more",
+                     c->rank, c->nranks, c->pending.size());
 }
 
 void drop_events(pekf_comm *c) {
     DeviceScope on(c->device);
     for (const auto &p : c->pending) release(c, p);
     c->pending.clear();
+    c->lost.clear();
     for (hipEvent_t e : c->spare) (void)hipEventDestroy(e);
     c->spare.clear();
 }
@@ -279,7 +302,9 @@ int enqueued(pekf_comm *c, ncclResult_t e, const char *what) {
 // Enqueues one collective of c on s between the two tracking events.
 template <class Enqueue>
 int tracked(pekf_comm *c, hipStream_t s, const char *what, Enqueue enqueue) {
+    if (int st = room(c)) return st;
     hipEvent_t pre = mark(c, s);
+    if (!pre) return set_error(PEKF_ERR_HIP, "%s: cannot record the event that times it; not enqueued", what);
     const int st = enqueued(c, enqueue(), what);
     if (st != PEKF_OK || !c->nc) {
         if (pre) c->spare.push_back(pre);
@@ -472,10 +497,16 @@ int pekf_comm_wait(pekf_comm *c, void *stream, double timeout_s) {
     PEKF_CHECK_ARG(c, "null communicator");
     PEKF_CHECK_ARG(c->nc, "communicator was aborted");
     const hipStream_t s = as_stream(stream);
+    const double called_at = now_s();
     for (;;) {
         const hipError_t q = hipStreamQuery(s);
         if (q == hipSuccess) {
             retire(c);
+            for (auto it = c->lost.begin(); it != c->lost.end(); ++it)
+                if (*it == s) {
+                    c->lost.erase(it);
+                    break;
+                }
             return PEKF_OK;
         }
         if (q != hipErrorNotReady) return hip_fail(q, "hipStreamQuery");
@@ -497,6 +528,15 @@ int pekf_comm_wait(pekf_comm *c, void *stream, double timeout_s) {
                 head = &*it;
                 break;
             }
+        }
+        // a collective on s went untracked: no per-collective clock can be trusted, so the whole drain
+        // gets the deadline from this call (compute queued on s is then charged too)
+        if (timeout_s > 0 && is_lost(c, s) && now_s() - called_at > timeout_s) {
+            abort_comm(c);
+            return set_error(PEKF_ERR_TIMEOUT,
+                             "rank %d of %d: a stream holding an untracked collective did not drain within %.0f s "
+                             "of the wait (a peer rank gone?); communicator aborted",
+                             c->rank, c->nranks, timeout_s);
         }
         if (head && timeout_s > 0 && hipEventQuery(head->pre) == hipSuccess) {
             const double t = now_s();
@@ -539,12 +579,20 @@ int pekf_gather_multi_dev(int ndev, pekf_comm *const *comms, const double *const
     PEKF_CHECK_ARG(count >= 0, "negative size");
     PEKF_CHECK_ARG(root >= 0 && root < ndev && recv, "root out of range or no receive buffer");
     for (int i = 0; i < ndev; ++i) PEKF_CHECK_ARG(comms[i] && comms[i]->nc, "null or aborted communicator");
+    for (int i = 0; i < ndev; ++i)
+        if (int st = room(comms[i])) return st;
     std::vector<hipEvent_t> pre(ndev);
     for (int i = 0; i < ndev; ++i) pre[i] = mark(comms[i], as_stream(streams[i]));
     const auto untrack = [&] {
         for (int i = 0; i < ndev; ++i)
             if (pre[i]) comms[i]->spare.push_back(pre[i]);
     };
+    for (int i = 0; i < ndev; ++i)
+        if (!pre[i]) {
+            untrack();
+            return set_error(PEKF_ERR_HIP, "ncclGather (grouped): cannot record the event that times it on device "
+                             "%d; not enqueued", comms[i]->device);
+        }
     ncclResult_t e = rccl().group_start();
     if (e != ncclSuccess) {
         untrack();

@@ -15,9 +15,6 @@ namespace pekf {
 
 constexpr int kFeBlock = 256;
 typedef float nv4f __attribute__((ext_vector_type(4)));  // the native vector the nontemporal builtins take
-// k_frontend's per-wave LDS record queue (profiles/r4/frontend_stage/: 8-16 rows x thresholds 52-60
-// swept; 10 rows = 25.6 KB per wave, 6 waves per CU): rows held (0: every record stored where it is
-// made), and the queue's oldest row is written once at most 64 - THR ready lanes still lack it.
 // Non-temporal event loads (every event is read once per pass): k_frontend -1.7 %, phase 2's means
 // -5 % (profiles/r4/ntload/).
 #ifndef PEKF_FE_NTL
@@ -26,50 +23,20 @@ typedef float nv4f __attribute__((ext_vector_type(4)));  // the native vector th
 #ifndef PEKF_INIT_NTL
 #define PEKF_INIT_NTL 1
 #endif
-// Queue depth: 10 rows = 25.6 KB of LDS per 64-lane block, tuned on gfx950's 160 KB of LDS per CU
-// (~6 blocks per CU); the library is built for gfx950 only (Makefile ARCH).  A 64 KB-LDS part would cap
-// this at 2 blocks per CU: re-measure the depth (or 0, the unstaged form) before building for one.
-#ifndef PEKF_FE_STAGE
-#define PEKF_FE_STAGE 10
-#endif
-#ifndef PEKF_FE_STAGE_THR
-#define PEKF_FE_STAGE_THR 56
-#endif
-// Lanes that share the queue's base row: 64 = the whole wave (round 4); 8 = each group of 8 lanes keeps
-// its own base (a row of 8 lanes is one 128 B line of the gd / am planes), writes its row once all its
-// ready lanes hold it (GROUP_THR), and drifts apart from the other groups: WRITE_SIZE 1.72x -> 1.59x
-// the record bytes, -0.8 % time at the same LDS (profiles/r5/frontend_group/; deeper queues reach 1.27x
-// but lose a third of the waves per CU and 20 % of the time).
-#ifndef PEKF_FE_GROUP
-#define PEKF_FE_GROUP 8
-#endif
-#ifndef PEKF_FE_GROUP_THR
-#define PEKF_FE_GROUP_THR (PEKF_FE_GROUP == 64 ? PEKF_FE_STAGE_THR : PEKF_FE_GROUP)
-#endif
 
-// Pooled queue (PEKF_FE_POOL > 0 slots per group of PEKF_FE_GROUP lanes; 0 = the per-lane rows of
-// PEKF_FE_STAGE above): a group's lanes share one pool of record slots instead of owning STG rows
-// each, so a lane running ahead of its group may queue up to PEKF_FE_POOL_ROWS rows past the group's
-// base while the lanes near the base use few -- the per-lane rows overflow when the LEAD lane is STG
-// rows ahead, the pool only when the group's queued records together fill it.  64 slots x 8 groups +
-// the slot table = 23 KB per wave, 7 waves per CU: WRITE_SIZE 1.58x -> 1.25x the record bytes, -5 %
-// time against the 10 per-lane rows (profiles/r5/frontend_pool/; 56-78 slots, 16 / 32 rows swept).
-#ifndef PEKF_FE_POOL
-#define PEKF_FE_POOL 64
-#endif
-#ifndef PEKF_FE_POOL_ROWS
-#define PEKF_FE_POOL_ROWS 32
-#endif
+// k_frontend's record queue: per group of kFeGroup lanes (one 128 B line of a gd / am row), a pool of
+// kFePool LDS record slots and the ring of its free slot numbers.  A lane's record for a row in [base,
+// base + kFeRows) of its group takes a free slot; the group writes row `base` as whole lines once every
+// ready lane of the group has made it (round 5, profiles/r5/frontend_pool/: WRITE_SIZE 1.25x the record
+// bytes, against 1.59x for 10 rows per lane and 2.6x storing each record where it is made; 56-78 slots
+// and 16 / 32 rows swept).  64 slots x 8 groups + the tables = 23 KB per wave, 7 waves per CU, sized
+// for gfx950's 160 KB of LDS (the library is built for gfx950 only).  The per-lane-row and wave-wide
+// forms it replaced are in git history (round 5) and measured in profiles/r4/frontend_stage/.
+constexpr int kFeGroup = 8;
+constexpr int kFePool = 64;
+constexpr int kFeRows = 32;
 
-// The staged form's LDS: each lane's queued records, one row per slot (row % S), lane-minor so a
-// lane's accesses are its own column (no other lane reads them: no barrier).
-template <int S>
-struct FeStage {
-    float4 gd[S][64];
-    float4 am[S][64];
-    float2 my[S][64];
-};
-// The pooled form's LDS (one wave per block, so no barrier: a wave's LDS accesses complete in
+// The pooled queue's LDS (one wave per block, so no barrier: a wave's LDS accesses complete in
 // order): per group, P record slots and the ring of its free slot numbers; per lane, the slot of its
 // record for each row base .. base + ROWS - 1 (row % ROWS).
 template <int P, int NG, int ROWS>
@@ -88,32 +55,22 @@ struct FePool {
 // TE: the event planes may hold time events (Phase3::event).  dtx (may be null): the window's dt side
 // plane [r_max][batch]; an escaped record's float64 dt goes there (err bit 4), else err bit 1.
 //
-// STG > 0 (one wave per block): lanes' record rows drift apart (a wave's lanes span ~20 rows, p90 7.5
-// from its median, scripts/record_drift.py), so a record stored where it is made writes 16 / 16 / 8 B
-// into its own row, and about one 32 B sector per store leaves L2: 2.6x the record bytes, half the
-// kernel's time (profiles/r4/frontend_occ/).  Here the wave keeps rows [base, base + STG) in LDS: a
-// lane's record for a row in that range is queued, any other (a lane that has fallen behind base, or
-// is STG rows ahead of it) is stored directly; row base is written by every lane holding it, as one
-// coalesced row, once at most 64 - THR ready lanes still lack it, and the queue drains after the last
-// event.  The records and their rows are unchanged; only the order of the stores differs.  10 rows:
-// 1.7x the record bytes written, -20 % time (profiles/r4/frontend_stage/).
-//
-// POOL > 0 (with STG > 0 and PEKF_FE_GROUP < 64): the pooled queue.  A lane's record for a row in
-// [base, base + PEKF_FE_POOL_ROWS) takes a free slot of its group's pool (the group's lanes that
-// queue in one flush take consecutive entries of the free ring, in lane order), or is stored
-// directly when the pool is empty; a written row's slots go back to the ring.
-template <bool TE, int STG, int POOL = 0>
-__global__ __launch_bounds__(STG ? 64 : kFeBlock) void k_frontend(int64_t batch, int64_t n_events,
-                                                       const float4 *__restrict__ ev,
-                                                       const double *__restrict__ init,
-                                                       const int64_t *__restrict__ t_init, double alpha,
-                                                       int64_t r_max, float4 *__restrict__ gd,
-                                                       float4 *__restrict__ am, float2 *__restrict__ my,
-                                                       double *__restrict__ dtx,
-                                                       int32_t *__restrict__ counts, double *__restrict__ refs,
-                                                       int *__restrict__ err) {
-    constexpr int kBlock = STG ? 64 : kFeBlock;
-    const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+// One wave per block.  Lanes' record rows drift apart (a wave's lanes span ~20 rows, p90 7.5 from its
+// median, scripts/record_drift.py), so a record stored where it is made writes 16 / 16 / 8 B into its
+// own row, and about one 32 B sector per store leaves L2 (profiles/r4/frontend_occ/).  Here each group
+// keeps its records for rows [base, base + kFeRows) in its pool (the group's lanes that queue in one
+// flush take consecutive entries of the free ring, in lane order); a record outside that range, or met
+// by an empty pool, is stored directly.  Row base is written by every lane of the group holding it once
+// all of the group's ready lanes have made it; its slots go back to the ring; the queue drains after
+// the last event.  The records and their rows are unchanged; only the order of the stores differs.
+template <bool TE>
+__global__ __launch_bounds__(64) void k_frontend(int64_t batch, int64_t n_events, const float4 *__restrict__ ev,
+                                                 const double *__restrict__ init, const int64_t *__restrict__ t_init,
+                                                 double alpha, int64_t r_max, float4 *__restrict__ gd,
+                                                 float4 *__restrict__ am, float2 *__restrict__ my,
+                                                 double *__restrict__ dtx, int32_t *__restrict__ counts,
+                                                 double *__restrict__ refs, int *__restrict__ err) {
+    const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;
     if (b >= batch) return;
     Phase3 fe;
     fe.start(init + 6 * b, t_init[b], alpha);
@@ -127,105 +84,28 @@ __global__ __launch_bounds__(STG ? 64 : kFeBlock) void k_frontend(int64_t batch,
     int32_t r = 0;  // this filter's records so far (r_max < 2^31, checked on the host)
     const int32_t rmax = (int32_t)r_max;
     int bad = 0;
-    static_assert(STG >= 0 && STG <= 32, "the queue's rows are bits of one 32-bit mask");
-    constexpr int kS = STG ? STG : 1;
-    constexpr int kG = PEKF_FE_GROUP;
-    static_assert(kG == 8 || kG == 16 || kG == 32 || kG == 64, "lane groups of 8, 16, 32 or 64");
-    constexpr int kRows = PEKF_FE_POOL_ROWS;
-    static_assert(POOL == 0 || (STG > 0 && kG < 64 && kRows > 0 && kRows <= 32 && (kRows & (kRows - 1)) == 0),
-                  "the pooled queue: staged, lane groups, a power-of-two row span of at most 32");
-    using Stage = typename std::conditional<(POOL > 0), FePool<(POOL > 0 ? POOL : 1), 64 / kG, kRows>,
-                                            FeStage<kS>>::type;
-    __shared__ Stage st;
+    constexpr int POOL = kFePool, kG = kFeGroup, kRows = kFeRows;
+    static_assert(kRows > 0 && kRows <= 32 && (kRows & (kRows - 1)) == 0, "a power-of-two row span of at most 32");
+    __shared__ FePool<POOL, 64 / kG, kRows> st;
     const int col = threadIdx.x & 63;
-    // STG: the oldest row the queue holds -- wave-uniform for kG = 64, else the same in each group of kG lanes
+    // the oldest row the group's queue holds (the same in each group of kG lanes)
     int32_t base = 0;
-    uint32_t held = 0;  // STG: bit row % STG (POOL: row % kRows) = this lane's record for that row is queued
+    uint32_t held = 0;  // bit row % kRows = this lane's record for that row is queued
     // this lane's group's bits of a wave ballot
     const int shift = col & ~(kG - 1);
-    constexpr uint64_t kMask = kG == 64 ? ~0ull : (1ull << (kG & 63)) - 1;
-    const int grp = col / kG;                       // POOL: the group's pool
+    constexpr uint64_t kMask = (1ull << kG) - 1;
+    const int grp = col / kG;                       // the group's pool
     const uint64_t below = (1ull << (col & (kG - 1))) - 1;  // the group's lanes before this one
-    int head = 0, nfree = POOL;                     // POOL: the free ring's first entry and length (group-uniform)
-    if constexpr (POOL > 0) {  // the ring holds every slot; a group cut short by the batch's end has fewer lanes
+    int head = 0, nfree = POOL;                     // the free ring's first entry and length (group-uniform)
+    {  // the ring holds every slot; a group cut short by the batch's end has fewer lanes
         const uint64_t act = (__ballot(true) >> shift) & kMask;
         const int na = __popcll(act);
         for (int i = __popcll(act & below); i < POOL; i += na) st.ring[grp][i] = (uint8_t)i;
     }
     // the pending record (Phase3::pend) is emitted every kFlush events; a lane never has two
     constexpr int kFlush = 3;
-    auto flush = [&]() {
-        if (!fe.pend) return;
-        bool esc;
-        const Rec rc = fe.emit(esc);
-        if (!ready) return;
-        if (esc) bad |= dtx ? 4 : 1;
-        if (r < rmax) {
-            const int64_t o = (int64_t)r * batch + b;
-            if (STG && r >= base && r < base + kS) {
-                const int sl = r % kS;
-                st.gd[sl][col] = rc.gd;
-                st.am[sl][col] = rc.am;
-                st.my[sl][col] = rc.my;
-                held |= 1u << sl;
-            } else {
-                gd[o] = rc.gd;
-                am[o] = rc.am;
-                my[o] = rc.my;
-            }
-            if (esc && dtx) dtx[o] = fe.p.dt;
-        } else {
-            bad |= 2;  // more records than the output window holds
-        }
-        ++r;
-    };
-    // STG: write out queued rows -- while few enough ready lanes still lack row base, or (all) until
-    // no lane holds any
-    auto drain = [&](bool all) {
-        if constexpr (kG == 64) {
-            for (;;) {
-                if (all) {
-                    if (!__any(held != 0)) break;
-                } else {
-                    const int behind = __popcll(__ballot(ready && r <= base && r < rmax));
-                    if (behind > 64 - PEKF_FE_STAGE_THR || !__any(held != 0)) break;
-                }
-                const int sl = base % kS;
-                if (held & (1u << sl)) {
-                    const int64_t o = (int64_t)base * batch + b;
-                    gd[o] = st.gd[sl][col];
-                    am[o] = st.am[sl][col];
-                    my[o] = st.my[sl][col];
-                    held &= ~(1u << sl);
-                }
-                ++base;
-            }
-        } else {
-            for (;;) {
-                const uint64_t anyheld = (__ballot(held != 0) >> shift) & kMask;
-                bool go = anyheld != 0;
-                if (!all) {
-                    const uint64_t behind = (__ballot(ready && r <= base && r < rmax) >> shift) & kMask;
-                    go = go && __popcll(behind) <= kG - PEKF_FE_GROUP_THR;
-                }
-                if (!__any(go)) break;
-                if (go) {
-                    const int sl = base % kS;
-                    if (held & (1u << sl)) {
-                        const int64_t o = (int64_t)base * batch + b;
-                        gd[o] = st.gd[sl][col];
-                        am[o] = st.am[sl][col];
-                        my[o] = st.my[sl][col];
-                        held &= ~(1u << sl);
-                    }
-                    ++base;
-                }
-            }
-        }
-    };
-    // POOL: flush with every lane active (the group's queueing lanes are ranked by a ballot)
+    // flush with every lane active (the group's queueing lanes are ranked by a ballot)
     auto flush_pool = [&]() {
-      if constexpr (POOL > 0) {
         const bool has = fe.pend;
         bool esc = false;
         Rec rc{};
@@ -259,17 +139,15 @@ __global__ __launch_bounds__(STG ? 64 : kFeBlock) void k_frontend(int64_t batch,
         if (head >= POOL) head -= POOL;
         nfree -= t;
         if (live) ++r;
-      }
     };
-    // POOL: write out row base while every ready lane of the group has made it (or, all, until no lane
-    // holds any); its slots go back to the free ring
+    // write out row base while every ready lane of the group has made it (or, all, until no lane holds
+    // any); its slots go back to the free ring
     auto drain_pool = [&](bool all) {
-      if constexpr (POOL > 0) {
         for (;;) {
             bool go = ((__ballot(held != 0) >> shift) & kMask) != 0;
             if (!all) {
                 const uint64_t behind = (__ballot(ready && r <= base && r < rmax) >> shift) & kMask;
-                go = go && __popcll(behind) <= kG - PEKF_FE_GROUP_THR;
+                go = go && behind == 0;
             }
             if (!__any(go)) break;
             const uint32_t sl = (uint32_t)base % kRows;
@@ -291,7 +169,6 @@ __global__ __launch_bounds__(STG ? 64 : kFeBlock) void k_frontend(int64_t batch,
                 ++base;
             }
         }
-      }
     };
 
     // Events stream through a register ring of kRing records loaded kRing events ahead (the loop is
@@ -329,21 +206,13 @@ __global__ __launch_bounds__(STG ? 64 : kFeBlock) void k_frontend(int64_t batch,
                 ring[k] = load(e0 + k + kRing);
                 fe.event<TE>(v4);
                 if ((k + 1) % kFlush == 0) {
-                    if constexpr (POOL > 0) {
-                        flush_pool();
-                        drain_pool(false);
-                    } else {
-                        flush();
-                        if constexpr (STG > 0) drain(false);
-                    }
+                    flush_pool();
+                    drain_pool(false);
                 }
             }
         }
     }
-    if constexpr (POOL > 0)
-        drain_pool(true);
-    else if constexpr (STG > 0)
-        drain(true);
+    drain_pool(true);
     counts[b] = r < rmax ? r : rmax;
     if (bad && err) atomicOr(err, bad);
 }
@@ -510,16 +379,13 @@ extern "C" int pekf_frontend_ext_dev(int64_t batch, int64_t n_events, const void
     auto *gd = static_cast<float4 *>(plane_gd);
     auto *am = static_cast<float4 *>(plane_am);
     auto *my = static_cast<float2 *>(plane_my);
-    constexpr int kStg = PEKF_FE_STAGE;
-    constexpr int kPool = PEKF_FE_POOL;
-    constexpr int kBlock = kStg ? 64 : kFeBlock;
-    const dim3 grid(grid_for(batch, kBlock)), block(kBlock);
+    const dim3 grid(grid_for(batch, 64)), block(64);
     if (flags & PEKF_EV_TIME_EVENTS)
-        hipLaunchKernelGGL((k_frontend<true, kStg, kPool>), grid, block, 0, as_stream(stream), batch, n_events, ev,
-                           init, t_init, alpha, r_max, gd, am, my, dt_ext, counts, refs, dev_error);
+        hipLaunchKernelGGL(k_frontend<true>, grid, block, 0, as_stream(stream), batch, n_events, ev, init, t_init,
+                           alpha, r_max, gd, am, my, dt_ext, counts, refs, dev_error);
     else
-        hipLaunchKernelGGL((k_frontend<false, kStg, kPool>), grid, block, 0, as_stream(stream), batch, n_events, ev,
-                           init, t_init, alpha, r_max, gd, am, my, dt_ext, counts, refs, dev_error);
+        hipLaunchKernelGGL(k_frontend<false>, grid, block, 0, as_stream(stream), batch, n_events, ev, init, t_init,
+                           alpha, r_max, gd, am, my, dt_ext, counts, refs, dev_error);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_frontend");
     return PEKF_OK;

@@ -52,46 +52,6 @@ namespace pekf {
 #ifndef PEKF_LIVE_ATTR
 #define PEKF_LIVE_ATTR __attribute__((amdgpu_waves_per_eu(2)))
 #endif
-#ifndef PEKF_LIVE_PIN
-#define PEKF_LIVE_PIN 0  // the filter step's Schur inverse pinned into the Wahba chain's block (pekf_step.hpp)
-#endif
-#ifndef PEKF_LIVE_PEND_LDS
-#define PEKF_LIVE_PEND_LDS 0  // 1: the captured record waits for its emit in LDS, not in registers
-#endif
-
-// A lane's captured record (Phase3's RawRec) between its capture and the next emit, held in LDS planes
-// [field][lane] instead of 27 registers.  The capture then costs the wave a few LDS stores of values
-// already in registers (plus the five time differences) instead of ~22 masked register copies, and it
-// runs on nearly every event, since some lane of 64 completes a record on almost every event.
-struct PendLds {
-    float (*f)[kRunBlock];   // 15 planes: gyro, acc0, acc1, mag0, mag1 (x, y, z each)
-    double (*d)[kRunBlock];  // 5 planes: dt, an, ad, mn, md
-    uint32_t *flags;         // bit 0: acc0 is the phase-2 mean, bit 1: mag0 is
-    __device__ __forceinline__ void put(const RawRec &r) const {
-        const int l = threadIdx.x;
-        const F3 *v[5] = {&r.gyro, &r.acc0, &r.acc1, &r.mag0, &r.mag1};
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            f[3 * k][l] = v[k]->x;
-            f[3 * k + 1][l] = v[k]->y;
-            f[3 * k + 2][l] = v[k]->z;
-        }
-        d[0][l] = r.dt; d[1][l] = r.an; d[2][l] = r.ad; d[3][l] = r.mn; d[4][l] = r.md;
-        flags[l] = (r.acc0_mean ? 1u : 0u) | (r.mag0_mean ? 2u : 0u);
-    }
-    __device__ __forceinline__ RawRec get() const {
-        const int l = threadIdx.x;
-        RawRec r;
-        F3 *v[5] = {&r.gyro, &r.acc0, &r.acc1, &r.mag0, &r.mag1};
-#pragma unroll
-        for (int k = 0; k < 5; ++k) *v[k] = {f[3 * k][l], f[3 * k + 1][l], f[3 * k + 2][l]};
-        r.dt = d[0][l]; r.an = d[1][l]; r.ad = d[2][l]; r.mn = d[3][l]; r.md = d[4][l];
-        const uint32_t fl = flags[l];
-        r.acc0_mean = (fl & 1u) != 0;
-        r.mag0_mean = (fl & 2u) != 0;
-        return r;
-    }
-};
 
 // A lane's records waiting for the wave's next filter step, oldest first: a ring of Q slots per lane in
 // LDS, [slot][lane] so that a wave's accesses fall in distinct banks whatever slot each lane is at.  A
@@ -224,6 +184,9 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
     constexpr int kPush = kRing / kFlush;  // records a lane can complete within one block
     static_assert(kRing % kFlush == 0, "the ring depth must be a multiple of the emit period");
     static_assert(kQueue >= kPush, "the queue must hold a block's records");
+    // LdsQueue64 keeps ONE escaped dt per lane (esc_dt) and want_step drains it before the next block,
+    // which is safe only while a block completes at most one record per lane
+    static_assert(!R64 || kPush == 1, "LdsQueue64's single escaped-dt register needs one record per lane per block");
     const int64_t b = (int64_t)blockIdx.x * kRunBlock + threadIdx.x;
     if (b >= batch) return;
 
@@ -271,12 +234,11 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
         if (has) {
             double gy[3], acc[3], mag[3];
             Queue::unpack(cur, gy, acc, mag);
-            constexpr bool kPin = PEKF_LIVE_PIN != 0;
             if (applied == 0)
-                ekf_record_step<double, true, false, true, kPin>(x, state_norm2(x), P, Wr, kc, gy, dt, false, acc, mag,
-                                                                 reload);
+                ekf_record_step<double, true, false, true>(x, state_norm2(x), P, Wr, kc, gy, dt, false, acc, mag,
+                                                           reload);
             else
-                ekf_record_step<double, true, true, true, kPin>(x, 1.0, P, Wr, kc, gy, dt, false, acc, mag, reload);
+                ekf_record_step<double, true, true, true>(x, 1.0, P, Wr, kc, gy, dt, false, acc, mag, reload);
             ++applied;
         }
         mode.leave();
@@ -292,25 +254,6 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
             if (ready) queue.push(rc, esc, q.dt);
         }
     };
-#if PEKF_LIVE_PEND_LDS
-    __shared__ float p_f[15][kRunBlock];
-    __shared__ double p_d[5][kRunBlock];
-    __shared__ uint32_t p_fl[kRunBlock];
-    const PendLds pend_lds = {p_f, p_d, p_fl};
-    bool pend = false;
-    auto on_event = [&](const float4 v4) {
-        fe.event<TE>(v4, [&](const RawRec &r) {
-            pend = true;
-            pend_lds.put(r);
-        });
-    };
-    auto flush = [&]() {
-        if (pend) {
-            pend = false;
-            push_pending(pend_lds.get());
-        }
-    };
-#else
     auto on_event = [&](const float4 v4) { fe.event<TE>(v4); };
     auto flush = [&]() {
         if (fe.pend) {
@@ -318,7 +261,6 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
             push_pending(fe.p);
         }
     };
-#endif
 
     // Events stream through a register ring of kRing rows loaded kRing events ahead (the loop is
     // unrolled by kRing so every ring index is static; rows past the end are clamped to the last one).

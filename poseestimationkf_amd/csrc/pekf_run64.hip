@@ -195,7 +195,8 @@ extern "C" int pekf_run_rec64_dev(int64_t batch, int64_t n_steps, int64_t window
     if (batch == 0 || n_steps == 0) return PEKF_OK;
     PEKF_CHECK_ARG(window > 0 && step0 >= 0, "window must be > 0 and step0 >= 0");
     PEKF_CHECK_ARG(batch < ((int64_t)1 << 27), "batch must be < 2^27 filters per launch (32-bit lane offsets of 32 B)");
-    PEKF_CHECK_ARG(n_steps < ((int64_t)1 << 31), "n_steps must be < 2^31 records per launch");
+    PEKF_CHECK_ARG(n_steps < ((int64_t)1 << 31) && window < ((int64_t)1 << 31),
+                   "n_steps and window must be < 2^31 (RowCursor64 holds the window as int32)");
     PEKF_CHECK_ARG(plane_gd && plane_am && plane_my && refs && X && P, "null pointer");
     PEKF_CHECK_ARG(((uintptr_t)plane_gd % 32 == 0) && ((uintptr_t)plane_am % 32 == 0) &&
                        ((uintptr_t)plane_my % 16 == 0) && ((uintptr_t)traj % 16 == 0),

@@ -391,12 +391,6 @@ __device__ __forceinline__ void from_ref_basis(const RW &Wr, double *x, Sym4T<PT
     P = sym_rotate<false>(qw, P);
 }
 
-// Records in flight per lane in the multi-record loop (2: ping-pong, the next row's record loads
-// while the current one is processed)
-#ifndef PEKF_RUN_PREFETCH
-#define PEKF_RUN_PREFETCH 2
-#endif
-
 // Occupancy target of k_run in waves per SIMD (0: the compiler's choice)
 #ifndef PEKF_RUN_WAVES
 #define PEKF_RUN_WAVES 0
@@ -515,12 +509,9 @@ __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run(int64_t batch, 
     const uint32_t lane = (uint32_t)b;
     const uint32_t off16 = lane * 16u, off8 = lane * 8u;
     RowCursor rows(gd, am, my, batch, window);
-    // rows the cursor runs ahead of the record a step works on (the prefetch depth)
-#if PEKF_RUN_PREFETCH > 2
-    constexpr int32_t kLag = PEKF_RUN_PREFETCH - 1;
-#else
+    // rows the cursor runs ahead of the record a step works on (ping-pong: one; deeper prefetch rings
+    // were measured and not kept, profiles/r1/README.md)
     constexpr int32_t kLag = 1;
-#endif
     // One record: Prediction + Correction (main_file.py:42-45) on (x, P) in registers.
     auto step = [&](const Rec &cur, int32_t t, double n2, const auto &ref, auto lazy) {
         // the multi-record loop (RefW) carries N and an unnormalised X, the one-record launch
@@ -608,30 +599,6 @@ __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run(int64_t batch, 
     rb = rows.load(off16, off8);
     // the FP64 loop folds its exact halvings into output modifiers, which need this MODE
     OmodMode mode;
-#if PEKF_RUN_PREFETCH > 2
-    // a ring of D records, D - 1 steps ahead: slot (k - 1) % D takes row t + D - 1 as step t
-    // consumes slot k % D (unrolled by D, so every index is static)
-    constexpr int D = PEKF_RUN_PREFETCH;
-    Rec ring[D];
-    ring[0] = ra;
-    ring[1] = rb;
-#pragma unroll
-    for (int k = 2; k < D; ++k) {
-        rows.advance();
-        ring[k] = rows.load(off16, off8);
-    }
-    if constexpr (!MIXED) mode.enter();
-    step(ring[0], 0, state_norm2(x), Wr, eager{});
-    for (int32_t t = 1; t < n32;) {
-#pragma unroll
-        for (int k = 1; k <= D; ++k) {
-            rows.advance();
-            ring[(k - 1) % D] = rows.load(off16, off8);
-            step(ring[k % D], t, 1.0, Wr, lazy{});
-            if (++t == n32) break;
-        }
-    }
-#else
     if constexpr (!MIXED) mode.enter();
     step(ra, 0, state_norm2(x), Wr, eager{});
     for (int32_t t = 1; t < n32;) {
@@ -644,7 +611,6 @@ __global__ __launch_bounds__(kRunBlock) PEKF_RUN_ATTR void k_run(int64_t batch, 
         step(ra, t, 1.0, Wr, lazy{});
         ++t;
     }
-#endif
     if constexpr (!MIXED) mode.leave();
     if (COUNTS && my_steps == 0) return;
     from_ref_basis(Wr, x, P, rs);

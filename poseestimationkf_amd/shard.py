@@ -101,7 +101,9 @@ class Communicator:
     def wait(self, stream=None, timeout=None):
         """Drain `stream`, collectives of this communicator included.  Each of its collectives gets the
         deadline (default comm_timeout()) from the moment the stream reaches it, so queued compute is never
-        charged; one a peer never joins raises CommTimeoutError and aborts the communicator."""
+        charged; one a peer never joins raises CommTimeoutError and aborts the communicator.  The clock starts
+        when this rank's inputs are ready, so the peers' skew (their remaining compute) counts against it:
+        the timeout must exceed that skew.  More than 1,024 collectives in flight are refused (pekf.h)."""
         check(self._lib.pekf_comm_wait(self.handle, stream, comm_timeout() if timeout is None else float(timeout)))
 
     def max_over_ranks_array(self, values, stream=None):
@@ -283,9 +285,14 @@ def connect(rank, world, rendezvous=None):
     rdzv = rendezvous or FileRendezvous(rank, world)
     uid = rdzv.share_id()
     try:
-        return Communicator(uid, world, rank)
-    finally:
-        rdzv.done()   # rank 0: created or failed, the id is spent (a relaunch must not read it)
+        comm = Communicator(uid, world, rank)
+    except BaseException as e:
+        # rank 0's creation failed or timed out: ranks that have not read the id yet stop at once
+        # (the failure marker replaces the id) instead of waiting out PEKF_RDZV_TIMEOUT_S
+        rdzv.fail("rank 0's RCCL communicator creation failed: %s" % e)
+        raise
+    rdzv.done()   # rank 0: created, the id is spent (a relaunch must not read it)
+    return comm
 
 
 def gather_quaternions(comm: Communicator, x_dev_ptr, batch_local, recv=None, root=0, stream=None):

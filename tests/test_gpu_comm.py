@@ -129,6 +129,35 @@ def test_comm_wait_deadline_charges_collectives_not_compute(eng):
     c.close()                                        # an aborted communicator only frees
 
 
+def test_collectives_past_the_tracking_limit_are_refused_not_untracked(eng):
+    """libpekf tracks at most 1,024 incomplete collectives per communicator (pekf_comm_wait's per-collective
+    clock needs each one's events).  Behind ~0.3 s of compute, 1,100 all-reduces are enqueued: the 1,025th
+    is refused with PEKF_ERR_COMM and never enqueued (an evicted, untracked collective that a
+    peer never joined would have stalled the stream with no deadline running); the 1,024 tracked ones
+    drain under the deadline, and afterwards the communicator takes collectives again."""
+    from poseestimationkf_amd import shard
+    from poseestimationkf_amd._lib import PekfError
+    c = shard.Communicator(shard.Communicator.unique_id(), 1, 0)
+    B = 1 << 18
+    win = eng.IMUWindow(B, 64).synthesize(seed=synth.DEFAULT_SEED)
+    f = eng.BatchedEKF(B)
+    s = eng.Stream()
+    buf = eng.DeviceBuffer(8)
+    buf.upload(np.array([1.5]))
+    f.run_async(win, 100000, 0, s.handle)
+    done = 0
+    with pytest.raises(PekfError, match="collectives already in flight"):
+        for _ in range(1100):
+            c.allreduce_max(buf.ptr, 1, s.handle)
+            done += 1
+    assert done == 1024
+    c.wait(s.handle, timeout=30)
+    c.allreduce_max(buf.ptr, 1, s.handle)
+    c.wait(s.handle, timeout=30)
+    assert buf.download((1,), np.float64)[0] == 1.5
+    c.close()
+
+
 def test_multi_device_ekf_sync_has_the_deadline(eng):
     """The one-process N-GPU path (MultiDeviceEKF, what plain `bench.py --gpus N` runs) drains through
     pekf_comm_wait: compute + a grouped gather pass a 5 ms deadline; a grouped-gather communicator with a

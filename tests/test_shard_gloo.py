@@ -210,9 +210,11 @@ def test_rendezvous_relaunch_with_the_same_key_after_a_failure(tmp_path):
     assert shard.FileRendezvous(1, 2, directory=d, environ=env1, timeout=5).share_id() == ID
 
 
-def test_connect_removes_the_id_when_communicator_creation_fails(tmp_path, monkeypatch):
-    """Rank 0's published id is removed even when its communicator creation raises (an init timeout,
-    after which bench.py leaves with os._exit), so a relaunch cannot read a spent id."""
+def test_connect_publishes_the_failure_when_communicator_creation_fails(tmp_path, monkeypatch):
+    """When rank 0's communicator creation raises (an init timeout, after which bench.py leaves with
+    os._exit), its published id is replaced by the failure marker: a rank that has not read the id yet
+    raises at once instead of waiting out PEKF_RDZV_TIMEOUT_S, and no rank can read the spent id.  On
+    success the id file is removed."""
     class Boom(RuntimeError):
         pass
 
@@ -224,4 +226,15 @@ def test_connect_removes_the_id_when_communicator_creation_fails(tmp_path, monke
     monkeypatch.setattr(shard.Communicator, "unique_id", staticmethod(lambda: ID))
     with pytest.raises(Boom):
         shard.connect(0, 2, r0)
+    import time
+    t0 = time.monotonic()
+    with pytest.raises(shard.RendezvousError, match="init timed out"):
+        shard.FileRendezvous(1, 2, key="jobC", directory=str(tmp_path), environ={}, timeout=60).share_id()
+    assert time.monotonic() - t0 < 5
+
+    def fake_init(self, uid, nranks, rank, _handle=None):
+        self.handle = None
+    monkeypatch.setattr(shard.Communicator, "__init__", fake_init)
+    r0 = shard.FileRendezvous(0, 2, key="jobD", directory=str(tmp_path), environ={})
+    assert isinstance(shard.connect(0, 2, r0), shard.Communicator)
     assert not os.path.exists(r0.path)
