@@ -21,6 +21,8 @@ import sys
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+# where the fixtures are written (tests/test_golden_regen.py regenerates them into a scratch directory)
+OUT = os.environ.get("PEKF_GOLDEN_OUT") or HERE
 ROOT = os.path.dirname(os.path.dirname(HERE))
 REF_DIR = "/root/reference/Python Kalman Filter"
 sys.path.insert(0, ROOT)
@@ -60,9 +62,9 @@ def main():
             z, P, Kk = kf.Prediction(g, T, X, P)
             X, P = kf.Correction(m, a, z, P, Kk)
             traj[i, k] = X
-    np.savez_compressed(os.path.join(HERE, "gaps.npz"), gyro=rec.gyro, acc=rec.acc, mag=rec.mag, dt=dt,
+    np.savez_compressed(os.path.join(OUT, "gaps.npz"), gyro=rec.gyro, acc=rec.acc, mag=rec.mag, dt=dt,
                         acc0=rec.acc0, mag0=rec.mag0, t0=t0, traj=traj)
-    print("gaps.npz", os.path.getsize(os.path.join(HERE, "gaps.npz")))
+    print("gaps.npz", os.path.getsize(os.path.join(OUT, "gaps.npz")))
 
 
 if __name__ == "__main__":

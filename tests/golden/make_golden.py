@@ -29,6 +29,8 @@ import sys
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+# where the fixtures are written (tests/test_golden_regen.py regenerates them into a scratch directory)
+OUT = os.environ.get("PEKF_GOLDEN_OUT") or HERE
 ROOT = os.path.dirname(os.path.dirname(HERE))
 REF_DIR = "/root/reference/Python Kalman Filter"
 sys.path.insert(0, ROOT)
@@ -323,18 +325,18 @@ def make_c1():
 def main():
     ekf, wb, uf = import_reference()
     kat = make_kat(ekf, wb, uf)
-    np.savez_compressed(os.path.join(HERE, "kat.npz"), **kat)
+    np.savez_compressed(os.path.join(OUT, "kat.npz"), **kat)
     traj = make_traj(ekf)
-    np.savez_compressed(os.path.join(HERE, "traj.npz"), **traj)
-    np.savez_compressed(os.path.join(HERE, "edge.npz"), **make_edge(ekf, wb))
-    np.savez_compressed(os.path.join(HERE, "side.npz"), **make_side(ekf, wb, uf))
+    np.savez_compressed(os.path.join(OUT, "traj.npz"), **traj)
+    np.savez_compressed(os.path.join(OUT, "edge.npz"), **make_edge(ekf, wb))
+    np.savez_compressed(os.path.join(OUT, "side.npz"), **make_side(ekf, wb, uf))
     text, xk = make_c1()
-    with open(os.path.join(HERE, "c1_log.txt.gz"), "wb") as raw, \
+    with open(os.path.join(OUT, "c1_log.txt.gz"), "wb") as raw, \
             gzip.GzipFile(fileobj=raw, mode="wb", mtime=0, filename="") as gz:  # byte-stable output
         gz.write(text.encode())
-    np.save(os.path.join(HERE, "c1_xk.npy"), xk)
-    for f in sorted(os.listdir(HERE)):
-        print(f, os.path.getsize(os.path.join(HERE, f)))
+    np.save(os.path.join(OUT, "c1_xk.npy"), xk)
+    for f in sorted(os.listdir(OUT)):
+        print(f, os.path.getsize(os.path.join(OUT, f)))
 
 
 if __name__ == "__main__":

@@ -23,6 +23,8 @@ import sys
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+# where the fixtures are written (tests/test_golden_regen.py regenerates them into a scratch directory)
+OUT = os.environ.get("PEKF_GOLDEN_OUT") or HERE
 ROOT = os.path.dirname(os.path.dirname(HERE))
 REF_DIR = "/root/reference/Python Kalman Filter"
 sys.path.insert(0, ROOT)
@@ -54,10 +56,10 @@ def main():
         g = runpy.run_path(os.path.join(REF_DIR, "Test.py"), run_name="__main__")["g"]
     finally:
         builtins.open = real_open
-    np.savez_compressed(os.path.join(HERE, "lpf_testpy.npz"), acc_raw=acc_raw, mag_raw=mag_raw,
+    np.savez_compressed(os.path.join(OUT, "lpf_testpy.npz"), acc_raw=acc_raw, mag_raw=mag_raw,
                         acc_lpf=np.asarray(g.acc_1, np.float64), mag_lpf=np.asarray(g.mag_1, np.float64),
                         alpha=np.array([0.1]))
-    print("lpf_testpy.npz", os.path.getsize(os.path.join(HERE, "lpf_testpy.npz")))
+    print("lpf_testpy.npz", os.path.getsize(os.path.join(OUT, "lpf_testpy.npz")))
 
 
 if __name__ == "__main__":
