@@ -266,6 +266,15 @@ int pekf_frontend_dev(int64_t batch, int64_t n_events, const void *ev_planes, co
 #define PEKF_EV_TIME 3u
 #define PEKF_EV_TIME_EVENTS 0x1u
 #define PEKF_EV_F32_RECORDS 0x2u /* pekf_live_ext_dev: records rounded to the f32 stream record format */
+/* FP64 events (pekf_live_ext_dev, pekf_frontend_ext_dev, pekf_frontend_init_ext_dev): ev_planes is double4
+ * [n_events][batch], 32 B per event, {x, y, z, w} where x, y, z are the sample as the server parses it
+ * (std::stod of the phone's text, KFS/Parser.cpp:23-25 -- in general not the f32 the phone measured) and
+ * w's bits are those of the event's absolute time in ns as a float64 (an integer, |t| < 2^51) with the
+ * type (0 acc, 1 gyro, 2 mag, 3 no sample) in its two lowest bits.  t_init / t_start are times on the
+ * same clock.  Any gap or clock step is just the next event's time (no time events); records are FP64
+ * throughout, their dt any float64.  Host packing: pekf_wire_parse (wire text) or pekf_f32_wire_values
+ * (f32 samples -> the doubles the server would parse). */
+#define PEKF_EV_F64_EVENTS 0x4u
 /* pekf_frontend_dev with time events (flags) and escaped records: a record whose dt does not fit the
  * dt word gets PEKF_DT_ESCAPE and its float64 dt in dt_ext[r_max][batch] (the window's dt side plane for
  * pekf_run_ext_dev; only escaped entries are written), and *dev_error |= 4 says some record was escaped.
@@ -293,7 +302,8 @@ int pekf_live_dev(int64_t batch, int64_t n_events, const void *ev_planes, const 
                   const int64_t *t_init, double alpha, double *X, double *P, double q, double r,
                   int32_t *counts, double *refs, int *dev_error, void *stream);
 /* pekf_live_dev with flags (PEKF_EV_TIME_EVENTS: the planes hold time events; PEKF_EV_F32_RECORDS: f32
- * records, the split pipeline's). */
+ * records, the split pipeline's; PEKF_EV_F64_EVENTS alone: FP64 events, every record field FP64 -- the
+ * server's own input values end to end). */
 int pekf_live_ext_dev(int64_t batch, int64_t n_events, const void *ev_planes, const double *init,
                       const int64_t *t_init, double alpha, double *X, double *P, double q, double r,
                       int32_t *counts, double *refs, uint32_t flags, int *dev_error, void *stream);
@@ -309,6 +319,29 @@ int pekf_live_ext_dev(int64_t batch, int64_t n_events, const void *ev_planes, co
  * with stats NULL the second pass over the events (the variances) is skipped. */
 int pekf_frontend_init_dev(int64_t batch, int64_t n_events, const void *ev_planes, const int64_t *t_start,
                            int n_avg, double *init, int64_t *t_init, double *stats, int32_t *ready, void *stream);
+/* pekf_frontend_init_dev with flags: PEKF_EV_F64_EVENTS (FP64 events: the means and variances of the
+ * server's own stod values, Parser.cpp:23-25,84-140; times absolute).  PEKF_EV_TIME_EVENTS is accepted
+ * and changes nothing (phase 2 always honours time events). */
+int pekf_frontend_init_ext_dev(int64_t batch, int64_t n_events, const void *ev_planes, const int64_t *t_start,
+                               int n_avg, double *init, int64_t *t_init, double *stats, int32_t *ready,
+                               uint32_t flags, void *stream);
+
+/* ---------------- the phone -> server wire: host code ----------------
+ * The Android client sends each sample as text, Float.toString of each value
+ * (ASC/MessageSender.java:217-233: "#<phase>,<type>:<x>,<y>,<z>,t:<ns>" padded to 99 characters), and
+ * the server parses the values with std::stod (KFS/Parser.cpp:12-26): doubles, in general not the
+ * floats the phone measured.  These two functions give the FP64 event planes those doubles.
+ * pekf_wire_parse: the server's parse of such text, one message per line (Parser::run keeps messages
+ * starting with '#'; ProcessString skips one of 30 characters or fewer after the '#', newline
+ * included).  phase / type: the digits' values; xyz[3n] as strtod (= std::stod) gives them; t_ns as
+ * strtoll (= std::stoll).  All four outputs NULL: count only (*n_events).  A message the server's stod /
+ * stoll would throw on returns PEKF_ERR_INVALID naming its line. */
+int pekf_wire_parse(const char *text, int64_t len, int64_t max_events, uint8_t *phase, uint8_t *type, double *xyz,
+                    int64_t *t_ns, int64_t *n_events);
+/* out[i] = the double std::stod makes of Float.toString(in[i]): the shortest decimal that rounds to the
+ * float, the closest one among those (JDK 19+ Float.toString; one that needs a single digit prints the
+ * closest of one or two digits), read back correctly rounded. */
+int pekf_f32_wire_values(int64_t n, const float *in, double *out);
 
 /* X = [1,0,0,0], P = I for every filter (main_file.py:23,26). */
 int pekf_reset_state_dev(int64_t batch, double *X, double *P, void *stream);

@@ -131,6 +131,8 @@ def initial_values(types, values, times, n_avg=100):
     kalman, t_last = False, None
     for ty, v, t in zip(types, values, times):
         ty, t = int(ty), int(t)
+        if ty not in keys:  # not a message (type 3: stream padding / a clock step)
+            continue
         if not all(done.values()):
             if ty in sums:
                 if len(samples[ty]) < n_avg:

@@ -27,6 +27,7 @@ RUN_STATE_SOA = 0x2
 DT_ESCAPE = 0x7FFFFFFF
 EV_TIME_EVENTS = 0x1
 EV_F32_RECORDS = 0x2
+EV_F64_EVENTS = 0x4
 
 
 class PekfError(RuntimeError):
@@ -114,6 +115,9 @@ SIGNATURES = {
     "pekf_frontend_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "pekf_frontend_ext_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp],
     "pekf_frontend_init_dev": [_i64, _i64, _vp, _vp, _int, _vp, _vp, _vp, _vp, _vp],
+    "pekf_frontend_init_ext_dev": [_i64, _i64, _vp, _vp, _int, _vp, _vp, _vp, _vp, _u32, _vp],
+    "pekf_f32_wire_values": [_i64, _vp, _vp],
+    "pekf_wire_parse": [ctypes.c_char_p, _i64, _i64, _vp, _vp, _vp, _vp, ctypes.POINTER(_i64)],
     "pekf_live_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _vp, _vp, _dbl, _dbl, _vp, _vp, _vp, _vp],
     "pekf_live_ext_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _vp, _vp, _dbl, _dbl, _vp, _vp, _u32, _vp, _vp],
     "pekf_log_scan": [ctypes.c_char_p, ctypes.POINTER(_i64)],

@@ -14,7 +14,6 @@
 namespace pekf {
 
 constexpr int kFeBlock = 256;
-typedef float nv4f __attribute__((ext_vector_type(4)));  // the native vector the nontemporal builtins take
 // Non-temporal event loads (every event is read once per pass): k_frontend -1.7 %, phase 2's means
 // -5 % (profiles/r4/ntload/).
 #ifndef PEKF_FE_NTL
@@ -35,21 +34,30 @@ typedef float nv4f __attribute__((ext_vector_type(4)));  // the native vector th
 constexpr int kFeGroup = 8;
 constexpr int kFePool = 64;
 constexpr int kFeRows = 32;
+// FP64 events write 80 B FP64 records: PEKF_FE_POOL64 slots per group (32 = 20 KB per wave, the f32
+// form's LDS footprint and waves per CU)
+#ifndef PEKF_FE_POOL64
+#define PEKF_FE_POOL64 32
+#endif
 
 // The pooled queue's LDS (one wave per block, so no barrier: a wave's LDS accesses complete in
 // order): per group, P record slots and the ring of its free slot numbers; per lane, the slot of its
-// record for each row base .. base + ROWS - 1 (row % ROWS).
-template <int P, int NG, int ROWS>
+// record for each row base .. base + ROWS - 1 (row % ROWS).  R: the record (Rec, or Rec64 for FP64
+// events), its three planes held as three arrays.
+template <int P, int NG, int ROWS, typename R>
 struct FePool {
     static_assert(P <= 255, "slot numbers are bytes");
-    float4 gd[NG][P];
-    float4 am[NG][P];
-    float2 my[NG][P];
+    decltype(R::gd) gd[NG][P];
+    decltype(R::am) am[NG][P];
+    decltype(R::my) my[NG][P];
     uint8_t ring[NG][P];
     uint8_t slot[ROWS][64];
 };
 #ifndef PEKF_FE_RING
 #define PEKF_FE_RING 9
+#endif
+#ifndef PEKF_FE_RING64
+#define PEKF_FE_RING64 3  // FP64 events: 32 B each, so fewer in flight (registers)
 #endif
 
 // TE: the event planes may hold time events (Phase3::event).  dtx (may be null): the window's dt side
@@ -63,16 +71,24 @@ struct FePool {
 // by an empty pool, is stored directly.  Row base is written by every lane of the group holding it once
 // all of the group's ready lanes have made it; its slots go back to the ring; the queue drains after
 // the last event.  The records and their rows are unchanged; only the order of the stores differs.
-template <bool TE>
-__global__ __launch_bounds__(64) void k_frontend(int64_t batch, int64_t n_events, const float4 *__restrict__ ev,
+//
+// EV64: FP64 events (double4 planes, PEKF_EV_F64_EVENTS) -> FP64 records (Rec64: the planes of
+// pekf_run_rec64_dev), every field FP64 and the dt any float64 (nothing escaped; dtx unused).
+template <bool TE, bool EV64 = false>
+__global__ __launch_bounds__(64) void k_frontend(int64_t batch, int64_t n_events,
+                                                 const std::conditional_t<EV64, double4, float4> *__restrict__ ev,
                                                  const double *__restrict__ init, const int64_t *__restrict__ t_init,
-                                                 double alpha, int64_t r_max, float4 *__restrict__ gd,
-                                                 float4 *__restrict__ am, float2 *__restrict__ my,
+                                                 double alpha, int64_t r_max,
+                                                 decltype(std::conditional_t<EV64, Rec64, Rec>::gd) *__restrict__ gd,
+                                                 decltype(std::conditional_t<EV64, Rec64, Rec>::am) *__restrict__ am,
+                                                 decltype(std::conditional_t<EV64, Rec64, Rec>::my) *__restrict__ my,
                                                  double *__restrict__ dtx, int32_t *__restrict__ counts,
                                                  double *__restrict__ refs, int *__restrict__ err) {
+    using EvT = std::conditional_t<EV64, double4, float4>;
+    using RecT = std::conditional_t<EV64, Rec64, Rec>;
     const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;
     if (b >= batch) return;
-    Phase3 fe;
+    Phase3T<std::conditional_t<EV64, V3, F3>> fe;
     fe.start(init + 6 * b, t_init[b], alpha);
     const bool ready = init_is_finite(init + 6 * b);  // not ready (phase 2 unfinished): no records
     {
@@ -84,9 +100,9 @@ __global__ __launch_bounds__(64) void k_frontend(int64_t batch, int64_t n_events
     int32_t r = 0;  // this filter's records so far (r_max < 2^31, checked on the host)
     const int32_t rmax = (int32_t)r_max;
     int bad = 0;
-    constexpr int POOL = kFePool, kG = kFeGroup, kRows = kFeRows;
+    constexpr int POOL = EV64 ? PEKF_FE_POOL64 : kFePool, kG = kFeGroup, kRows = kFeRows;
     static_assert(kRows > 0 && kRows <= 32 && (kRows & (kRows - 1)) == 0, "a power-of-two row span of at most 32");
-    __shared__ FePool<POOL, 64 / kG, kRows> st;
+    __shared__ FePool<POOL, 64 / kG, kRows, RecT> st;
     const int col = threadIdx.x & 63;
     // the oldest row the group's queue holds (the same in each group of kG lanes)
     int32_t base = 0;
@@ -108,8 +124,16 @@ __global__ __launch_bounds__(64) void k_frontend(int64_t batch, int64_t n_events
     auto flush_pool = [&]() {
         const bool has = fe.pend;
         bool esc = false;
-        Rec rc{};
-        if (has) rc = fe.emit(esc);
+        RecT rc{};
+        if (has) {
+            if constexpr (EV64) {
+                rc.gd = fe.emit64();
+                rc.am = make_double4(fe.lpf_acc.x, fe.lpf_acc.y, fe.lpf_acc.z, fe.lpf_mag.x);
+                rc.my = make_double2(fe.lpf_mag.y, fe.lpf_mag.z);
+            } else {
+                rc = fe.emit(esc);
+            }
+        }
         const bool live = has && ready;
         if (live && esc) bad |= dtx ? 4 : 1;
         const bool in = live && r < rmax;
@@ -133,7 +157,7 @@ __global__ __launch_bounds__(64) void k_frontend(int64_t batch, int64_t n_events
             am[o] = rc.am;
             my[o] = rc.my;
         }
-        if (in && esc && dtx) dtx[o] = fe.p.dt;
+        if (!EV64 && in && esc && dtx) dtx[o] = fe.p.dt;
         const int t = k < nfree ? k : nfree;
         head += t;
         if (head >= POOL) head -= POOL;
@@ -179,32 +203,30 @@ __global__ __launch_bounds__(64) void k_frontend(int64_t batch, int64_t n_events
     // is pending after a whole block.
     const uint32_t lane = (uint32_t)b;
     const int32_t n_ev = (int32_t)n_events;
-    auto load = [&](int32_t e) -> float4 {
+    auto load = [&](int32_t e) -> EvT {
         const int32_t row = e < n_ev ? e : n_ev - 1;
-#if PEKF_FE_NTL
-        const nv4f v = __builtin_nontemporal_load((const nv4f *)(ev + (int64_t)row * batch + lane));
-        return make_float4(v.x, v.y, v.z, v.w);
-#else
-        return (ev + (int64_t)row * batch)[lane];
-#endif
+        return load_event<PEKF_FE_NTL>(ev + (int64_t)row * batch + lane);
     };
     if (n_ev > 0) {
-        constexpr int kRing = PEKF_FE_RING;  // events in flight per lane (a multiple of kFlush)
+        constexpr int kRing = EV64 ? PEKF_FE_RING64 : PEKF_FE_RING;  // events in flight per lane (a multiple of kFlush)
         static_assert(kRing % kFlush == 0, "the ring depth must be a multiple of the flush period");
-        float4 ring[kRing];
+        EvT ring[kRing];
 #pragma unroll
         for (int k = 0; k < kRing; ++k) ring[k] = load(k);
         for (int32_t e0 = 0; e0 < n_ev; e0 += kRing) {
             if (e0 + kRing > n_ev) {  // uniform, once per launch
 #pragma unroll
                 for (int k = 0; k < kRing; ++k)
-                    if (e0 + k >= n_ev) ring[k] = make_float4(0.f, 0.f, 0.f, __uint_as_float(PEKF_EV_TIME));
+                    if (e0 + k >= n_ev) ring[k] = null_event<EvT>();
             }
 #pragma unroll
             for (int k = 0; k < kRing; ++k) {
-                const float4 v4 = ring[k];
+                const EvT v4 = ring[k];
                 ring[k] = load(e0 + k + kRing);
-                fe.event<TE>(v4);
+                if constexpr (EV64)
+                    fe.event64(v4);
+                else
+                    fe.template event<TE>(v4);
                 if ((k + 1) % kFlush == 0) {
                     flush_pool();
                     drain_pool(false);
@@ -227,10 +249,15 @@ __global__ __launch_bounds__(64) void k_frontend(int64_t batch, int64_t n_events
 // from init = {mean acc, mean mag} at t_init = the last phase-2 event's time -- exactly the inputs of
 // pekf_frontend_dev.  Same event planes as phase 3; two passes over them (the variance needs the
 // mean first, as InitialValues::compute_mean_and_variance has it).
-__global__ __launch_bounds__(kFeBlock) void k_frontend_init(int64_t batch, int64_t n_events, const float4 *__restrict__ ev,
+// EV64: FP64 events (the server's stod doubles are what it averages, Parser.cpp:23-25,84-140); their
+// times are absolute, and a type-3 event carries no sample.
+template <bool EV64 = false>
+__global__ __launch_bounds__(kFeBlock) void k_frontend_init(int64_t batch, int64_t n_events,
+                                                            const std::conditional_t<EV64, double4, float4> *__restrict__ ev,
                                                             const int64_t *__restrict__ t_start, int n_avg,
                                                             double *__restrict__ init, int64_t *__restrict__ t_init,
                                                             double *__restrict__ stats, int32_t *__restrict__ ready) {
+    using EvT = std::conditional_t<EV64, double4, float4>;
     const int64_t b = (int64_t)blockIdx.x * kFeBlock + threadIdx.x;
     if (b >= batch) return;
     const uint32_t lane = (uint32_t)b;
@@ -246,17 +273,11 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend_init(int64_t batch, int64
     // in both passes), so no exit sits inside the unrolled body.
     constexpr int kInitRing = 8;
     const int32_t n_ev = (int32_t)n_events;
-    const float4 null_ev = make_float4(0.f, 0.f, 0.f, __uint_as_float(PEKF_EV_TIME));
-    auto row = [&](int32_t e) -> float4 {
-        const float4 *q = ev + (int64_t)(e < n_ev ? e : n_ev - 1) * batch + lane;
-#if PEKF_INIT_NTL
-        const nv4f v = __builtin_nontemporal_load((const nv4f *)q);
-        return make_float4(v.x, v.y, v.z, v.w);
-#else
-        return *q;
-#endif
+    const EvT null_ev = null_event<EvT>();
+    auto row = [&](int32_t e) -> EvT {
+        return load_event<PEKF_INIT_NTL>(ev + (int64_t)(e < n_ev ? e : n_ev - 1) * batch + lane);
     };
-    auto pad = [&](int32_t e0, float4 (&r)[kInitRing]) {
+    auto pad = [&](int32_t e0, EvT (&r)[kInitRing]) {
         if (e0 + kInitRing > n_ev) {  // uniform: the last block only
 #pragma unroll
             for (int k = 0; k < kInitRing; ++k)
@@ -264,20 +285,27 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend_init(int64_t batch, int64
         }
     };
     for (int32_t e0 = 0; e0 < n_ev; e0 += kInitRing) {
-        float4 r[kInitRing];
+        EvT r[kInitRing];
 #pragma unroll
         for (int k = 0; k < kInitRing; ++k) r[k] = row(e0 + k);
         pad(e0, r);
 #pragma unroll
         for (int k = 0; k < kInitRing; ++k) {
-            const float4 v4 = r[k];
-            const uint32_t word = __float_as_uint(v4.w);
-            const int ty = (int)(word & 3u);
-            if (word == PEKF_EV_TIME) {  // a time event: the clock moves, nothing else happens
-                t += (int64_t)time_step(v4);
-                continue;
+            const EvT v4 = r[k];
+            int ty;
+            if constexpr (EV64) {
+                ty = (int)ev64_type(v4);
+                if (ty == 3) continue;  // no sample
+                t = (int64_t)ev64_time(v4);
+            } else {
+                const uint32_t word = __float_as_uint(v4.w);
+                ty = (int)(word & 3u);
+                if (word == PEKF_EV_TIME) {  // a time event: the clock moves, nothing else happens
+                    t += (int64_t)time_step(v4);
+                    continue;
+                }
+                t += (int64_t)(word >> 2);
             }
-            t += (int64_t)(word >> 2);
             if (!(done[0] && done[1] && done[2])) {
                 if (ty <= 2) {
                     if (cnt[ty] < n_avg) {
@@ -307,14 +335,18 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend_init(int64_t batch, int64
     for (int32_t e0 = 0; stats && e0 < n_ev; e0 += kInitRing) {
         // done once every type has its n_avg; a filter that never got ready reports NaN, so reads none
         if (!kalman || (c2[0] >= n_avg && c2[1] >= n_avg && c2[2] >= n_avg)) break;
-        float4 r[kInitRing];
+        EvT r[kInitRing];
 #pragma unroll
         for (int k = 0; k < kInitRing; ++k) r[k] = row(e0 + k);
         pad(e0, r);
 #pragma unroll
         for (int k = 0; k < kInitRing; ++k) {
-            const float4 v4 = r[k];
-            const int ty = (int)(__float_as_uint(v4.w) & 3u);
+            const EvT v4 = r[k];
+            int ty;
+            if constexpr (EV64)
+                ty = (int)ev64_type(v4);
+            else
+                ty = (int)(__float_as_uint(v4.w) & 3u);
             if (ty <= 2 && c2[ty] < n_avg) {
 #pragma clang fp contract(off)
                 const double d0 = (double)v4.x - mean[ty][0], d1 = (double)v4.y - mean[ty][1],
@@ -349,19 +381,33 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend_init(int64_t batch, int64
 
 using namespace pekf;
 
-extern "C" int pekf_frontend_init_dev(int64_t batch, int64_t n_events, const void *ev_planes, const int64_t *t_start,
-                                      int n_avg, double *init, int64_t *t_init, double *stats, int32_t *ready,
-                                      void *stream) {
+extern "C" int pekf_frontend_init_ext_dev(int64_t batch, int64_t n_events, const void *ev_planes,
+                                          const int64_t *t_start, int n_avg, double *init, int64_t *t_init,
+                                          double *stats, int32_t *ready, uint32_t flags, void *stream) {
     PEKF_CHECK_ARG(batch >= 0 && n_events >= 0, "negative size");
     PEKF_CHECK_ARG(n_avg >= 2, "n_avg must be >= 2 (the variance divides by n_avg - 1)");
     PEKF_CHECK_ARG(n_events < ((int64_t)1 << 30), "n_events must be < 2^30 per launch");
+    PEKF_CHECK_ARG((flags & ~(PEKF_EV_TIME_EVENTS | PEKF_EV_F64_EVENTS)) == 0, "unknown flags");
     if (batch == 0) return PEKF_OK;
     PEKF_CHECK_ARG(ev_planes && t_start && init && t_init && ready, "null pointer");
-    hipLaunchKernelGGL(k_frontend_init, dim3(grid_for(batch, kFeBlock)), dim3(kFeBlock), 0, as_stream(stream), batch,
-                       n_events, static_cast<const float4 *>(ev_planes), t_start, n_avg, init, t_init, stats, ready);
+    PEKF_CHECK_ARG((uintptr_t)ev_planes % 16 == 0, "misaligned event planes");
+    const dim3 grid(grid_for(batch, kFeBlock)), block(kFeBlock);
+    if (flags & PEKF_EV_F64_EVENTS)
+        hipLaunchKernelGGL(k_frontend_init<true>, grid, block, 0, as_stream(stream), batch, n_events,
+                           static_cast<const double4 *>(ev_planes), t_start, n_avg, init, t_init, stats, ready);
+    else  // phase 2 always honours time events
+        hipLaunchKernelGGL(k_frontend_init<false>, grid, block, 0, as_stream(stream), batch, n_events,
+                           static_cast<const float4 *>(ev_planes), t_start, n_avg, init, t_init, stats, ready);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_frontend_init");
     return PEKF_OK;
+}
+
+extern "C" int pekf_frontend_init_dev(int64_t batch, int64_t n_events, const void *ev_planes, const int64_t *t_start,
+                                      int n_avg, double *init, int64_t *t_init, double *stats, int32_t *ready,
+                                      void *stream) {
+    return pekf_frontend_init_ext_dev(batch, n_events, ev_planes, t_start, n_avg, init, t_init, stats, ready, 0u,
+                                      stream);
 }
 
 extern "C" int pekf_frontend_ext_dev(int64_t batch, int64_t n_events, const void *ev_planes, const double *init,
@@ -369,23 +415,34 @@ extern "C" int pekf_frontend_ext_dev(int64_t batch, int64_t n_events, const void
                                      void *plane_am, void *plane_my, double *dt_ext, int32_t *counts, double *refs,
                                      uint32_t flags, int *dev_error, void *stream) {
     PEKF_CHECK_ARG(batch >= 0 && n_events >= 0 && r_max >= 0, "negative size");
-    PEKF_CHECK_ARG((flags & ~PEKF_EV_TIME_EVENTS) == 0, "unknown flags");
+    PEKF_CHECK_ARG((flags & ~(PEKF_EV_TIME_EVENTS | PEKF_EV_F64_EVENTS)) == 0, "unknown flags");
+    const bool ev64 = (flags & PEKF_EV_F64_EVENTS) != 0;
+    PEKF_CHECK_ARG(!ev64 || ((flags & PEKF_EV_TIME_EVENTS) == 0 && !dt_ext),
+                   "FP64 events carry their times and write FP64 records (no time events, no dt side plane)");
     if (batch == 0) return PEKF_OK;
     PEKF_CHECK_ARG(n_events < ((int64_t)1 << 30), "n_events must be < 2^30 per launch");
     PEKF_CHECK_ARG(r_max < ((int64_t)1 << 31), "r_max must be < 2^31");
     PEKF_CHECK_ARG(ev_planes && init && t_init && plane_gd && plane_am && plane_my && counts && refs,
                    "null pointer");
-    const auto *ev = static_cast<const float4 *>(ev_planes);
-    auto *gd = static_cast<float4 *>(plane_gd);
-    auto *am = static_cast<float4 *>(plane_am);
-    auto *my = static_cast<float2 *>(plane_my);
+    PEKF_CHECK_ARG((uintptr_t)ev_planes % 16 == 0 && (uintptr_t)plane_gd % 16 == 0 && (uintptr_t)plane_am % 16 == 0 &&
+                       (uintptr_t)plane_my % 8 == 0,
+                   "misaligned planes");
     const dim3 grid(grid_for(batch, 64)), block(64);
-    if (flags & PEKF_EV_TIME_EVENTS)
-        hipLaunchKernelGGL(k_frontend<true>, grid, block, 0, as_stream(stream), batch, n_events, ev, init, t_init,
-                           alpha, r_max, gd, am, my, dt_ext, counts, refs, dev_error);
+    if (ev64)
+        hipLaunchKernelGGL((k_frontend<false, true>), grid, block, 0, as_stream(stream), batch, n_events,
+                           static_cast<const double4 *>(ev_planes), init, t_init, alpha, r_max,
+                           static_cast<double4 *>(plane_gd), static_cast<double4 *>(plane_am),
+                           static_cast<double2 *>(plane_my), nullptr, counts, refs, dev_error);
+    else if (flags & PEKF_EV_TIME_EVENTS)
+        hipLaunchKernelGGL(k_frontend<true>, grid, block, 0, as_stream(stream), batch, n_events,
+                           static_cast<const float4 *>(ev_planes), init, t_init, alpha, r_max,
+                           static_cast<float4 *>(plane_gd), static_cast<float4 *>(plane_am),
+                           static_cast<float2 *>(plane_my), dt_ext, counts, refs, dev_error);
     else
-        hipLaunchKernelGGL(k_frontend<false>, grid, block, 0, as_stream(stream), batch, n_events, ev, init, t_init,
-                           alpha, r_max, gd, am, my, dt_ext, counts, refs, dev_error);
+        hipLaunchKernelGGL(k_frontend<false>, grid, block, 0, as_stream(stream), batch, n_events,
+                           static_cast<const float4 *>(ev_planes), init, t_init, alpha, r_max,
+                           static_cast<float4 *>(plane_gd), static_cast<float4 *>(plane_am),
+                           static_cast<float2 *>(plane_my), dt_ext, counts, refs, dev_error);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_frontend");
     return PEKF_OK;

@@ -37,6 +37,12 @@ struct Rec {
     float4 am;  // ax, ay, az, mx
     float2 my;  // my, mz
 };
+// The FP64 record (pekf_run_rec64_dev's planes; pekf_frontend_ext_dev's output with FP64 events)
+struct Rec64 {
+    double4 gd;  // gx, gy, gz, dt_ns
+    double4 am;  // ax, ay, az, mx
+    double2 my;  // my, mz
+};
 
 // Host-pointer calls: inputs are packed into one coherent, mapped pinned buffer.  Small calls
 // (<= kZeroCopyMaxBytes of inputs + outputs, e.g. the n = 1 calls of main_file.py) run

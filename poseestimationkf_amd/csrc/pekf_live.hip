@@ -46,11 +46,14 @@ namespace pekf {
 #ifndef PEKF_LIVE_QUEUE64
 #define PEKF_LIVE_QUEUE64 5  // the same with FP64 acc / mag (64 B each): 20 KB of LDS per wave, all of it
 #endif
+#ifndef PEKF_LIVE_QUEUE_EV64
+#define PEKF_LIVE_QUEUE_EV64 4  // FP64 events: all-FP64 records (80 B each), 20 KB of LDS per wave
+#endif
 #ifndef PEKF_LIVE_QUORUM
 #define PEKF_LIVE_QUORUM 56  // lanes of 64 with a queued record that trigger a filter step
 #endif
-#ifndef PEKF_LIVE_ATTR
-#define PEKF_LIVE_ATTR __attribute__((amdgpu_waves_per_eu(2)))
+#ifndef PEKF_LIVE_EV64_WAVES
+#define PEKF_LIVE_EV64_WAVES 1
 #endif
 
 // A lane's records waiting for the wave's next filter step, oldest first: a ring of Q slots per lane in
@@ -172,25 +175,76 @@ struct LdsQueue64 {
     }
 };
 
+// The queue of FP64-event launches: every field of the record in FP64 -- gyro and dt too, as the server's
+// filter gets them (dt any float64, so no escape) -- 80 B per slot as five double2 planes [slot][lane]
+// (16 B per lane and plane: conflict-free ds_*_b128), 4 deep = 20 KB per wave, the CU's 160 KB at 2
+// waves per SIMD.
+template <int Q>
+struct LdsQueueF64 {
+    static constexpr size_t kBytes = 5 * sizeof(double2) * Q * kRunBlock;
+    double2 (*v)[5][kRunBlock];  // {gx, gy}, {gz, dt}, {ax, ay}, {az, mx}, {my, mz}
+    int head = 0, n = 0;
+    __device__ __forceinline__ void bind(unsigned char *lds) { v = reinterpret_cast<double2(*)[5][kRunBlock]>(lds); }
+    __device__ __forceinline__ bool esc_queued() const { return false; }
+    __device__ __forceinline__ void push(const double4 &g, const V3 &a, const V3 &m) {
+        const int slot = head + n < Q ? head + n : head + n - Q;
+        v[slot][0][threadIdx.x] = make_double2(g.x, g.y);
+        v[slot][1][threadIdx.x] = make_double2(g.z, g.w);
+        v[slot][2][threadIdx.x] = make_double2(a.x, a.y);
+        v[slot][3][threadIdx.x] = make_double2(a.z, m.x);
+        v[slot][4][threadIdx.x] = make_double2(m.y, m.z);
+        ++n;
+    }
+    struct Slot {
+        double2 v[5];
+    };
+    __device__ __forceinline__ Slot pop(double &dtv) {
+        Slot r;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) r.v[k] = v[head][k][threadIdx.x];
+        dtv = r.v[1].y;
+        if (n > 0) {
+            head = head + 1 < Q ? head + 1 : 0;
+            --n;
+        }
+        return r;
+    }
+    static __device__ __forceinline__ void unpack(const Slot &r, double (&gy)[3], double (&acc)[3], double (&mag)[3]) {
+        gy[0] = r.v[0].x; gy[1] = r.v[0].y; gy[2] = r.v[1].x;
+        acc[0] = r.v[2].x; acc[1] = r.v[2].y; acc[2] = r.v[3].x;
+        mag[0] = r.v[3].y; mag[1] = r.v[4].x; mag[2] = r.v[4].y;
+    }
+    __device__ __forceinline__ void reload(double *a, double *m) const {
+        const int slot = head == 0 ? Q - 1 : head - 1;
+        const double2 v2 = v[slot][2][threadIdx.x], v3 = v[slot][3][threadIdx.x], v4 = v[slot][4][threadIdx.x];
+        a[0] = v2.x; a[1] = v2.y; a[2] = v3.x;
+        m[0] = v3.y; m[1] = v4.x; m[2] = v4.y;
+    }
+};
+
 // TE: the event planes may hold time events (Phase3::event).  R64: records keep their FP64 acc / mag
 // (LdsQueue64); otherwise they are the f32 stream records pekf_frontend_dev writes (LdsQueue).
-template <bool TE, bool R64>
-__global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
-    int64_t batch, int64_t n_events, const float4 *__restrict__ ev, const double *__restrict__ init,
-    const int64_t *__restrict__ t_init, double alpha, double qs, double rs, double *__restrict__ Xio,
-    double *__restrict__ Pio, int32_t *__restrict__ counts, double *__restrict__ refs) {
+// EV64: FP64 events (PEKF_EV_F64_EVENTS, double4 planes: the server's own sample values), records all
+// FP64 (LdsQueueF64); TE and R64 do not apply.
+template <bool TE, bool R64, bool EV64 = false>
+__global__ __launch_bounds__(kRunBlock) __attribute__((amdgpu_waves_per_eu(EV64 ? PEKF_LIVE_EV64_WAVES : 2))) void k_live(
+    int64_t batch, int64_t n_events, const std::conditional_t<EV64, double4, float4> *__restrict__ ev,
+    const double *__restrict__ init, const int64_t *__restrict__ t_init, double alpha, double qs, double rs,
+    double *__restrict__ Xio, double *__restrict__ Pio, int32_t *__restrict__ counts, double *__restrict__ refs) {
+    using EvT = std::conditional_t<EV64, double4, float4>;
     constexpr int kRing = PEKF_LIVE_RING, kFlush = 3, kQuorum = PEKF_LIVE_QUORUM;
-    constexpr int kQueue = R64 ? PEKF_LIVE_QUEUE64 : PEKF_LIVE_QUEUE;
+    constexpr int kQueue = EV64 ? PEKF_LIVE_QUEUE_EV64 : R64 ? PEKF_LIVE_QUEUE64 : PEKF_LIVE_QUEUE;
     constexpr int kPush = kRing / kFlush;  // records a lane can complete within one block
     static_assert(kRing % kFlush == 0, "the ring depth must be a multiple of the emit period");
     static_assert(kQueue >= kPush, "the queue must hold a block's records");
+    static_assert(!(EV64 && (TE || R64)), "FP64 events take their own record queue and carry their times");
     // LdsQueue64 keeps ONE escaped dt per lane (esc_dt) and want_step drains it before the next block,
     // which is safe only while a block completes at most one record per lane
     static_assert(!R64 || kPush == 1, "LdsQueue64's single escaped-dt register needs one record per lane per block");
     const int64_t b = (int64_t)blockIdx.x * kRunBlock + threadIdx.x;
     if (b >= batch) return;
 
-    Phase3 fe;
+    Phase3T<std::conditional_t<EV64, V3, F3>> fe;
     fe.start(init + 6 * b, t_init[b], alpha);
     // a filter that never finished phase 2 (non-finite init: pekf_frontend_init_dev's "not ready")
     // applies no record: its state is left as it was and counts[b] = 0
@@ -216,7 +270,8 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
     }
     const StepK<double> kc = step_consts<double, true>(qs, rs);
 
-    using Queue = std::conditional_t<R64, LdsQueue64<kQueue>, LdsQueue<kQueue>>;
+    using Queue = std::conditional_t<EV64, LdsQueueF64<kQueue>,
+                                     std::conditional_t<R64, LdsQueue64<kQueue>, LdsQueue<kQueue>>>;
     __shared__ __attribute__((aligned(16))) unsigned char q_lds[Queue::kBytes];
     Queue queue;
     queue.bind(q_lds);
@@ -244,9 +299,12 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
         mode.leave();
     };
     // the pending record (captured by Phase3::event) into the queue
-    auto push_pending = [&](const RawRec &q) {
+    auto push_pending = [&](const auto &q) {
         bool esc;
-        if constexpr (R64) {
+        if constexpr (EV64) {
+            const double4 g = fe.emit64(q);
+            if (ready) queue.push(g, fe.lpf_acc, fe.lpf_mag);
+        } else if constexpr (R64) {
             const float4 g = fe.emit_lpf(q, esc);
             if (ready) queue.push(g, fe.lpf_acc, fe.lpf_mag, esc, q.dt);
         } else {
@@ -254,7 +312,12 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
             if (ready) queue.push(rc, esc, q.dt);
         }
     };
-    auto on_event = [&](const float4 v4) { fe.event<TE>(v4); };
+    auto on_event = [&](const EvT &v4) {
+        if constexpr (EV64)
+            fe.event64(v4);
+        else
+            fe.template event<TE>(v4);
+    };
     auto flush = [&]() {
         if (fe.pend) {
             fe.pend = false;
@@ -268,12 +331,19 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
     // then scalar compares, where 64-bit ones took a VALU move and compare each, twice per event.
     const uint32_t lane = (uint32_t)b;
     const int32_t n_ev = (int32_t)n_events;
-    auto load = [&](int32_t e) -> float4 {
+    auto load = [&](int32_t e) -> EvT {
         const int32_t row = e < n_ev ? e : n_ev - 1;
 #if PEKF_LIVE_NTL
-        typedef float nv4 __attribute__((ext_vector_type(4)));
-        const nv4 v = __builtin_nontemporal_load((const nv4 *)(ev + (int64_t)row * batch + lane));
-        return make_float4(v.x, v.y, v.z, v.w);
+        if constexpr (EV64) {
+            typedef double nd2 __attribute__((ext_vector_type(2)));
+            const nd2 *q = (const nd2 *)(ev + (int64_t)row * batch + lane);
+            const nd2 lo = __builtin_nontemporal_load(q), hi = __builtin_nontemporal_load(q + 1);
+            return make_double4(lo.x, lo.y, hi.x, hi.y);
+        } else {
+            typedef float nv4 __attribute__((ext_vector_type(4)));
+            const nv4 v = __builtin_nontemporal_load((const nv4 *)(ev + (int64_t)row * batch + lane));
+            return make_float4(v.x, v.y, v.z, v.w);
+        }
 #else
         return (ev + (int64_t)row * batch)[lane];
 #endif
@@ -284,7 +354,7 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
     auto want_step = [&](bool last) {
         const uint64_t queued = __ballot(queue.n > 0);
         return queued != 0 && (last || __any(queue.n > kQueue - kPush) || __popcll(queued) >= kQuorum ||
-                               (R64 && __any(queue.esc_queued())));
+                               (R64 && !EV64 && __any(queue.esc_queued())));
     };
     auto steps = [&](bool last) {
         // tested before the loop, so a block that runs no step does not pass the loop's header
@@ -295,7 +365,7 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
         }
     };
     if (n_ev > 0) {
-        float4 ring[kRing];
+        EvT ring[kRing];
 #pragma unroll
         for (int k = 0; k < kRing; ++k) ring[k] = load(k);
         // No exit inside the unrolled body (one per event made the compiler copy the ring on the back
@@ -306,11 +376,16 @@ __global__ __launch_bounds__(kRunBlock) PEKF_LIVE_ATTR void k_live(
             if (e0 + kRing > n_ev) {  // uniform, once per launch
 #pragma unroll
                 for (int k = 0; k < kRing; ++k)
-                    if (e0 + k >= n_ev) ring[k] = make_float4(0.f, 0.f, 0.f, __uint_as_float(PEKF_EV_TIME));
+                    if (e0 + k >= n_ev) {
+                        if constexpr (EV64)
+                            ring[k] = ev64_null();
+                        else
+                            ring[k] = make_float4(0.f, 0.f, 0.f, __uint_as_float(PEKF_EV_TIME));
+                    }
             }
 #pragma unroll
             for (int k = 0; k < kRing; ++k) {
-                const float4 v4 = ring[k];
+                const EvT v4 = ring[k];
                 ring[k] = load(e0 + k + kRing);
                 on_event(v4);
                 if ((k + 1) % kFlush == 0) flush();
@@ -332,7 +407,10 @@ extern "C" int pekf_live_ext_dev(int64_t batch, int64_t n_events, const void *ev
                                  const int64_t *t_init, double alpha, double *X, double *P, double q, double r,
                                  int32_t *counts, double *refs, uint32_t flags, int *dev_error, void *stream) {
     PEKF_CHECK_ARG(batch >= 0 && n_events >= 0, "negative size");
-    PEKF_CHECK_ARG((flags & ~(PEKF_EV_TIME_EVENTS | PEKF_EV_F32_RECORDS)) == 0, "unknown flags");
+    PEKF_CHECK_ARG((flags & ~(PEKF_EV_TIME_EVENTS | PEKF_EV_F32_RECORDS | PEKF_EV_F64_EVENTS)) == 0, "unknown flags");
+    const bool ev64 = (flags & PEKF_EV_F64_EVENTS) != 0;
+    PEKF_CHECK_ARG(!ev64 || (flags & (PEKF_EV_TIME_EVENTS | PEKF_EV_F32_RECORDS)) == 0,
+                   "PEKF_EV_F64_EVENTS takes no other flag (FP64 events carry their times; their records are FP64)");
     if (batch == 0) return PEKF_OK;
     PEKF_CHECK_ARG(batch < ((int64_t)1 << 28), "batch must be < 2^28 filters per launch");
     PEKF_CHECK_ARG(n_events < ((int64_t)1 << 30), "n_events must be < 2^30 per launch");
@@ -347,7 +425,10 @@ extern "C" int pekf_live_ext_dev(int64_t batch, int64_t n_events, const void *ev
         hipLaunchKernelGGL(kernel, grid, block, 0, as_stream(stream), batch, n_events, ev, init, t_init, alpha, q, r, X,
                            P, counts, refs);
     };
-    if (te)
+    if (ev64)
+        hipLaunchKernelGGL((k_live<false, false, true>), grid, block, 0, as_stream(stream), batch, n_events,
+                           static_cast<const double4 *>(ev_planes), init, t_init, alpha, q, r, X, P, counts, refs);
+    else if (te)
         r64 ? launch(k_live<true, true>) : launch(k_live<true, false>);
     else
         r64 ? launch(k_live<false, true>) : launch(k_live<false, false>);

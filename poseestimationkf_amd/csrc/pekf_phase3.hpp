@@ -12,6 +12,13 @@
 // outputs in FP64 instead (emit_lpf + lpf_acc / lpf_mag), as the server hands them to its filter.  The arithmetic is contracted as the compiler's default
 // (fp contract fast) whatever the including file is compiled with: every function with arithmetic
 // opens with that pragma, so k_live's records are k_frontend's.
+//
+// Two event forms (Phase3T<S>): f32 events (S = F3, 16 B: float4 {x, y, z, bits(gap << 2 | type)}) and
+// FP64 events (S = V3, 32 B: double4 {x, y, z, bits(t) | type}, PEKF_EV_F64_EVENTS).  The server parses
+// each sample from the phone's text with std::stod (Parser.cpp:23-25) -- the double nearest the
+// decimal Float.toString printed (MessageSender.java:222-227), in general not the f32 itself -- so only
+// the FP64 form carries the server's own input values; the state machine and the record arithmetic are
+// the same code for both.
 #pragma once
 
 #include "pekf_internal.hpp"
@@ -42,6 +49,7 @@ struct F3 {
     float x, y, z;
 };
 __device__ __forceinline__ V3 widen(const F3 &f) { return {f.x, f.y, f.z}; }
+__device__ __forceinline__ V3 widen(const V3 &v) { return v; }
 // component-wise c ? a : b (a struct-valued ?: would go through scratch memory)
 __device__ __forceinline__ V3 sel(bool c, const V3 &a, const V3 &b) {
     return {c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z};
@@ -61,28 +69,76 @@ __device__ __forceinline__ V3 normalised(const V3 &v) {
 // once) and turned into the record by Phase3::emit: the gyro sample, acc_0 / acc_1 / mag_0 / mag_1
 // (f32 samples; *_mean: acc_0 / mag_0 is still the phase-2 mean) and the time differences of
 // LinearInterpolationSensor and of the record's dt.
-struct RawRec {
-    F3 gyro, acc0, acc1, mag0, mag1;
+template <typename S>
+struct RawRecT {
+    S gyro, acc0, acc1, mag0, mag1;
     bool acc0_mean, mag0_mean;
     double dt, an, ad, mn, md;  // dt, acc / mag lerp num and den
 };
+using RawRec = RawRecT<F3>;
 
-// Samples are f32 values, so the state machine moves them as f32 (one select per component instead
-// of two, no conversions per event); they are widened only when a record is emitted.  acc_0 / mag_0
-// start as the phase-2 means (FP64, not f32 values): a flag says a slot still holds the mean.
-struct Phase3 {
+// An FP64 event {x, y, z, w}: w's bits are those of the event's time in ns as a float64 (an integer of
+// magnitude < 2^51, so its two lowest mantissa bits are zero) with the type in those two bits (3: no
+// sample, e.g. padding).  Absolute times: any gap or clock step is just the next event's time.
+__device__ __forceinline__ uint32_t ev64_type(const double4 &e) {
+    return (uint32_t)__double_as_longlong(e.w) & 3u;
+}
+__device__ __forceinline__ double ev64_time(const double4 &e) {
+    return __longlong_as_double(__double_as_longlong(e.w) & ~3ll);
+}
+// the padding event (type 3 at time 0: moves nothing)
+__device__ __forceinline__ double4 ev64_null() { return make_double4(0.0, 0.0, 0.0, __longlong_as_double(3ll)); }
+
+// The padding event of either form: f32 -- a zero-step time event {0, 0, 0, word 3}; FP64 -- ev64_null.
+template <typename EvT>
+__device__ __forceinline__ EvT null_event() {
+    if constexpr (std::is_same<EvT, double4>::value)
+        return ev64_null();
+    else
+        return make_float4(0.f, 0.f, 0.f, __uint_as_float(PEKF_EV_TIME));
+}
+
+// One event of a plane, non-temporal (NT: each event is read once per pass) or plain.
+template <bool NT>
+__device__ __forceinline__ float4 load_event(const float4 *q) {
+    if constexpr (NT) {
+        typedef float nv4 __attribute__((ext_vector_type(4)));
+        const nv4 v = __builtin_nontemporal_load((const nv4 *)q);
+        return make_float4(v.x, v.y, v.z, v.w);
+    } else {
+        return *q;
+    }
+}
+template <bool NT>
+__device__ __forceinline__ double4 load_event(const double4 *q) {
+    if constexpr (NT) {
+        typedef double nd2 __attribute__((ext_vector_type(2)));
+        const nd2 lo = __builtin_nontemporal_load((const nd2 *)q), hi = __builtin_nontemporal_load((const nd2 *)q + 1);
+        return make_double4(lo.x, lo.y, hi.x, hi.y);
+    } else {
+        return *q;
+    }
+}
+
+// With f32 events (S = F3) the state machine moves samples as f32 (one select per component instead
+// of two, no conversions per event); they are widened only when a record is emitted.  With FP64 events
+// (S = V3) they are the server's doubles throughout.  acc_0 / mag_0 start as the phase-2 means (FP64,
+// not samples): a flag says a slot still holds the mean.
+template <typename S>
+struct Phase3T {
+    using Raw = RawRecT<S>;
     // phase-2 state: acc_0 / mag_0 = raw means at the initialisation time (Parser.cpp:44-53)
     V3 mean_acc, mean_mag;
-    F3 acc0, mag0;
+    S acc0, mag0;
     bool acc0_mean, mag0_mean;  // acc_0 / mag_0 is still the phase-2 mean
-    double t_acc0, t_mag0, prev_t, t;
+    double t_acc0, t_mag0, prev_t, t;  // t: the f32 events' running clock (FP64 events carry their time)
     // The latest acc / mag sample and its time.  The Parser's acc_1 / mag_1 is always the latest sample
     // while it is set (it is written by every sample after the gyro, and nothing else moves until the
     // record completes or the next gyro shifts it to acc_0 / mag_0), so it is not held separately: each
     // event updates the latest sample once and acc_0 / mag_0 copy it when the Parser would, 10 VALU
     // per event fewer than moving acc_1 / mag_1 and acc_0 / mag_0 through two selects each.
-    F3 acc1, mag1;
-    F3 gyro;
+    S acc1, mag1;
+    S gyro;
     double t_acc1, t_mag1, t_gyro;
     bool gyro_set, acc1_set, mag1_set;
     V3 lpf_acc, lpf_mag;
@@ -96,7 +152,7 @@ struct Phase3 {
     // acc, mag) between two records, so when emit runs every 3 events it never has two pending.
     // Arithmetic is unchanged: the time differences are formed at capture, exactly as lerp_to would.
     bool pend;
-    RawRec p;
+    Raw p;
 
     __device__ __forceinline__ void start(const double *init6, int64_t t_start, double a) {
         mean_acc = {init6[0], init6[1], init6[2]};
@@ -125,11 +181,8 @@ struct Phase3 {
 
     // One event {x, y, z, bits(word)}: the word carries the type and the ns gap to the previous event.
     // Parser::WriteKalmanFilterMeasurement (Parser.cpp:148-219), branch-free: each state variable is
-    // one select, so nothing is copied between divergent paths.
-    //   before a gyro sample: acc -> acc_0, mag -> mag_0, gyro -> gyro (gyro_is_set);
-    //   after it: acc -> acc_1, mag -> mag_1 (set); a new gyro replaces the gyro and shifts a set
-    //   acc_1 -> acc_0 / mag_1 -> mag_0, clearing both flags.
-    // on_done(const RawRec &) runs for a lane whose event completes a record.
+    // one select, so nothing is copied between divergent paths (step).
+    // on_done(const Raw &) runs for a lane whose event completes a record.
     // TE: the stream may hold time events (word == PEKF_EV_TIME: no sample, the clock moves by the
     // float64 in the x / y bits -- a pause of 2^30 ns or more, or a clock stepping back); without TE
     // such an event moves nothing.  Either way type 3 matches no sensor, so the state machine skips it.
@@ -142,15 +195,28 @@ struct Phase3 {
             t += word == PEKF_EV_TIME ? time_step(v4) : (double)(word >> 2);
         else
             t += (double)(word >> 2);
+        step(S{v4.x, v4.y, v4.z}, ty, t, on_done);
+    }
+    // One FP64 event {x, y, z, bits(t) | type} (PEKF_EV_F64_EVENTS): the sample is the server's double.
+    template <typename F>
+    __device__ __forceinline__ void event64(const double4 &e, F &&on_done) {
+        step(S{e.x, e.y, e.z}, ev64_type(e), ev64_time(e), on_done);
+    }
+
+    // The state machine for a sample v of type ty at time tn:
+    //   before a gyro sample: acc -> acc_0, mag -> mag_0, gyro -> gyro (gyro_is_set);
+    //   after it: acc -> acc_1, mag -> mag_1 (set); a new gyro replaces the gyro and shifts a set
+    //   acc_1 -> acc_0 / mag_1 -> mag_0, clearing both flags.
+    template <typename F>
+    __device__ __forceinline__ void step(const S &v, const uint32_t ty, const double tn, F &&on_done) {
         const bool isA = ty == kEvAcc, isM = ty == kEvMag, isG = ty == kEvGyro;
         const bool gs = gyro_set;
-        const F3 v = {v4.x, v4.y, v4.z};
         const bool wA1 = isA && gs, wM1 = isM && gs;
         // acc1 / mag1: the latest sample (equal to the Parser's acc_1 / mag_1 whenever that is set)
         acc1 = sel(isA, v, acc1);
-        t_acc1 = isA ? t : t_acc1;
+        t_acc1 = isA ? tn : t_acc1;
         mag1 = sel(isM, v, mag1);
-        t_mag1 = isM ? t : t_mag1;
+        t_mag1 = isM ? tn : t_mag1;
         const bool a1s = wA1 || (acc1_set && !(isG && gs)), m1s = wM1 || (mag1_set && !(isG && gs));
         const bool sA = isG && gs && acc1_set, sM = isG && gs && mag1_set;  // gyro shift
         // ExecuteKalmanFilter (Parser.cpp:229-257) once acc_1 and mag_1 are both set: record its
@@ -158,7 +224,7 @@ struct Phase3 {
         const bool done = a1s && m1s;
         if (done) {
             asm volatile("");  // keeps this a branch: masked 64-bit moves, not two selects per double
-            RawRec r;
+            Raw r;
             r.gyro = gyro; r.dt = t_gyro - prev_t;
             r.acc0 = acc0; r.acc0_mean = acc0_mean; r.acc1 = acc1; r.an = t_gyro - t_acc0; r.ad = t_acc1 - t_acc0;
             r.mag0 = mag0; r.mag0_mean = mag0_mean; r.mag1 = mag1; r.mn = t_gyro - t_mag0; r.md = t_mag1 - t_mag0;
@@ -174,7 +240,7 @@ struct Phase3 {
         mag0_mean = mag0_mean && !cM;
         t_mag0 = cM ? t_mag1 : t_mag0;
         gyro = sel(isG, v, gyro);
-        t_gyro = isG ? t : t_gyro;
+        t_gyro = isG ? tn : t_gyro;
         gyro_set = (gs || isG) && !done;
         acc1_set = a1s && !done;
         mag1_set = m1s && !done;
@@ -183,7 +249,13 @@ struct Phase3 {
     // the deferring form: the completed record's inputs wait in p (pend) for emit(esc)
     template <bool TE = false>
     __device__ __forceinline__ void event(const float4 v4) {
-        event<TE>(v4, [&](const RawRec &r) {
+        event<TE>(v4, [&](const Raw &r) {
+            pend = true;
+            p = r;
+        });
+    }
+    __device__ __forceinline__ void event64(const double4 &e) {
+        event64(e, [&](const Raw &r) {
             pend = true;
             p = r;
         });
@@ -209,10 +281,8 @@ struct Phase3 {
     }
 
     // A captured record, in the order they complete: interpolation, normalisation, low-pass (the FP64
-    // results stay in lpf_acc / lpf_mag), and the gyro / dt half of the record, which is returned.
-    // esc: its dt does not fit the dt word (not in [0, 2^31 - 1) ns): the word is PEKF_DT_ESCAPE and
-    // the caller keeps q.dt beside the record (pekf.h).
-    __device__ __forceinline__ float4 emit_lpf(const RawRec &q, bool &esc) {
+    // results stay in lpf_acc / lpf_mag).
+    __device__ __forceinline__ void lpf_record(const Raw &q) {
 #pragma clang fp contract(fast)
         // Parser::LinearInterpolationSensor (:259-267): (y2 - y1) / (t2 - t1) * (t3 - t1) + y1, the
         // division taken as one reciprocal.  Timestamps are integer ns held in doubles (exact below
@@ -230,13 +300,31 @@ struct Phase3 {
         const V3 m = normalised({(m1.x - m0.x) * fm + m0.x, (m1.y - m0.y) * fm + m0.y, (m1.z - m0.z) * fm + m0.z});
         lpf_step(lpf_mag.x, m.x); lpf_step(lpf_mag.y, m.y); lpf_step(lpf_mag.z, m.z);
         lpf_step(lpf_acc.x, a.x); lpf_step(lpf_acc.y, a.y); lpf_step(lpf_acc.z, a.z);
+    }
+
+    // lpf_record, and the gyro / dt half of the 40 B record, which is returned (f32 events).
+    // esc: its dt does not fit the dt word (not in [0, 2^31 - 1) ns): the word is PEKF_DT_ESCAPE and
+    // the caller keeps q.dt beside the record (pekf.h).
+    __device__ __forceinline__ float4 emit_lpf(const Raw &q, bool &esc) {
+        lpf_record(q);
         esc = !(q.dt >= 0.0 && q.dt < (double)PEKF_DT_ESCAPE);
         return make_float4((float)q.gyro.x, (float)q.gyro.y, (float)q.gyro.z,
                            __uint_as_float(esc ? PEKF_DT_ESCAPE : (uint32_t)q.dt));
     }
 
+    // lpf_record, and the record's gyro and dt in FP64 (FP64 events: {gx, gy, gz, dt_ns}, the GD half of
+    // an 80 B record; the dt is any float64, so nothing is escaped).
+    __device__ __forceinline__ double4 emit64(const Raw &q) {
+        lpf_record(q);
+        return make_double4(q.gyro.x, q.gyro.y, q.gyro.z, q.dt);
+    }
+    __device__ __forceinline__ double4 emit64() {
+        pend = false;
+        return emit64(p);
+    }
+
     // The 40 B stream record (acc / mag rounded to f32, as every record of the stream planes).
-    __device__ __forceinline__ Rec emit(const RawRec &q, bool &esc) {
+    __device__ __forceinline__ Rec emit(const Raw &q, bool &esc) {
         Rec r;
         r.gd = emit_lpf(q, esc);
         r.am = make_float4((float)lpf_acc.x, (float)lpf_acc.y, (float)lpf_acc.z, (float)lpf_mag.x);
@@ -244,5 +332,7 @@ struct Phase3 {
         return r;
     }
 };
+using Phase3 = Phase3T<F3>;    // f32 events
+using Phase3_64 = Phase3T<V3>; // FP64 events (the server's stod values)
 
 }  // namespace pekf

@@ -19,11 +19,6 @@
 
 namespace pekf {
 
-struct Rec64 {
-    double4 gd, am;
-    double2 my;
-};
-
 // k_run's RowCursor for the 80 B record: rows of batch x 32 B (gd, am) and batch x 16 B (my), read
 // through buffer descriptors of a chunk of rows with the row's offset in the scalar offset, so the
 // next row is two scalar adds and a compare and no vector address arithmetic is kept per record

@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 from . import synth
-from ._lib import EV_F32_RECORDS, EV_TIME_EVENTS, RUN_MIXED_PRECISION, RUN_STATE_SOA, check, dptr, f64, lib
+from ._lib import (EV_F32_RECORDS, EV_F64_EVENTS, EV_TIME_EVENTS, RUN_MIXED_PRECISION, RUN_STATE_SOA, check, dptr,
+                   f64, lib)
 
 
 # ------------------------------------------------------------------ device plumbing
@@ -332,6 +333,16 @@ class RecordWindow64:
         win.counts = np.minimum(lens, W).astype(np.int32)
         return win
 
+    def download_filters(self, cols):
+        """The records of filter columns `cols` as float64 arrays: (gyro (W, n, 3), dt_ns (W, n), acc (W, n, 3),
+        mag (W, n, 3), refs (n, 6))."""
+        cols = np.asarray(cols)
+        gd = self.gd.download((self.window, self.batch, 4), np.float64)[:, cols]
+        am = self.am.download((self.window, self.batch, 4), np.float64)[:, cols]
+        my = self.my.download((self.window, self.batch, 2), np.float64)[:, cols]
+        refs = self.refs.download((self.batch, 6), np.float64)[cols]
+        return gd[..., :3], gd[..., 3], am[..., :3], np.concatenate([am[..., 3:4], my], axis=-1), refs
+
     def wahba_quaternions(self, n_steps=None, step0=0, k_acc=0.5, k_mag=0.5):
         """Pure-Wahba attitude of every record with fixed weights (main_file.py:40): (n_steps, batch, 4)."""
         n_steps = self.window if n_steps is None else int(n_steps)
@@ -357,30 +368,61 @@ class RecordWindow64:
 
 # ------------------------------------------------------------------ server front-end (raw events)
 
-def _event_planes(ev):
-    """(device event planes, n_events, flags): synth.pack_events (time events inserted for gaps the
-    30-bit field cannot hold), uploaded; flags = PEKF_EV_TIME_EVENTS when the planes hold any."""
+EVENT_FORMS = ("f32", "f64")
+
+
+def server_event_values(ev):
+    """The sample values the server computes with: ev["values64"] when the events came as wire text
+    (wire.events_from_wire: the server's own std::stod parse), else the doubles it would parse from
+    the phone's Float.toString of ev["values"] (wire.server_values)."""
+    from . import wire
+    return np.asarray(ev["values64"], np.float64) if "values64" in ev else wire.server_values(ev["values"])
+
+
+def _event_planes(ev, events="f32"):
+    """(device event planes, n_events, flags).  events="f32": synth.pack_events (16 B, the float32
+    samples; time events inserted for gaps the 30-bit field cannot hold), flags = PEKF_EV_TIME_EVENTS when
+    the planes hold any.  events="f64": synth.pack_events64 of the server's values (32 B,
+    server_event_values), flags = PEKF_EV_F64_EVENTS."""
+    if events not in EVENT_FORMS:
+        raise ValueError("events must be 'f32' or 'f64'")
+    if events == "f64":
+        planes = synth.pack_events64(ev, server_event_values(ev))
+        return DeviceBuffer(planes.nbytes).upload(planes), planes.shape[0], EV_F64_EVENTS
     planes = synth.pack_events(ev)
     return (DeviceBuffer(planes.nbytes).upload(planes), planes.shape[0],
             EV_TIME_EVENTS if synth.has_time_events(planes) else 0)
 
 
-def run_frontend(ev, alpha=0.1, r_max=None):
-    """Raw phone events (synth.generate_events layout) -> (IMUWindow of records, counts (K,) int32).
+def run_frontend(ev, alpha=0.1, r_max=None, events="f32"):
+    """Raw phone events (synth.generate_events layout) -> (window of records, counts (K,) int32).
 
     Runs pekf_frontend_ext_dev.  Every record needs a gyro, an accelerometer and a
-    magnetometer event, so r_max defaults to n_events // 3 + 1.  Event gaps of any size go through
+    magnetometer event, so r_max defaults to n_events // 3 + 1.  Raises if a filter overflows r_max.
+    events="f32": float32 samples -> an IMUWindow of 40 B records; event gaps of any size go through
     time events, and records whose dt does not fit the dt word through the window's dt side plane
-    (win.dtx, kept only if some record needed it).  Raises if a filter overflows r_max."""
+    (win.dtx, kept only if some record needed it).  events="f64": the server's own sample values
+    (server_event_values) -> a RecordWindow64 of FP64 records, every field FP64 (pekf_run_rec64_dev's
+    input), any dt."""
     K = np.asarray(ev["types"]).shape[1]
     E0 = np.asarray(ev["types"]).shape[0]
-    evb, E, flags = _event_planes(ev)
+    evb, E, flags = _event_planes(ev, events)
     r_max = E0 // 3 + 1 if r_max is None else int(r_max)
     init = DeviceBuffer(48 * K).upload(np.concatenate([ev["init_acc"], ev["init_mag"]], axis=1).astype(np.float64))
     tib = DeviceBuffer(8 * K).upload(np.ascontiguousarray(ev["t_init"], np.int64))
-    win = IMUWindow(K, max(1, r_max))
     cnt = DeviceBuffer(4 * K)
     errb = DeviceBuffer(4)
+    if events == "f64":
+        win = RecordWindow64(K, max(1, r_max))
+        errb.upload(np.zeros(1, np.int32))
+        check(lib.pekf_frontend_ext_dev(K, E, evb.ptr, init.ptr, tib.ptr, float(alpha), r_max, win.gd.ptr,
+                                        win.am.ptr, win.my.ptr, None, cnt.ptr, win.refs.ptr, flags, errb.ptr, None))
+        check(lib.pekf_device_sync())
+        if int(errb.download((1,), np.int32)[0]) & 2:
+            raise ValueError("more than r_max=%d records for some filter" % r_max)
+        win.counts = cnt.download((K,), np.int32)
+        return win, win.counts
+    win = IMUWindow(K, max(1, r_max))
     dtx = None
     while True:
         # without a side plane first; only if some record's dt does not fit the dt word (err bit 1: a
@@ -403,19 +445,20 @@ def run_frontend(ev, alpha=0.1, r_max=None):
     return win, win.counts
 
 
-def frontend_init(ev, n_avg=100, stats=True):
+def frontend_init(ev, n_avg=100, stats=True, events="f32"):
     """Phase-2 events (synth.generate_events layout; ev["t_init"] = the time before the first one) ->
     dict(init (K, 6) raw {acc, mag} means, t_init (K,) int64, ready (K,) bool, gyro_mean (K, 3),
-    var_acc / var_mag / var_gyro (K, 3)) by pekf_frontend_init_dev: the inputs run_frontend needs
+    var_acc / var_mag / var_gyro (K, 3)) by pekf_frontend_init_ext_dev: the inputs run_frontend needs
     for phase 3 (KFS/Parser.cpp:36-58,84-140, KFS/InitialValues.cpp).  stats=False: init / t_init /
-    ready only (the kernel then skips its second pass, the variances)."""
+    ready only (the kernel then skips its second pass, the variances).  events: as run_frontend ("f64":
+    the statistics of the server's own sample values)."""
     K = np.asarray(ev["types"]).shape[1]
-    evb, E, _ = _event_planes(ev)   # phase 2 always honours time events
+    evb, E, flags = _event_planes(ev, events)   # phase 2 always honours time events
     tsb = DeviceBuffer(8 * K).upload(np.ascontiguousarray(ev["t_init"], np.int64))
     ib, tib, rb = DeviceBuffer(48 * K), DeviceBuffer(8 * K), DeviceBuffer(4 * K)
     sb = DeviceBuffer(96 * K) if stats else None
-    check(lib.pekf_frontend_init_dev(K, E, evb.ptr, tsb.ptr, int(n_avg), ib.ptr, tib.ptr,
-                                     sb.ptr if stats else None, rb.ptr, None))
+    check(lib.pekf_frontend_init_ext_dev(K, E, evb.ptr, tsb.ptr, int(n_avg), ib.ptr, tib.ptr,
+                                         sb.ptr if stats else None, rb.ptr, flags & EV_F64_EVENTS, None))
     check(lib.pekf_device_sync())
     out = dict(init=ib.download((K, 6), np.float64), t_init=tib.download((K,), np.int64),
                ready=rb.download((K,), np.int32).astype(bool))
@@ -425,20 +468,24 @@ def frontend_init(ev, n_avg=100, stats=True):
     return out
 
 
-def _record_flags(records):
+def _record_flags(records, events="f32"):
     """pekf_live_ext_dev's record precision: "f64" (the low-pass acc / mag as the server's filter gets them,
-    KFS/KalmanFilter.cpp:279-303) or "f32" (the 40 B stream record, as the split pipeline's)."""
+    KFS/KalmanFilter.cpp:279-303) or "f32" (the 40 B stream record, as the split pipeline's).  FP64 events
+    always make FP64 records."""
     if records not in ("f64", "f32"):
         raise ValueError("records must be 'f64' or 'f32'")
+    if events == "f64" and records != "f64":
+        raise ValueError("FP64 events make FP64 records (records='f64')")
     return EV_F32_RECORDS if records == "f32" else 0
 
 
-def run_session(phase2, phase3, filters, n_avg=100, alpha=0.1, records="f64"):
+def run_session(phase2, phase3, filters, n_avg=100, alpha=0.1, records="f64", events="f32"):
     """A whole client session of the server on the device (KFS/Parser.cpp:28-72): phase-2 events ->
     initial means and start time (pekf_frontend_init_dev) -> phase-3 events -> records -> the filters'
     state (pekf_live_dev), the phase-2 results handed over in device memory.  phase3's times continue
     phase2's (its first gap is taken from phase2's last event, the time phase 3 starts from).
-    filters: a BatchedEKF (FP64, AoS) whose state is advanced; records as BatchedEKF.run_events.
+    filters: a BatchedEKF (FP64, AoS) whose state is advanced; records and events as
+    BatchedEKF.run_events.
     Returns dict(ready (K,) bool -- a filter
     that never finished phase 2 has NaN references, applies no record and keeps its state --, counts
     (K,) records applied, refs (K, 6))."""
@@ -446,13 +493,14 @@ def run_session(phase2, phase3, filters, n_avg=100, alpha=0.1, records="f64"):
     assert np.asarray(phase2["types"]).shape[1] == K and np.asarray(phase2["types"]).shape[0] > 0
     assert np.asarray(phase3["types"]).shape[1] == K
     t_last = np.asarray(phase2["times"], np.int64)[-1]
-    ev2, E2, _ = _event_planes(phase2)
-    ev3, E3, flags3 = _event_planes(dict(phase3, t_init=t_last))
+    ev2, E2, flags2 = _event_planes(phase2, events)
+    ev3, E3, flags3 = _event_planes(dict(phase3, t_init=t_last), events)
     tsb = DeviceBuffer(8 * K).upload(np.ascontiguousarray(phase2["t_init"], np.int64))
     ib, tib, rb = DeviceBuffer(48 * K), DeviceBuffer(8 * K), DeviceBuffer(4 * K)
-    check(lib.pekf_frontend_init_dev(K, E2, ev2.ptr, tsb.ptr, int(n_avg), ib.ptr, tib.ptr, None, rb.ptr, None))
+    check(lib.pekf_frontend_init_ext_dev(K, E2, ev2.ptr, tsb.ptr, int(n_avg), ib.ptr, tib.ptr, None, rb.ptr,
+                                         flags2 & EV_F64_EVENTS, None))
     cnt, refs = DeviceBuffer(4 * K), DeviceBuffer(48 * K)
-    filters.run_events_async(ev3, E3, ib, tib, cnt, refs, alpha, flags=flags3 | _record_flags(records))
+    filters.run_events_async(ev3, E3, ib, tib, cnt, refs, alpha, flags=flags3 | _record_flags(records, events))
     check(lib.pekf_device_sync())
     return dict(ready=rb.download((K,), np.int32).astype(bool), counts=cnt.download((K,), np.int32),
                 refs=refs.download((K, 6), np.float64))
@@ -568,20 +616,23 @@ class BatchedEKF:
                                     self.X.ptr, self.P.ptr, self.q, self.r, counts.ptr, refs.ptr, int(flags), None,
                                     stream))
 
-    def run_events(self, ev, alpha=0.1, records="f64"):
+    def run_events(self, ev, alpha=0.1, records="f64", events="f32"):
         """Raw phone events (synth.generate_events layout) -> front-end -> filter, fused in one launch
         (pekf_live_ext_dev).  Returns (counts (batch,) int32 records applied, refs (batch, 6)
         the filters' acc0 / mag0).  Any event gap and any record dt is applied (time events, escapes).
         records: "f64" (default) feeds the filter the FP64 low-pass acc / mag, as the server does
         (KFS/KalmanFilter.cpp:279-303); "f32" rounds them to the 40 B stream record first, which makes the
-        result equal run_frontend + run bit for bit."""
+        result equal run_frontend + run bit for bit.
+        events: "f32" the float32 samples (16 B events); "f64" the server's own values (32 B events,
+        server_event_values: what std::stod parses from the phone's text), every record field FP64 --
+        equal to run_frontend(events="f64") + run bit for bit."""
         assert np.asarray(ev["types"]).shape[1] == self.batch
-        evb, E, flags = _event_planes(ev)
+        evb, E, flags = _event_planes(ev, events)
         init = DeviceBuffer(48 * self.batch).upload(
             np.concatenate([ev["init_acc"], ev["init_mag"]], axis=1).astype(np.float64))
         tib = DeviceBuffer(8 * self.batch).upload(np.ascontiguousarray(ev["t_init"], np.int64))
         cnt, refs = DeviceBuffer(4 * self.batch), DeviceBuffer(48 * self.batch)
-        self.run_events_async(evb, E, init, tib, cnt, refs, alpha, flags=flags | _record_flags(records))
+        self.run_events_async(evb, E, init, tib, cnt, refs, alpha, flags=flags | _record_flags(records, events))
         check(lib.pekf_device_sync())
         return cnt.download((self.batch,), np.int32), refs.download((self.batch, 6), np.float64)
 

@@ -340,6 +340,31 @@ def pack_events(ev):
     return planes
 
 
+EV64_T_LIMIT = 1 << 51  # FP64 events: |t| < 2^51 ns keeps the two lowest mantissa bits of t free for the type
+
+
+def pack_events64(ev, values=None):
+    """generate_events-style dict -> the FP64 event plane (E, K, 4) float64 {x, y, z, w}
+    (PEKF_EV_F64_EVENTS, include/pekf.h): x, y, z the sample as float64 -- `values` if given, else
+    ev["values64"] if present (e.g. wire.parse's doubles), else ev["values"] widened -- and w's bits
+    those of the event's absolute time in ns as a float64 with the type in its two lowest bits.  32 B
+    per event; times are absolute, so no time events are needed for any gap or clock step."""
+    types = np.asarray(ev["types"], np.uint64)
+    times = np.asarray(ev["times"], np.int64)
+    if values is None:
+        values = ev["values64"] if "values64" in ev else ev["values"]
+    values = np.asarray(values, np.float64)
+    if times.size and int(np.abs(times).max()) >= EV64_T_LIMIT:
+        raise ValueError("FP64 events need |t| < 2^51 ns")
+    if types.size and int(types.max()) > 3:
+        raise ValueError("event types are 0 acc, 1 gyro, 2 mag, 3 none")
+    E, K = types.shape
+    planes = np.empty((E, K, 4), np.float64)
+    planes[..., :3] = values
+    planes[..., 3] = (times.astype(np.float64).view(np.uint64) | types).view(np.float64)
+    return planes
+
+
 def has_time_events(planes):
     """Whether an event plane holds time events (word == EV_TIME): the flag the phase-3 kernels need."""
     return bool((np.ascontiguousarray(planes[..., 3]).view(np.uint32) == EV_TIME).any())
@@ -361,4 +386,4 @@ def c1_timestamps(dt_ns, t0_ns=1_234_567_890_123):
 
 __all__ = ["DEFAULT_SEED", "SynthParams", "Records", "philox4x32", "reference_vectors", "generate",
            "pack_planes", "unpack_planes", "refs_array", "window_bytes", "c1_timestamps",
-           "MISSING_BIT", "DT_MASK", "DT_ESCAPE", "pack_events", "has_time_events", "EV_TIME"]
+           "MISSING_BIT", "DT_MASK", "DT_ESCAPE", "pack_events", "pack_events64", "has_time_events", "EV_TIME"]

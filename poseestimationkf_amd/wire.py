@@ -1,0 +1,118 @@
+"""The phone -> server link: the sample values the server computes with.
+
+The Android client sends every sample as text -- ``Float.toString`` of each value, in
+``"#<phase>,<type>:<x>,<y>,<z>,t:<ns>"`` padded with spaces to 99 characters
+(ASC/MessageSender.java:217-233, ConvertSensorMsg) -- and the server parses the values with
+``std::stod`` (KFS/Parser.cpp:12-26).  The server's filter therefore starts from the doubles nearest
+the printed decimals, not from the floats the phone measured (``"0.1"`` is 0.1, not
+0.100000001490116...).  The FP64 event planes (``PEKF_EV_F64_EVENTS``, include/pekf.h) carry exactly
+those doubles; this module produces them, natively (libpekf's host functions, csrc/pekf_wire.cpp):
+
+* :func:`parse` -- the server's own parse of wire text (``pekf_wire_parse``);
+* :func:`server_values` -- for samples known only as float32, the double the server would parse from
+  ``Float.toString(f)`` (``pekf_f32_wire_values``);
+* :func:`message` / :func:`events_text` -- the client's text for given samples (what the phone sends,
+  JDK 19+ ``Float.toString`` formatting), for feeding recorded or synthetic streams through the same
+  parse;
+* :func:`events_from_wire` -- per-filter wire streams -> the event dict the engine takes.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._lib import check, lib
+
+
+def server_values(values):
+    """float32 samples (any shape) -> float64: std::stod(Float.toString(f)) for each."""
+    f = np.ascontiguousarray(values, np.float32)
+    out = np.empty(f.shape, np.float64)
+    check(lib.pekf_f32_wire_values(f.size, f.ctypes.data, out.ctypes.data))
+    return out
+
+
+def parse(text):
+    """Wire text (str or bytes, one message per line) -> dict(phase (n,) uint8, types (n,) uint8,
+    values (n, 3) float64, times (n,) int64), as the server's Parser reads it."""
+    b = text.encode() if isinstance(text, str) else bytes(text)
+    n = ctypes.c_int64()
+    check(lib.pekf_wire_parse(b, len(b), 0, None, None, None, None, ctypes.byref(n)))
+    n = n.value
+    ph, ty = np.empty(n, np.uint8), np.empty(n, np.uint8)
+    xyz, t = np.empty((n, 3), np.float64), np.empty(n, np.int64)
+    check(lib.pekf_wire_parse(b, len(b), n, ph.ctypes.data, ty.ctypes.data, xyz.ctypes.data, t.ctypes.data,
+                              ctypes.byref(ctypes.c_int64())))
+    return dict(phase=ph, types=ty, values=xyz, times=t)
+
+
+def java_float_string(f):
+    """Float.toString(f) as JDK 19+ prints it: the shortest decimal that rounds to f, the closest among
+    those (one or two digits when one suffices), as "ddd.ddd" for 1e-3 <= |f| < 1e7, else "d.dddE[-]n"."""
+    f = np.float32(f)
+    if np.isnan(f):
+        return "NaN"
+    if np.isinf(f):
+        return "Infinity" if f > 0 else "-Infinity"
+    if f == 0:
+        return "-0.0" if np.signbit(f) else "0.0"
+    sci = np.format_float_scientific(f, unique=True, trim="-")       # shortest digits, e.g. "1.2345e-05"
+    mant, exp = sci.split("e")
+    if len(mant.lstrip("-").replace(".", "")) == 1:                   # one digit: the closest of one or two
+        mant, exp = ("%.1e" % float(f)).split("e")
+    neg = mant.startswith("-")
+    digits = mant.lstrip("-").replace(".", "").rstrip("0") or "0"
+    e = int(exp)
+    a = abs(float(f))
+    if 1e-3 <= a < 1e7:
+        if e >= 0:
+            ip = digits[:e + 1].ljust(e + 1, "0")
+            fp = digits[e + 1:] or "0"
+        else:
+            ip, fp = "0", "0" * (-e - 1) + digits
+        s = ip + "." + fp
+    else:
+        s = digits[0] + "." + (digits[1:] or "0") + "E" + str(e)
+    return ("-" if neg else "") + s
+
+
+def message(phase, sensor_type, xyz, t_ns):
+    """One client message (ConvertSensorMsg, MessageSender.java:217-233): "#p,t:x,y,z,t:ns" padded with
+    spaces to 99 characters; println adds the newline."""
+    s = "#%d,%d:" % (int(phase), int(sensor_type))
+    for v in np.asarray(xyz, np.float32).reshape(3):
+        s += java_float_string(v) + ","
+    s += "t:%d" % int(t_ns)
+    return s.ljust(99) + "\n"
+
+
+def events_text(types, values, times, phase=3):
+    """One filter's stream of float32 samples -> the text the phone sends (one message per event)."""
+    return "".join(message(phase, ty, v, t) for ty, v, t in zip(np.asarray(types), np.asarray(values, np.float32),
+                                                               np.asarray(times)))
+
+
+def events_from_wire(texts, init_acc, init_mag, t_init, phase=3):
+    """Per-filter wire texts -> the engine's event dict (types (E, K), values64 (E, K, 3) the server's
+    doubles, times (E, K), init_acc / init_mag (K, 3), t_init (K,)).  Messages of other phases are
+    dropped; streams of different lengths are padded with type-3 events (no sample)."""
+    ps = [parse(t) for t in texts]
+    ps = [{k: v[p["phase"] == phase] for k, v in p.items()} for p in ps]
+    E, K = max((len(p["types"]) for p in ps), default=0), len(ps)
+    types = np.full((E, K), 3, np.uint32)
+    vals = np.zeros((E, K, 3), np.float64)
+    times = np.zeros((E, K), np.int64)
+    for k, p in enumerate(ps):
+        n = len(p["types"])
+        types[:n, k] = p["types"]
+        vals[:n, k] = p["values"]
+        times[:n, k] = p["times"]
+        times[n:, k] = p["times"][-1] if n else int(np.asarray(t_init).reshape(-1)[k])
+    return dict(types=types, values64=vals, values=vals.astype(np.float32), times=times,
+                init_acc=np.asarray(init_acc, np.float64).reshape(K, 3),
+                init_mag=np.asarray(init_mag, np.float64).reshape(K, 3),
+                t_init=np.asarray(t_init, np.int64).reshape(K))
+
+
+__all__ = ["server_values", "parse", "java_float_string", "message", "events_text", "events_from_wire"]

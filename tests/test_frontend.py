@@ -14,9 +14,16 @@ from oracle import frontend_numpy as fe
 from poseestimationkf_amd import synth
 
 
-def _oracle_records(ev, k):
-    return fe.run_frontend(ev["types"][:, k], ev["values"][:, k].astype(np.float64), ev["times"][:, k],
-                           ev["init_acc"][k], ev["init_mag"][k], ev["t_init"][k])
+def _oracle_records(ev, k, server=False):
+    """Filter k's records by the restatement; server=True feeds it the server's own sample values
+    (std::stod of the phone's Float.toString text, wire.server_values) instead of the floats widened."""
+    if server:
+        from poseestimationkf_amd import wire
+        vals = wire.server_values(ev["values"][:, k])
+    else:
+        vals = ev["values"][:, k].astype(np.float64)
+    return fe.run_frontend(ev["types"][:, k], vals, ev["times"][:, k], ev["init_acc"][k], ev["init_mag"][k],
+                           ev["t_init"][k])
 
 
 def test_oracle_lpf_matches_reference_test_py():
@@ -330,3 +337,113 @@ def test_phase2_then_phase3_events_to_filter(eng, oracle_c):
     err = float(np.abs(X2[cols] - Xo).max())
     print("phase 2 + phase 3 + filter vs oracle chain: max |dq| = %.3e over %d records" % (err, n))
     assert err < 1e-9
+
+
+# ------------------------------------------------------------------ FP64 events (PEKF_EV_F64_EVENTS)
+
+@pytest.mark.gpu
+def test_frontend_fp64_events_records_vs_oracle(eng):
+    """k_frontend on FP64 events writes FP64 records (pekf_run_rec64_dev's planes): against the
+    restatement fed the server's values, gyro and dt exactly, acc / mag within 1e-15 (the kernel's
+    reciprocal / rsqrt with a Newton step against IEEE divisions), the pooled queue's rows intact.  The
+    f32 events' records against the same oracle differ by the samples' f32 rounding (~1e-7)."""
+    K, E = 300, 1200
+    ev = synth.generate_events(np.arange(K), E, seed=7)
+    win, counts = eng.run_frontend(ev, events="f64")
+    g, dt, a, m, refs = win.download_filters(np.arange(K))
+    win32, _ = eng.run_frontend(ev)
+    rec32 = win32.download_filters(np.arange(K))
+    worst = worst32 = 0.0
+    for k in range(K):
+        og, odt, oa, om = _oracle_records(ev, k, server=True)
+        r = len(odt)
+        assert counts[k] == r
+        assert np.array_equal(g[:r, k], og) and np.array_equal(dt[:r, k], odt.astype(np.float64))
+        worst = max(worst, float(np.abs(a[:r, k] - oa).max()), float(np.abs(m[:r, k] - om).max()))
+        worst32 = max(worst32, float(np.abs(rec32.acc[:r, k] - oa).max()), float(np.abs(rec32.mag[:r, k] - om).max()))
+        an = np.asarray(ev["init_acc"][k]) / np.sqrt(((ev["init_acc"][k] ** 2).sum()))
+        assert np.abs(refs[k, :3] - an).max() < 1e-15
+    print("FP64-event records vs the server-value restatement %.2e; f32-event records vs it %.2e" % (worst, worst32))
+    assert worst < 1e-15 and 1e-9 < worst32 < 1e-6
+
+
+@pytest.mark.gpu
+def test_frontend_fp64_events_drifting_lanes_and_padding(eng):
+    """The FP64-record pool (32 slots per 8-lane group) under lanes drifting apart, a slow lane, one with
+    no record, and streams padded with no-sample events: every record equals the restatement's."""
+    A, G, M = synth.EV_ACC, synth.EV_GYRO, synth.EV_MAG
+    K, E = 64 * 2 + 5, 600
+    types = np.empty((E, K), np.uint32)
+    for k in range(K):
+        lane = k % 64
+        if lane < 58:
+            seq = [A] * (3 * (lane % 13)) + [G, A, M] * E
+        elif lane < 62:
+            seq = [G, A, M, G, A] * E
+        else:
+            seq = [A, M] * E
+        types[:, k] = seq[:E]
+    types[E - 40:, ::3] = 3                                  # padded tails
+    e = np.arange(E)[:, None]
+    gaps = 900 + (e * 7 + np.arange(K)[None, :] * 13) % 400
+    times = synth.T_INIT_NS + np.cumsum(gaps, axis=0)
+    vals = (np.sin(0.05 * e[..., None] + 0.1 * np.arange(K)[None, :, None] + np.arange(3)[None, None, :]) +
+            np.where(types[..., None] == A, [0, 0, 9.0], [0, 0, 0])).astype(np.float32)
+    ev = dict(types=types, values=vals, times=times, init_acc=np.tile([0.1, 0.2, 9.8], (K, 1)),
+              init_mag=np.tile([20.0, 1.0, -40.0], (K, 1)), t_init=np.full(K, synth.T_INIT_NS, np.int64))
+    win, counts = eng.run_frontend(ev, events="f64")
+    g, dt, a, m, _ = win.download_filters(np.arange(K))
+    for k in range(K):
+        og, odt, oa, om = _oracle_records(ev, k, server=True)
+        r = len(odt)
+        assert counts[k] == r
+        assert np.array_equal(g[:r, k], og) and np.array_equal(dt[:r, k], odt.astype(np.float64))
+        if r:
+            assert np.abs(a[:r, k] - oa).max() < 1e-15 and np.abs(m[:r, k] - om).max() < 1e-15
+    assert counts.max() - counts.min() > 100 and counts.min() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("E,n_avg", [(700, 100), (520, 100), (40, 2)])
+def test_frontend_init_fp64_events_vs_oracle(eng, E, n_avg):
+    """Phase 2 on FP64 events: the means and variances of the server's own values, bit for bit against
+    the restatement fed the same doubles (the same sequential sums and IEEE divisions)."""
+    from poseestimationkf_amd import wire
+    K = 300
+    ev = synth.generate_events(np.arange(K), E, seed=8)
+    v64 = wire.server_values(ev["values"])
+    got = eng.frontend_init(ev, n_avg=n_avg, events="f64")
+    n_ready = 0
+    for k in range(K):
+        o = fe.initial_values(ev["types"][:, k], v64[:, k], ev["times"][:, k], n_avg=n_avg)
+        assert got["ready"][k] == o["ready"]
+        if not o["ready"]:
+            assert np.isnan(got["init"][k]).all()
+            continue
+        n_ready += 1
+        assert got["t_init"][k] == o["t_init"]
+        assert np.array_equal(got["init"][k], np.array(o["acc"] + o["mag"]))
+        assert np.array_equal(got["gyro_mean"][k], np.array(o["gyro"]))
+        for name in ("acc", "mag", "gyro"):
+            assert np.array_equal(got["var_" + name][k], np.array(o["var_" + name]))
+    assert n_ready > 0 and (E != 520 or n_ready < K)
+
+
+@pytest.mark.gpu
+def test_fp64_event_arguments_are_checked(eng):
+    """PEKF_EV_F64_EVENTS takes no time-event, f32-record or dt-side-plane companion."""
+    from poseestimationkf_amd._lib import EV_F32_RECORDS, EV_F64_EVENTS, EV_TIME_EVENTS, PekfError, lib, check
+    K, E = 8, 30
+    ev = synth.generate_events(np.arange(K), E, seed=9)
+    with pytest.raises(ValueError, match="FP64 events make FP64 records"):
+        eng.BatchedEKF(K).run_events(ev, records="f32", events="f64")
+    buf = eng.DeviceBuffer(32 * K * E)
+    st = eng.DeviceBuffer(4096)
+    f = eng.BatchedEKF(K)
+    for fl in (EV_F64_EVENTS | EV_TIME_EVENTS, EV_F64_EVENTS | EV_F32_RECORDS):
+        with pytest.raises(PekfError, match="PEKF_EV_F64_EVENTS"):
+            check(lib.pekf_live_ext_dev(K, E, buf.ptr, st.ptr, st.ptr, 0.1, f.X.ptr, f.P.ptr, 1.0, 0.1, st.ptr,
+                                        st.ptr, fl, None, None))
+    with pytest.raises(PekfError, match="FP64 events"):
+        check(lib.pekf_frontend_ext_dev(K, E, buf.ptr, st.ptr, st.ptr, 0.1, 10, buf.ptr, buf.ptr, buf.ptr, st.ptr,
+                                        st.ptr, st.ptr, EV_F64_EVENTS, None, None))

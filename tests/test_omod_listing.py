@@ -127,7 +127,8 @@ def test_omod_only_inside_the_mode_window_multi_record(tmp_path):
 def test_omod_only_inside_the_mode_window_live(tmp_path):
     lines = _listing("pekf_live.hip", [], tmp_path)
     n_fn, n_omod = _check(lines)
-    assert n_fn == 4 and n_omod > 100       # k_live<TE, R64>: time events or not x FP64 / f32 records
+    # k_live<TE, R64>: time events or not x FP64 / f32 records, and k_live<.., EV64> (FP64 events)
+    assert n_fn == 5 and n_omod > 100
 
 
 def test_checker_catches_an_omod_outside_the_window():
