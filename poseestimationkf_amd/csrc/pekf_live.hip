@@ -37,6 +37,9 @@ namespace pekf {
 #ifndef PEKF_LIVE_RING
 #define PEKF_LIVE_RING 3  // event rows in flight per lane; a filter step may run after each block of them
 #endif
+#ifndef PEKF_LIVE_RING64
+#define PEKF_LIVE_RING64 3  // the same for FP64 events (32 B each)
+#endif
 #ifndef PEKF_LIVE_NTL
 #define PEKF_LIVE_NTL 1  // non-temporal event loads: each event is read once (-1.4 %, profiles/r4/ntload/)
 #endif
@@ -53,7 +56,7 @@ namespace pekf {
 #define PEKF_LIVE_QUORUM 56  // lanes of 64 with a queued record that trigger a filter step
 #endif
 #ifndef PEKF_LIVE_EV64_WAVES
-#define PEKF_LIVE_EV64_WAVES 1
+#define PEKF_LIVE_EV64_WAVES 2
 #endif
 
 // A lane's records waiting for the wave's next filter step, oldest first: a ring of Q slots per lane in
@@ -232,7 +235,7 @@ __global__ __launch_bounds__(kRunBlock) __attribute__((amdgpu_waves_per_eu(EV64 
     const double *__restrict__ init, const int64_t *__restrict__ t_init, double alpha, double qs, double rs,
     double *__restrict__ Xio, double *__restrict__ Pio, int32_t *__restrict__ counts, double *__restrict__ refs) {
     using EvT = std::conditional_t<EV64, double4, float4>;
-    constexpr int kRing = PEKF_LIVE_RING, kFlush = 3, kQuorum = PEKF_LIVE_QUORUM;
+    constexpr int kRing = EV64 ? PEKF_LIVE_RING64 : PEKF_LIVE_RING, kFlush = 3, kQuorum = PEKF_LIVE_QUORUM;
     constexpr int kQueue = EV64 ? PEKF_LIVE_QUEUE_EV64 : R64 ? PEKF_LIVE_QUEUE64 : PEKF_LIVE_QUEUE;
     constexpr int kPush = kRing / kFlush;  // records a lane can complete within one block
     static_assert(kRing % kFlush == 0, "the ring depth must be a multiple of the emit period");

@@ -64,6 +64,13 @@ __device__ __forceinline__ V3 normalised(const V3 &v) {
     const double in = rsqrt<true>((v.x * v.x + v.y * v.y) + v.z * v.z);
     return {v.x * in, v.y * in, v.z * in};
 }
+// The same with the sum of squares fused explicitly, fma(z, z, fma(y, y, x x)): which product of a sum of
+// products the compiler contracts depends on the code around it, and the FP64-event records of k_live and
+// k_frontend must round identically (normalised keeps the f32 form's rounding as it was)
+__device__ __forceinline__ V3 normalised_fma(const V3 &v) {
+    const double in = rsqrt<true>(__builtin_fma(v.z, v.z, __builtin_fma(v.y, v.y, v.x * v.x)));
+    return {v.x * in, v.y * in, v.z * in};
+}
 
 // A completed record's inputs, captured when the state machine completes it (its state moves on at
 // once) and turned into the record by Phase3::emit: the gyro sample, acc_0 / acc_1 / mag_0 / mag_1
@@ -76,6 +83,14 @@ struct RawRecT {
     double dt, an, ad, mn, md;  // dt, acc / mag lerp num and den
 };
 using RawRec = RawRecT<F3>;
+// FP64 events: the record waits with its interpolations already formed, each scaled by |t2 - t1| (A, M:
+// Phase3T::lerp_scaled), so a pending record is 10 doubles instead of 20 -- the registers that keep
+// k_live's FP64-event form at two waves per SIMD -- and its emit needs no reciprocal.
+template <>
+struct RawRecT<V3> {
+    V3 A, M, gyro;
+    double dt;
+};
 
 // An FP64 event {x, y, z, w}: w's bits are those of the event's time in ns as a float64 (an integer of
 // magnitude < 2^51, so its two lowest mantissa bits are zero) with the type in those two bits (3: no
@@ -127,6 +142,7 @@ __device__ __forceinline__ double4 load_event(const double4 *q) {
 template <typename S>
 struct Phase3T {
     using Raw = RawRecT<S>;
+    static constexpr bool kLean = std::is_same<S, V3>::value;  // FP64 events: the lean capture (RawRecT<V3>)
     // phase-2 state: acc_0 / mag_0 = raw means at the initialisation time (Parser.cpp:44-53)
     V3 mean_acc, mean_mag;
     S acc0, mag0;
@@ -153,8 +169,10 @@ struct Phase3T {
     // Arithmetic is unchanged: the time differences are formed at capture, exactly as lerp_to would.
     bool pend;
     Raw p;
+    const double *init;  // kLean: the phase-2 means are re-read from here in the (rare) capture that needs them
 
     __device__ __forceinline__ void start(const double *init6, int64_t t_start, double a) {
+        init = init6;
         mean_acc = {init6[0], init6[1], init6[2]};
         mean_mag = {init6[3], init6[4], init6[5]};
         acc0 = mag0 = acc1 = mag1 = gyro = {0, 0, 0};
@@ -165,11 +183,35 @@ struct Phase3T {
         gyro_set = acc1_set = mag1_set = false;
         alpha = a;
         beta = 1.0 - a;
+        if constexpr (kLean) {  // wave-uniform: kept in SGPRs (VGPRs are what this form is short of)
+            alpha = uniform(alpha);
+            beta = uniform(beta);
+        }
         pend = false;
-        p.gyro = p.acc0 = p.mag0 = p.acc1 = p.mag1 = {0, 0, 0};
-        p.acc0_mean = p.mag0_mean = true;
-        p.dt = p.an = p.mn = 0;
-        p.ad = p.md = 1;
+        if constexpr (kLean) {
+            p.A = p.M = p.gyro = {0, 0, 0};
+            p.dt = 0;
+        } else {
+            p.gyro = p.acc0 = p.mag0 = p.acc1 = p.mag1 = {0, 0, 0};
+            p.acc0_mean = p.mag0_mean = true;
+            p.dt = p.an = p.mn = 0;
+            p.ad = p.md = 1;
+        }
+    }
+
+    // kLean: Parser::LinearInterpolationSensor (:259-267), y1 + (y2 - y1) / (t2 - t1) * (t3 - t1), formed
+    // times d = |t2 - t1| as (y2 - y1) * s + y1 * d with s = sign(t2 - t1) (t3 - t1) -- equal in real
+    // arithmetic, and normalisation removes the positive scale d.  d = 0 gives NaN, as the reference's
+    // division by zero does (every component inf or NaN, normalised to NaN).
+    __device__ __forceinline__ static V3 lerp_scaled(const V3 &y1, const V3 &y2, double num, double den) {
+#pragma clang fp contract(fast)
+        const double d = fabs(den), sn = den < 0.0 ? -num : num;
+        // explicit fmas: the contraction of a sum of two products is the compiler's choice, and k_live and
+        // k_frontend must round their records identically
+        V3 r = {__builtin_fma(y2.x - y1.x, sn, y1.x * d), __builtin_fma(y2.y - y1.y, sn, y1.y * d),
+                __builtin_fma(y2.z - y1.z, sn, y1.z * d)};
+        if (d == 0.0) r.x = __builtin_nan("");
+        return r;
     }
 
     // the filter's reference vectors: the normalised phase-2 means (Parser.cpp:48-49); call after start
@@ -226,8 +268,19 @@ struct Phase3T {
             asm volatile("");  // keeps this a branch: masked 64-bit moves, not two selects per double
             Raw r;
             r.gyro = gyro; r.dt = t_gyro - prev_t;
-            r.acc0 = acc0; r.acc0_mean = acc0_mean; r.acc1 = acc1; r.an = t_gyro - t_acc0; r.ad = t_acc1 - t_acc0;
-            r.mag0 = mag0; r.mag0_mean = mag0_mean; r.mag1 = mag1; r.mn = t_gyro - t_mag0; r.md = t_mag1 - t_mag0;
+            if constexpr (kLean) {
+                V3 a0 = acc0, m0 = mag0;
+                // acc_0 / mag_0 can still be the phase-2 means only up to a lane's first record
+                if (__builtin_expect(__any(acc0_mean || mag0_mean), 0)) {
+                    a0 = sel(acc0_mean, V3{init[0], init[1], init[2]}, a0);
+                    m0 = sel(mag0_mean, V3{init[3], init[4], init[5]}, m0);
+                }
+                r.A = lerp_scaled(a0, acc1, t_gyro - t_acc0, t_acc1 - t_acc0);
+                r.M = lerp_scaled(m0, mag1, t_gyro - t_mag0, t_mag1 - t_mag0);
+            } else {
+                r.acc0 = acc0; r.acc0_mean = acc0_mean; r.acc1 = acc1; r.an = t_gyro - t_acc0; r.ad = t_acc1 - t_acc0;
+                r.mag0 = mag0; r.mag0_mean = mag0_mean; r.mag1 = mag1; r.mn = t_gyro - t_mag0; r.md = t_mag1 - t_mag0;
+            }
             on_done(r);
             prev_t = t_gyro;
         }
@@ -277,7 +330,17 @@ struct Phase3T {
     // (6 moves per emit).
     __device__ __forceinline__ void lpf_step(double &l, double x) const {
         const double ax = alpha * x;
-        asm("v_fma_f64 %0, %1, %0, %2" : "+v"(l) : "v"(beta), "v"(ax));
+        if constexpr (kLean)
+            asm("v_fma_f64 %0, %1, %0, %2" : "+v"(l) : "s"(beta), "v"(ax));
+        else
+            asm("v_fma_f64 %0, %1, %0, %2" : "+v"(l) : "v"(beta), "v"(ax));
+    }
+    // a wave-uniform double moved to SGPRs (readfirstlane of its two halves)
+    static __device__ __forceinline__ double uniform(double v) {
+        const long long b = __double_as_longlong(v);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(b >> 32));
+        return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
     }
 
     // A captured record, in the order they complete: interpolation, normalisation, low-pass (the FP64
@@ -315,7 +378,11 @@ struct Phase3T {
     // lpf_record, and the record's gyro and dt in FP64 (FP64 events: {gx, gy, gz, dt_ns}, the GD half of
     // an 80 B record; the dt is any float64, so nothing is escaped).
     __device__ __forceinline__ double4 emit64(const Raw &q) {
-        lpf_record(q);
+        static_assert(kLean, "FP64 records come from FP64 events");
+        // the captured interpolations normalised (their scale d drops out), then the low-pass
+        const V3 a = normalised_fma(q.A), m = normalised_fma(q.M);
+        lpf_step(lpf_mag.x, m.x); lpf_step(lpf_mag.y, m.y); lpf_step(lpf_mag.z, m.z);
+        lpf_step(lpf_acc.x, a.x); lpf_step(lpf_acc.y, a.y); lpf_step(lpf_acc.z, a.z);
         return make_double4(q.gyro.x, q.gyro.y, q.gyro.z, q.dt);
     }
     __device__ __forceinline__ double4 emit64() {

@@ -8,6 +8,7 @@ import sys
 
 CUS, SIMDS, XCDS = 256, 4, 8
 K, E = 1 << 20, 1024
+EVB = int(sys.argv[3]) if len(sys.argv) > 3 else 16  # bytes per event (32: FP64 events)
 
 
 def last(path):
@@ -28,7 +29,7 @@ out = {"kernel": "k_live<false> (pekf_live_dev)", "dispatches": n, "summarised":
        "valu_insts_per_wave": s["SQ_INSTS_VALU"] / s["SQ_WAVES"],
        "valu_busy": 4 * s["SQ_ACTIVE_INST_VALU"] / (CUS * SIMDS * s["GRBM_GUI_ACTIVE"] / XCDS),
        "effective_clock_ghz": clk / 1e9, "sq_wait_any_frac": s["SQ_WAIT_ANY"] / s["SQ_WAVE_CYCLES"],
-       "traffic_bytes": 2.0 * f["FETCH_SIZE"] * 1024, "algorithmic_bytes": 16 * K * E,
+       "traffic_bytes": 2.0 * f["FETCH_SIZE"] * 1024, "algorithmic_bytes": EVB * K * E,
        "note": "traffic = 2 x FETCH_SIZE x 1024 (gfx950); valu_busy = 4 x SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE/8)"}
 out["traffic_over_algorithmic"] = out["traffic_bytes"] / out["algorithmic_bytes"]
 print(json.dumps(out, indent=1))
