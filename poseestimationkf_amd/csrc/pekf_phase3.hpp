@@ -255,10 +255,24 @@ struct Phase3T {
         const bool gs = gyro_set;
         const bool wA1 = isA && gs, wM1 = isM && gs;
         // acc1 / mag1: the latest sample (equal to the Parser's acc_1 / mag_1 whenever that is set)
-        acc1 = sel(isA, v, acc1);
-        t_acc1 = isA ? tn : t_acc1;
-        mag1 = sel(isM, v, mag1);
-        t_mag1 = isM ? tn : t_mag1;
+        if constexpr (kLean) {
+            // FP64 samples: a masked 64-bit move per double (a branch) instead of two selects
+            if (isA) {
+                asm volatile("");
+                acc1 = v;
+                t_acc1 = tn;
+            }
+            if (isM) {
+                asm volatile("");
+                mag1 = v;
+                t_mag1 = tn;
+            }
+        } else {
+            acc1 = sel(isA, v, acc1);
+            t_acc1 = isA ? tn : t_acc1;
+            mag1 = sel(isM, v, mag1);
+            t_mag1 = isM ? tn : t_mag1;
+        }
         const bool a1s = wA1 || (acc1_set && !(isG && gs)), m1s = wM1 || (mag1_set && !(isG && gs));
         const bool sA = isG && gs && acc1_set, sM = isG && gs && mag1_set;  // gyro shift
         // ExecuteKalmanFilter (Parser.cpp:229-257) once acc_1 and mag_1 are both set: record its
@@ -286,14 +300,34 @@ struct Phase3T {
         }
         // acc_0 <- the sample before any gyro (then acc1 = v), or acc_1 on a shift or after a record
         const bool cA = (isA && !gs) || sA || done, cM = (isM && !gs) || sM || done;
-        acc0 = sel(cA, acc1, acc0);
-        acc0_mean = acc0_mean && !cA;
-        t_acc0 = cA ? t_acc1 : t_acc0;
-        mag0 = sel(cM, mag1, mag0);
-        mag0_mean = mag0_mean && !cM;
-        t_mag0 = cM ? t_mag1 : t_mag0;
-        gyro = sel(isG, v, gyro);
-        t_gyro = isG ? tn : t_gyro;
+        if constexpr (kLean) {
+            if (cA) {
+                asm volatile("");
+                acc0 = acc1;
+                t_acc0 = t_acc1;
+            }
+            if (cM) {
+                asm volatile("");
+                mag0 = mag1;
+                t_mag0 = t_mag1;
+            }
+            if (isG) {
+                asm volatile("");
+                gyro = v;
+                t_gyro = tn;
+            }
+            acc0_mean = acc0_mean && !cA;
+            mag0_mean = mag0_mean && !cM;
+        } else {
+            acc0 = sel(cA, acc1, acc0);
+            acc0_mean = acc0_mean && !cA;
+            t_acc0 = cA ? t_acc1 : t_acc0;
+            mag0 = sel(cM, mag1, mag0);
+            mag0_mean = mag0_mean && !cM;
+            t_mag0 = cM ? t_mag1 : t_mag0;
+            gyro = sel(isG, v, gyro);
+            t_gyro = isG ? tn : t_gyro;
+        }
         gyro_set = (gs || isG) && !done;
         acc1_set = a1s && !done;
         mag1_set = m1s && !done;
