@@ -19,7 +19,13 @@ must equal the f32 form's, and the four filters' final X must agree with the unr
 F64_TOL; NaN where the chain's SVD raises (a NaN record: duplicate timestamps interpolate 0/0).
 check_f64 says which filters the reference's own ill-conditioning exempts.
 
-usage: python3 scripts/fuzz_live.py [--cases N] [--seed S]   (exit status 1 on any difference)
+--ev64 (round 6) adds FP64 events (PEKF_EV_F64_EVENTS: the server's own stod values) on every case: the
+fused kernel must equal the FP64 split pipeline (pekf_frontend_ext_dev writing FP64 records, then
+pekf_run_rec64_dev with counts) bit for bit, its counts and reference pairs the f32 form's, and the
+four filters' final X the oracle chain fed the server's values (wire.server_values) within F64_TOL,
+with the same exemptions as check_f64.
+
+usage: python3 scripts/fuzz_live.py [--cases N] [--seed S] [--ev64]   (exit status 1 on any difference)
 """
 from __future__ import annotations
 
@@ -34,7 +40,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from oracle import ekf_numpy, frontend_numpy  # noqa: E402  (the checkers)
-from poseestimationkf_amd import engine, synth  # noqa: E402
+from poseestimationkf_amd import engine, synth, wire  # noqa: E402
 
 KINDS = np.array([synth.EV_ACC, synth.EV_GYRO, synth.EV_MAG], np.uint32)
 F64_TOL = 1e-9   # FP64 records vs the unrounded chain (tests/test_live.py asserts 1e-12 on smooth streams)
@@ -124,13 +130,25 @@ def split(case, cols=None):
     return X, P, counts, win.refs.download((case["K"], 6), np.float64)
 
 
-def fused(case, records="f32"):
+def fused(case, records="f32", events="f32"):
     f = engine.BatchedEKF(case["K"])
     if case["X0"] is not None:
         f.set_state(case["X0"], case["P0"])
-    counts, refs = f.run_events(case["ev"], records=records)   # f32: the split pipeline's records
+    counts, refs = f.run_events(case["ev"], records=records, events=events)   # f32: the split pipeline's records
     X, P = f.get_state()
     return X, P, counts, refs
+
+
+def split64(case):
+    """The FP64-event split pipeline: FP64 records (a RecordWindow64), then pekf_run_rec64_dev with counts."""
+    win, counts = engine.run_frontend(case["ev"], events="f64")
+    f = engine.BatchedEKF(case["K"])
+    if case["X0"] is not None:
+        f.set_state(case["X0"], case["P0"])
+    if counts.max(initial=0) > 0:
+        f.run(win, n_steps=max(2, int(counts.max())))
+    X, P = f.get_state()
+    return X, P, counts, win.refs.download((case["K"], 6), np.float64)
 
 
 def _chain(g, dt, a, m, refs_k, X0, P0):
@@ -143,7 +161,7 @@ def _chain(g, dt, a, m, refs_k, X0, P0):
         return np.full(4, np.nan), True
 
 
-def check_f64(case, got, cols, tally):
+def check_f64(case, got, cols, tally, server=False):
     """(problems, worst |dq|) of the FP64-record run's filters cols against the unrounded oracle chain.
 
     Two kinds of filter are not held to F64_TOL, each counted in `tally`: where the reference itself
@@ -159,7 +177,8 @@ def check_f64(case, got, cols, tally):
     for k in cols:
         if not np.isfinite(ev["init_acc"][k]).all():
             continue
-        g, dt, a, m = frontend_numpy.run_frontend(ev["types"][:, k], ev["values"][:, k].astype(np.float64),
+        vals = wire.server_values(ev["values"][:, k]) if server else ev["values"][:, k].astype(np.float64)
+        g, dt, a, m = frontend_numpy.run_frontend(ev["types"][:, k], vals,
                                                   ev["times"][:, k], ev["init_acc"][k], ev["init_mag"][k],
                                                   ev["t_init"][k])
         if len(dt) == 0:
@@ -168,9 +187,27 @@ def check_f64(case, got, cols, tally):
         P0 = None if case["P0"] is None else case["P0"][k]
         dt = dt.astype(np.float64)
         Xo, raised = _chain(g, dt, a, m, refs[k], X0, P0)
+
+        def ulp_spread():
+            # the reference's own answer under 1-ulp input noise (16 samples): near an identity Wahba
+            # rotation its R->q divides rounding noise by the angle; NaN if any sample is
+            pr = np.random.default_rng(k)
+            sp = 0.0
+            for _ in range(16):
+                u = lambda v: v * (1 + 2.2e-16 * pr.standard_normal(np.shape(v)))  # noqa: E731
+                Xn, _ = _chain(u(g), dt, u(a), u(m), u(refs[k]), X0, P0)
+                sp = max(sp, float(np.abs(Xn - Xo).max())) if np.isfinite(Xn).all() else np.nan
+            return sp
         if raised or np.isnan(X[k]).any():
-            if not (raised and np.isnan(X[k]).all()):
-                out.append("filter %d: NaN in one of kernel / chain (chain raised: %s)" % (k, raised))
+            if raised and np.isnan(X[k]).all():
+                continue                                  # both NaN: a NaN record (0 / 0 interpolation)
+            if not raised and np.isnan(Xo).all() and np.isnan(X[k]).all():
+                tally["reference_nan"] += 1               # both NaN from finite records: the reference's R->q
+                continue                                  # at an exactly-identity rotation, taken by both
+            if not raised and not np.isnan(Xo).any() and not ulp_spread() < 1e-6:
+                tally["ill_conditioned"] += 1             # the kernel NaN where the reference's own answer
+                continue                                  # is noise-driven (NaN or moved under 1-ulp noise)
+            out.append("filter %d: NaN in one of kernel / chain (chain raised: %s)" % (k, raised))
             continue
         if np.isnan(Xo).any():
             tally["reference_nan"] += 1
@@ -182,16 +219,13 @@ def check_f64(case, got, cols, tally):
             continue
         d = float(np.abs(X[k] - Xo).max())
         if d > F64_TOL:
-            # near an identity Wahba rotation the reference's R->q divides rounding noise by the angle
-            # (DESIGN.md §4.1): its own answer then moves by ~d under 1-ulp input noise.  Such a filter
-            # is held to four times that spread (a 16-sample estimate), and counted.
-            pr = np.random.default_rng(k)
-            spread = 0.0
-            for _ in range(16):
-                u = lambda v: v * (1 + 2.2e-16 * pr.standard_normal(np.shape(v)))  # noqa: E731
-                Xn, _ = _chain(u(g), dt, u(a), u(m), u(refs[k]), X0, P0)
-                spread = max(spread, float(np.abs(Xn - Xo).max()))
-            if d <= 4 * spread:
+            # such a filter is held to four times the reference's own 1-ulp spread, and counted; one whose
+            # answer turns NaN under 1-ulp noise (an exactly-identity rotation one ulp away) is ill-conditioned
+            sp = ulp_spread()
+            if np.isnan(sp):
+                tally["ill_conditioned"] += 1
+                continue
+            if d <= 4 * sp:
                 tally["ulp_sensitive"] += 1
                 continue
         worst = max(worst, d)
@@ -205,10 +239,12 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", type=int, default=100)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--ev64", action="store_true")
     a = ap.parse_args(argv)
     rng = np.random.default_rng(a.seed)
-    fails, records, t0, worst64 = 0, 0, time.time(), 0.0
+    fails, records, t0, worst64, worst_ev64 = 0, 0, time.time(), 0.0, 0.0
     tally = dict(checked=0, reference_nan=0, ill_conditioned=0, ulp_sensitive=0)
+    tally64 = dict(checked=0, reference_nan=0, ill_conditioned=0, ulp_sensitive=0)
     for i in range(a.cases):
         if i and i % 25 == 0:
             print("%d cases, %d differ, %d records applied, FP64 records vs the unrounded chain <= %.3e, %.0f s"
@@ -230,6 +266,18 @@ def main(argv=None):
             fails += 1
             print("F64 case %d: %s  K=%d E=%d mix=%s" % (i, "; ".join(probs[:4]), case["K"], case["E"], case["mix"]),
                   flush=True)
+        if a.ev64:
+            x64, s64 = fused(case, "f64", "f64"), split64(case)
+            probs, d = check_f64(case, x64, cols, tally64, server=True)
+            worst_ev64 = max(worst_ev64, d)
+            if not (np.array_equal(x64[2], u[2]) and np.array_equal(x64[3], u[3], equal_nan=True)):
+                probs.append("FP64 events: counts / refs differ from the f32 form")
+            if not all(np.array_equal(x, y, equal_nan=True) for x, y in zip(x64, s64)):
+                probs.append("FP64 events: fused != FP64 split pipeline")
+            if probs:
+                fails += 1
+                print("EV64 case %d: %s  K=%d E=%d mix=%s" % (i, "; ".join(probs[:4]), case["K"], case["E"],
+                                                             case["mix"]), flush=True)
         same = all(np.array_equal(x, y, equal_nan=True) for x, y in zip(u, v))
         if not same:
             fails += 1
@@ -242,6 +290,11 @@ def main(argv=None):
           "%d within 4x the reference's own spread under 1-ulp input noise)"
           % (a.cases, fails, records, worst64, tally["checked"], tally["reference_nan"], tally["ill_conditioned"],
              tally["ulp_sensitive"]))
+    if a.ev64:
+        print("FP64 events: fused = FP64 split pipeline bit for bit on every case; vs the oracle chain fed the "
+              "server's values <= %.3e over %d filters (%d reference NaN, %d ill-conditioned, %d ulp-sensitive)"
+              % (worst_ev64, tally64["checked"], tally64["reference_nan"], tally64["ill_conditioned"],
+                 tally64["ulp_sensitive"]))
     return 1 if fails else 0
 
 
