@@ -10,7 +10,7 @@
 // sequence through the Python engine, bit for bit.  It loads the client as a shared library
 // (pekf_example_run) rather than starting a process from the GPU-initialised test process.
 //
-// build: g++ -O2 -std=c++17 examples/c_client.cpp -Iinclude -Lposeestimationkf_amd -lpekf \
+// build: g++ -O2 -std=c++17 examples/c_client.cpp -Iinclude -Lposeestimationkf_amd -lpekf
 //        -Wl,-rpath,$PWD/poseestimationkf_amd -o build/c_client
 //        (add -shared -fPIC -DPEKF_EXAMPLE_LIBRARY for the library form)
 #include <cstdint>

@@ -19,21 +19,25 @@ from poseestimationkf_amd import synth
 from .conftest import ROOT
 
 CLIENT_SRC = os.path.join(ROOT, "examples", "c_client.cpp")
+WIRE_SRC = os.path.join(ROOT, "examples", "wire_client.cpp")
 PREBUILT = os.path.join(ROOT, "examples", "build", "libc_client.so")
+WIRE_PREBUILT = os.path.join(ROOT, "examples", "build", "libwire_client.so")
 
 
-def _build(tmp_path, library):
-    out = str(tmp_path / ("libc_client.so" if library else "c_client"))
+def _build(tmp_path, library, src=CLIENT_SRC):
+    name = os.path.splitext(os.path.basename(src))[0]
+    out = str(tmp_path / (("lib%s.so" % name) if library else name))
     pkg = os.path.join(ROOT, "poseestimationkf_amd")
     extra = ["-shared", "-fPIC", "-DPEKF_EXAMPLE_LIBRARY"] if library else []
-    subprocess.check_call(["g++", "-O2", "-std=c++17", *extra, CLIENT_SRC, "-I" + os.path.join(ROOT, "include"),
-                           "-L" + pkg, "-lpekf", "-Wl,-rpath," + pkg, "-o", out])
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-Wall", "-Werror", *extra, src,
+                           "-I" + os.path.join(ROOT, "include"), "-L" + pkg, "-lpekf", "-Wl,-rpath," + pkg, "-o", out])
     return out
 
 
 @pytest.mark.parametrize("library", [False, True])
-def test_c_client_builds(tmp_path, library):
-    assert os.path.exists(_build(tmp_path, library))
+@pytest.mark.parametrize("src", [CLIENT_SRC, WIRE_SRC])
+def test_c_client_builds(tmp_path, library, src):
+    assert os.path.exists(_build(tmp_path, library, src))
 
 
 @pytest.mark.gpu
@@ -73,3 +77,41 @@ def test_c_client_matches_python_engine(tmp_path):
     h.run(win, n_steps=W)
     X2, _ = h.get_state()
     assert np.array_equal(vals[:B], X1) and np.array_equal(vals[B:], X2)
+
+
+@pytest.mark.gpu
+def test_wire_client_matches_python_session(tmp_path):
+    """examples/wire_client.cpp: K phones' wire text (phase-2 then phase-3 messages, as the Android
+    client sends them) -> pekf_wire_parse -> FP64 event planes -> pekf_frontend_init_ext_dev ->
+    pekf_live_ext_dev, all from C++; the same texts through wire.events_from_wire and
+    engine.run_session(events="f64") give the same counts and quaternions, bit for bit."""
+    from poseestimationkf_amd import engine, wire
+    K = 24
+    ph2 = synth.generate_events(np.arange(K), 700, seed=51)
+    ph3 = synth.generate_events(np.arange(K), 400, seed=52)
+    ph3 = dict(ph3, times=ph3["times"] - ph3["t_init"][None, :] + ph2["times"][-1][None, :])
+    paths = []
+    for k in range(K):
+        n3 = 400 - 7 * (k % 4)                                   # ragged phase-3 streams
+        text = (wire.events_text(ph2["types"][:, k], ph2["values"][:, k], ph2["times"][:, k], phase=2) +
+                wire.events_text(ph3["types"][:n3, k], ph3["values"][:n3, k], ph3["times"][:n3, k], phase=3))
+        p = tmp_path / ("phone%d.txt" % k)
+        p.write_text(text)
+        paths.append(str(p))
+    client = ctypes.CDLL(WIRE_PREBUILT)  # built by csrc/Makefile with the library
+    client.pekf_wire_example_run.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    res = tmp_path / "out.txt"
+    assert client.pekf_wire_example_run("\n".join(paths).encode(), os.fsencode(res)) == 0
+    got = np.array([[float(v) for v in line.split()] for line in res.read_text().strip().splitlines()])
+    assert got.shape == (K, 5)
+
+    texts = [open(p).read() for p in paths]
+    t0 = ph2["times"][0]
+    e2 = wire.events_from_wire(texts, np.zeros((K, 3)), np.zeros((K, 3)), t0, phase=2)
+    e3 = wire.events_from_wire(texts, np.zeros((K, 3)), np.zeros((K, 3)), t0, phase=3)
+    f = engine.BatchedEKF(K)
+    out = engine.run_session(e2, e3, f, events="f64")
+    X, _ = f.get_state()
+    assert out["ready"].all() and out["counts"].min() > 0
+    assert np.array_equal(got[:, 0].astype(np.int64), out["counts"])
+    assert np.array_equal(got[:, 1:], X)
