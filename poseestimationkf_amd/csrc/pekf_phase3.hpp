@@ -183,10 +183,6 @@ struct Phase3T {
         gyro_set = acc1_set = mag1_set = false;
         alpha = a;
         beta = 1.0 - a;
-        if constexpr (kLean) {  // wave-uniform: kept in SGPRs (VGPRs are what this form is short of)
-            alpha = uniform(alpha);
-            beta = uniform(beta);
-        }
         pend = false;
         if constexpr (kLean) {
             p.A = p.M = p.gyro = {0, 0, 0};
@@ -364,17 +360,7 @@ struct Phase3T {
     // (6 moves per emit).
     __device__ __forceinline__ void lpf_step(double &l, double x) const {
         const double ax = alpha * x;
-        if constexpr (kLean)
-            asm("v_fma_f64 %0, %1, %0, %2" : "+v"(l) : "s"(beta), "v"(ax));
-        else
-            asm("v_fma_f64 %0, %1, %0, %2" : "+v"(l) : "v"(beta), "v"(ax));
-    }
-    // a wave-uniform double moved to SGPRs (readfirstlane of its two halves)
-    static __device__ __forceinline__ double uniform(double v) {
-        const long long b = __double_as_longlong(v);
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(b >> 32));
-        return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+        asm("v_fma_f64 %0, %1, %0, %2" : "+v"(l) : "v"(beta), "v"(ax));
     }
 
     // A captured record, in the order they complete: interpolation, normalisation, low-pass (the FP64
