@@ -2,7 +2,9 @@
 and UndefinedBehaviorSanitizer: tests/native/log_harness.cpp, built here with g++ against the reader's
 source, scans and reads well-formed logs (pauses, a clock stepping back, lines of any length) and broken
 ones (truncated, a missing value, no colon, binary bytes, empty, absent) without a sanitizer report,
-with the results the library reports."""
+with the results the library reports.  The same for the phone's wire text (csrc/pekf_wire.cpp,
+tests/native/wire_harness.cpp): pekf_wire_parse on good, truncated, malformed and binary input, and
+pekf_f32_wire_values over every class of float."""
 import os
 import shutil
 import subprocess
@@ -74,3 +76,53 @@ def test_log_reader_under_sanitizers(harness, tmp_path):
     assert " scan=0 " in got["trunc"] and " ext=0 " in got["trunc"] and " r64=0 " in got["trunc"]
     for name in ("missing_value", "no_colon", "binary", "empty", "absent"):
         assert " scan=1 " in got[name], got[name]
+
+
+@pytest.fixture(scope="module")
+def wire_harness(tmp_path_factory):
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    out = tmp_path_factory.mktemp("asan_wire") / "wire_harness"
+    cmd = ["g++", "-g", "-O1", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+           "-fno-omit-frame-pointer", "-I" + os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "tests", "native", "wire_harness.cpp"),
+           os.path.join(ROOT, "poseestimationkf_amd", "csrc", "pekf_wire.cpp"), "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return str(out)
+
+
+def test_wire_parser_under_sanitizers(wire_harness, tmp_path):
+    from poseestimationkf_amd import wire
+    ev = synth.generate_events(np.arange(1), 60, seed=3)
+    good = wire.events_text(ev["types"][:, 0], ev["values"][:, 0], ev["times"][:, 0])
+    files = {"good": good, "trunc": good[: len(good) // 2 + 37], "no_newline": good.rstrip("\n"),
+             "noise": "hello\n#\n#3\n" + "x" * 200 + "\n" + good,
+             "missing_comma": "#3,0:1.5 2.5 3.5,t:12345" + " " * 60 + "\n",
+             "missing_t": "#3,0:1.5,2.5,3.5," + " " * 60 + "\n",
+             "bad_number": "#3,0:abc,2.5,3.5,t:12" + " " * 60 + "\n",
+             "long_line": "#3,1:" + "1" * 20000 + ",2,3,t:5\n", "empty": ""}
+    paths = []
+    for name, text in files.items():
+        p = tmp_path / (name + ".txt")
+        p.write_text(text)
+        paths.append(str(p))
+    p = tmp_path / "binary.bin"
+    p.write_bytes(bytes(range(256)) * 40 + b"#" + bytes(range(1, 256)) * 3)
+    paths.append(str(p))
+    r = subprocess.run([wire_harness] + paths, capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
+                                UBSAN_OPTIONS="print_stacktrace=1"))
+    report = r.stdout + r.stderr
+    assert r.returncode == 0 and "Sanitizer" not in report and "runtime error" not in report, report[-3000:]
+    got = dict(zip(list(files) + ["binary"], r.stdout.splitlines()))
+    assert " scan=0 messages=60 full=0 under=1 " in got["good"], got["good"]
+    assert " scan=0 messages=60 full=0 " in got["no_newline"] and " scan=0 messages=60 " in got["noise"]
+    assert " messages=0" in got["empty"]
+    # a message cut short (or malformed) is an error, where the server's std::stod / std::stoll would throw
+    for name in ("trunc", "missing_comma", "missing_t", "bad_number", "binary"):
+        assert " scan=1 " in got[name], (name, got[name])
+    assert " scan=0 messages=1 full=0 " in got["long_line"], got["long_line"]
+    last = r.stdout.splitlines()[-1]
+    n = int(last.split("n=")[1].split()[0])
+    assert last.startswith("f32_wire_values=0 ") and last.endswith("roundtrip=%d" % n), last
