@@ -107,20 +107,23 @@ def test_wire_parser_under_sanitizers(wire_harness, tmp_path):
         p = tmp_path / (name + ".txt")
         p.write_text(text)
         paths.append(str(p))
-    p = tmp_path / "binary.bin"
-    p.write_bytes(bytes(range(256)) * 40 + b"#" + bytes(range(1, 256)) * 3)
+    p = tmp_path / "binary.bin"                          # no line starts with '#': nothing for the server
+    p.write_bytes(bytes(range(256)) * 40)
+    paths.append(str(p))
+    p = tmp_path / "binary_hash.bin"                     # a '#' line of 245 garbage bytes: not a message
+    p.write_bytes(b"\n#" + bytes(range(11, 256)) + b"\n")
     paths.append(str(p))
     r = subprocess.run([wire_harness] + paths, capture_output=True, text=True, timeout=120,
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
                                 UBSAN_OPTIONS="print_stacktrace=1"))
     report = r.stdout + r.stderr
     assert r.returncode == 0 and "Sanitizer" not in report and "runtime error" not in report, report[-3000:]
-    got = dict(zip(list(files) + ["binary"], r.stdout.splitlines()))
+    got = dict(zip(list(files) + ["binary", "binary_hash"], r.stdout.splitlines()))
     assert " scan=0 messages=60 full=0 under=1 " in got["good"], got["good"]
     assert " scan=0 messages=60 full=0 " in got["no_newline"] and " scan=0 messages=60 " in got["noise"]
-    assert " messages=0" in got["empty"]
+    assert " scan=0 messages=0" in got["empty"] and " scan=0 messages=0" in got["binary"]
     # a message cut short (or malformed) is an error, where the server's std::stod / std::stoll would throw
-    for name in ("trunc", "missing_comma", "missing_t", "bad_number", "binary"):
+    for name in ("trunc", "missing_comma", "missing_t", "bad_number", "binary_hash"):
         assert " scan=1 " in got[name], (name, got[name])
     assert " scan=0 messages=1 full=0 " in got["long_line"], got["long_line"]
     last = r.stdout.splitlines()[-1]
