@@ -101,7 +101,8 @@ def test_wire_parser_under_sanitizers(wire_harness, tmp_path):
              "missing_comma": "#3,0:1.5 2.5 3.5,t:12345" + " " * 60 + "\n",
              "missing_t": "#3,0:1.5,2.5,3.5," + " " * 60 + "\n",
              "bad_number": "#3,0:abc,2.5,3.5,t:12" + " " * 60 + "\n",
-             "long_line": "#3,1:" + "1" * 20000 + ",2,3,t:5\n", "empty": ""}
+             "long_line": "#3,1:1." + "0" * 20000 + "1,2,3,t:5\n",
+             "overflow": "#3,1:" + "1" * 400 + ",2,3,t:5\n", "empty": ""}
     paths = []
     for name, text in files.items():
         p = tmp_path / (name + ".txt")
@@ -123,7 +124,8 @@ def test_wire_parser_under_sanitizers(wire_harness, tmp_path):
     assert " scan=0 messages=60 full=0 " in got["no_newline"] and " scan=0 messages=60 " in got["noise"]
     assert " scan=0 messages=0" in got["empty"] and " scan=0 messages=0" in got["binary"]
     # a message cut short (or malformed) is an error, where the server's std::stod / std::stoll would throw
-    for name in ("trunc", "missing_comma", "missing_t", "bad_number", "binary_hash"):
+    # (a value past the double range: std::stod's out_of_range)
+    for name in ("trunc", "missing_comma", "missing_t", "bad_number", "binary_hash", "overflow"):
         assert " scan=1 " in got[name], (name, got[name])
     assert " scan=0 messages=1 full=0 " in got["long_line"], got["long_line"]
     last = r.stdout.splitlines()[-1]
