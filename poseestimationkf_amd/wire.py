@@ -96,7 +96,9 @@ def events_text(types, values, times, phase=3):
 def events_from_wire(texts, init_acc, init_mag, t_init, phase=3):
     """Per-filter wire texts -> the engine's event dict (types (E, K), values64 (E, K, 3) the server's
     doubles, times (E, K), init_acc / init_mag (K, 3), t_init (K,)).  Messages of other phases are
-    dropped; streams of different lengths are padded with type-3 events (no sample)."""
+    dropped; streams of different lengths are padded with type-3 events (no sample), and a message whose
+    sensor type is not 0 / 1 / 2 becomes one too (the server's state machine matches no sensor for it,
+    KFS/Parser.cpp:148-219)."""
     ps = [parse(t) for t in texts]
     ps = [{k: v[p["phase"] == phase] for k, v in p.items()} for p in ps]
     E, K = max((len(p["types"]) for p in ps), default=0), len(ps)
@@ -105,7 +107,7 @@ def events_from_wire(texts, init_acc, init_mag, t_init, phase=3):
     times = np.zeros((E, K), np.int64)
     for k, p in enumerate(ps):
         n = len(p["types"])
-        types[:n, k] = p["types"]
+        types[:n, k] = np.where(p["types"] <= 2, p["types"], 3)
         vals[:n, k] = p["values"]
         times[:n, k] = p["times"]
         times[n:, k] = p["times"][-1] if n else int(np.asarray(t_init).reshape(-1)[k])

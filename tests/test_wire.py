@@ -93,6 +93,9 @@ def test_events_from_wire_pads_ragged_streams():
     got = wire.events_from_wire(texts, ev["init_acc"], ev["init_mag"], ev["t_init"])
     assert got["types"].shape == (50, 3)
     assert np.all(got["types"][40:, 0] == 3) and np.all(got["types"][:, 2] != 3)
+    odd = wire.events_from_wire([wire.message(3, 7, [1, 2, 3], 5) + texts[0]], ev["init_acc"][:1],
+                                ev["init_mag"][:1], ev["t_init"][:1])
+    assert odd["types"][0, 0] == 3 and np.array_equal(odd["types"][1:41, 0], got["types"][:40, 0])
     assert _same_bits(got["values64"][:50, 2], wire.server_values(ev["values"][:, 2]))
     # padding is no message: the restatements skip it
     k = 0
