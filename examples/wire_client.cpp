@@ -93,7 +93,10 @@ int planes(const std::vector<Messages> &ms, uint8_t p, void **dev, int64_t *E, s
             double *dst = &ev[4 * (e * K + k)];
             if (e < (int64_t)idx[k].size()) {
                 const int64_t i = idx[k][e];
-                put_event(dst, &ms[k].xyz[3 * i], ms[k].t[i], ms[k].type[i]);
+                // a sensor type other than 0 / 1 / 2 matches no sensor in the server's state machine
+                // (KFS/Parser.cpp:148-219): no sample, like the padding (wire.events_from_wire)
+                const unsigned ty = ms[k].type[i] <= 2 ? ms[k].type[i] : 3u;
+                put_event(dst, &ms[k].xyz[3 * i], ms[k].t[i], ty);
             } else {
                 put_event(dst, nullptr, 0, 3u);
             }

@@ -93,8 +93,11 @@ def test_wire_client_matches_python_session(tmp_path):
     paths = []
     for k in range(K):
         n3 = 400 - 7 * (k % 4)                                   # ragged phase-3 streams
-        text = (wire.events_text(ph2["types"][:, k], ph2["values"][:, k], ph2["times"][:, k], phase=2) +
-                wire.events_text(ph3["types"][:n3, k], ph3["values"][:n3, k], ph3["times"][:n3, k], phase=3))
+        t3 = wire.events_text(ph3["types"][:n3, k], ph3["values"][:n3, k], ph3["times"][:n3, k], phase=3)
+        if k % 5 == 1:                                           # a sensor type the server matches no sensor for
+            cut = 100 * 200
+            t3 = t3[:cut] + wire.message(3, 7, [1.5, -2.0, 3.25], ph3["times"][199, k]) + t3[cut:]
+        text = wire.events_text(ph2["types"][:, k], ph2["values"][:, k], ph2["times"][:, k], phase=2) + t3
         p = tmp_path / ("phone%d.txt" % k)
         p.write_text(text)
         paths.append(str(p))
