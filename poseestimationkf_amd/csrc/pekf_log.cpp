@@ -3,7 +3,8 @@
 //
 // Line tags and precedence follow the offline reader (Python Kalman Filter/ReadFile.py:27-45):
 // mag_0, acc_0, Acc_1, Mag_1, q_gyro, gyro, any line containing 'T', Wahba_quart, X_k; values are
-// the comma-separated numbers after the first ':' (strtod == Python float() for these tokens).
+// the comma-separated numbers after the first ':' (strtod in the "C" locale == Python float() for these
+// tokens, pekf_cnum.hpp).
 // Records follow main_file.py:19-47: one per Acc_1 line, record i uses gyro[i], Mag_1[i],
 // Acc_1[i] and dt_i = T[i+1] - T[i] (float64, as ExtendedKalmanFilter.py:62 computes
 // T - previousT with previousT starting at the first timestamp).
@@ -17,6 +18,7 @@
 #include <vector>
 
 #include "../../include/pekf.h"
+#include "pekf_cnum.hpp"
 
 namespace pekf {
 int set_error(int code, const char *fmt, ...);  // pekf_capi.hip
@@ -37,7 +39,7 @@ bool values(const char *line, std::vector<double> &dst, int want) {
     while (*p) {
         char *end = nullptr;
         errno = 0;
-        const double v = std::strtod(p, &end);
+        const double v = pekf::strtod_c(p, &end);
         if (end == p) return false;
         dst.push_back(v);
         ++got;

@@ -10,7 +10,8 @@
 // not the float itself (e.g. "0.1" is 0.1, not 0.100000001490116...).
 //
 //  * pekf_wire_parse: the server's own parse of such text (Parser::run's '#' test and ProcessString's
-//    length test and field splitting, strtod / strtoll as std::stod / std::stoll call them).
+//    length test and field splitting, strtod / strtoll as std::stod / std::stoll call them, strtod in the
+//    "C" locale, pekf_cnum.hpp).
 //  * pekf_f32_wire_values: for samples known only as floats, the double the server would parse from
 //    Float.toString(f).  Float.toString prints the shortest decimal that rounds to f, the closest to f
 //    among those (JDK 19+ specification; for a float whose shortest decimal has one digit it picks the
@@ -25,6 +26,7 @@
 #include <string>
 
 #include "../../include/pekf.h"
+#include "pekf_cnum.hpp"
 
 namespace pekf {
 int set_error(int code, const char *fmt, ...);  // pekf_capi.hip
@@ -41,7 +43,7 @@ double wire_value(float f) {
     for (const char *p = buf; p < r.ptr && *p != 'e'; ++p) digits += (*p >= '0' && *p <= '9');
     if (digits == 1) r = std::to_chars(buf, buf + sizeof(buf) - 1, f, std::chars_format::scientific, 1);
     *r.ptr = '\0';
-    return std::strtod(buf, nullptr);
+    return pekf::strtod_c(buf, nullptr);
 }
 
 }  // namespace
@@ -82,7 +84,7 @@ int pekf_wire_parse(const char *text, int64_t len, int64_t max_events, uint8_t *
                 const char *comma = std::strchr(p, ',');
                 char *e = nullptr;
                 errno = 0;
-                v[k] = std::strtod(p, &e);
+                v[k] = pekf::strtod_c(p, &e);
                 ok = comma && e != p && errno != ERANGE;
                 p = comma ? comma + 1 : p;
             }
