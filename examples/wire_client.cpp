@@ -63,7 +63,8 @@ int parse(const std::string &text, Messages &m) {
     return 0;
 }
 
-// One FP64 event {x, y, z, bits(t) | type} (PEKF_EV_F64_EVENTS); type 3 (no sample) pads short streams.
+// One FP64 event {x, y, z, bits(t) | type} (PEKF_EV_F64_EVENTS); xyz = NULL: no message at all, w = the
+// bits of -0.0 with type 3, which pads short streams.
 void put_event(double *e, const double *xyz, int64_t t, unsigned type) {
     e[0] = xyz ? xyz[0] : 0.0;
     e[1] = xyz ? xyz[1] : 0.0;
@@ -71,7 +72,7 @@ void put_event(double *e, const double *xyz, int64_t t, unsigned type) {
     const double td = (double)t;
     uint64_t bits;
     std::memcpy(&bits, &td, 8);
-    bits |= type;
+    bits = xyz ? bits | type : 0x8000000000000003ull;
     std::memcpy(&e[3], &bits, 8);
 }
 
@@ -94,7 +95,7 @@ int planes(const std::vector<Messages> &ms, uint8_t p, void **dev, int64_t *E, s
             if (e < (int64_t)idx[k].size()) {
                 const int64_t i = idx[k][e];
                 // a sensor type other than 0 / 1 / 2 matches no sensor in the server's state machine
-                // (KFS/Parser.cpp:148-219): no sample, like the padding (wire.events_from_wire)
+                // (KFS/Parser.cpp:148-219) but is a message (in phase 2 it moves the time, :36-62): type 3
                 const unsigned ty = ms[k].type[i] <= 2 ? ms[k].type[i] : 3u;
                 put_event(dst, &ms[k].xyz[3 * i], ms[k].t[i], ty);
             } else {

@@ -248,7 +248,8 @@ int pekf_log_read64(const char *path, int64_t n_records, double *gyro, double *a
  * ([r_max][batch], the layout pekf_run_dev reads), dt = gyro time - previous record's (initially
  * t_init[b]).  Events: ev_planes float4 [n_events][batch] {x, y, z, bits(word)}, 16 B each, with
  * word = (ns since the filter's previous event, first: since t_init[b]) << 2 | type (0 acc, 1 gyro,
- * 2 mag), so gaps must be < 2^30 ns.  init[batch*6] = raw phase-2 means {acc xyz, mag xyz}
+ * 2 mag, 3 a message no sensor takes: skipped in phase 3, a message like any other in phase 2), so gaps
+ * must be < 2^30 ns (and a type-3 message's > 0: word 3 is the time event below).  init[batch*6] = raw phase-2 means {acc xyz, mag xyz}
  * (Parser.cpp:44-53); refs[batch*6] receives their normalised values (the filter's acc0 / mag0).
  * A filter whose init is not finite (pekf_frontend_init_dev's "not ready") produces no record (counts 0).
  * *dev_error |= 1 if a record dt does not fit 31 bits, 2 if a filter had more than r_max records. */
@@ -270,8 +271,9 @@ int pekf_frontend_dev(int64_t batch, int64_t n_events, const void *ev_planes, co
  * [n_events][batch], 32 B per event, {x, y, z, w} where x, y, z are the sample as the server parses it
  * (std::stod of the phone's text, KFS/Parser.cpp:23-25 -- in general not the f32 the phone measured) and
  * w's bits are those of the event's absolute time in ns as a float64 (an integer, |t| < 2^51) with the
- * type (0 acc, 1 gyro, 2 mag, 3 no sample) in its two lowest bits.  t_init / t_start are times on the
- * same clock.  Any gap or clock step is just the next event's time (no time events); records are FP64
+ * type (0 acc, 1 gyro, 2 mag, 3 a message no sensor takes) in its two lowest bits; w = the bits of -0.0
+ * with type 3 (0x8000000000000003, which no time packs to) is no message at all, for padding.  t_init /
+ * t_start are times on the same clock.  Any gap or clock step is just the next event's time (no time events); records are FP64
  * throughout, their dt any float64.  Host packing: pekf_wire_parse (wire text) or pekf_f32_wire_values
  * (f32 samples -> the doubles the server would parse). */
 #define PEKF_EV_F64_EVENTS 0x4u
@@ -312,8 +314,9 @@ int pekf_live_ext_dev(int64_t batch, int64_t n_events, const void *ev_planes, co
  * filter, the mean and sample variance of the first n_avg (the server: 100) samples of each sensor type,
  * and the time phase 3 continues from.  Events as for pekf_frontend_dev (ev_planes [n_events][batch], word
  * = gap << 2 | type, the first gap from t_start[b]).  A filter is ready once every sensor has had a sample
- * after its first n_avg and one more event has arrived (the KalmanFilter construction, :41-55); later
- * events move t_init to their time (:57-62).  Outputs (device): init[batch*6] = raw means {acc xyz, mag
+ * after its first n_avg and one more message of any type (3 included) has arrived (the KalmanFilter
+ * construction, :41-55); later messages move t_init to their time (:57-62).  Time events and FP64
+ * no-message events are not messages.  Outputs (device): init[batch*6] = raw means {acc xyz, mag
  * xyz} and t_init[batch] -- pekf_frontend_dev's init / t_init --, ready[batch] (0: not enough phase-2
  * events; init is then NaN), stats[batch*12] (optional) = {gyro mean, acc / mag / gyro variance};
  * with stats NULL the second pass over the events (the variances) is skipped. */

@@ -29,6 +29,7 @@ from __future__ import annotations
 import numpy as np
 
 ACC, GYRO, MAG = 0, 1, 2
+OTHER, NONE = 3, 4  # a message no sensor takes; no message at all (padding)
 
 
 def _interp(t1, t2, t3, y1, y2):
@@ -123,7 +124,10 @@ def initial_values(types, values, times, n_avg=100):
     sum / n, then sum((x - mean)^2) / (n - 1), InitialValues.cpp:20-66) and the sensor counts as
     initialised at its next sample; the first event after all three are initialised builds the
     KalmanFilter at its time, and every later one moves acc_0 / mag_0's time and previousT to its
-    own (:41-62).  PARITY UNPINNED (C++ source that cannot be built here, no fixtures)."""
+    own (:41-62).  PARITY UNPINNED (C++ source that cannot be built here, no fixtures).
+    Every message counts, whatever its type (a Type char no sensor matches, here 3, adds no sample but
+    builds the filter or moves its time once all three are initialised); type NONE (4) is no message
+    (stream padding) and is skipped."""
     keys = (ACC, GYRO, MAG)
     sums = {k: [0.0, 0.0, 0.0] for k in keys}
     samples = {k: [] for k in keys}
@@ -131,7 +135,7 @@ def initial_values(types, values, times, n_avg=100):
     kalman, t_last = False, None
     for ty, v, t in zip(types, values, times):
         ty, t = int(ty), int(t)
-        if ty not in keys:  # not a message (type 3: stream padding / a clock step)
+        if ty == NONE:
             continue
         if not all(done.values()):
             if ty in sums:

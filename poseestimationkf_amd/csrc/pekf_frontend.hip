@@ -249,8 +249,10 @@ __global__ __launch_bounds__(64) void k_frontend(int64_t batch, int64_t n_events
 // from init = {mean acc, mean mag} at t_init = the last phase-2 event's time -- exactly the inputs of
 // pekf_frontend_dev.  Same event planes as phase 3; two passes over them (the variance needs the
 // mean first, as InitialValues::compute_mean_and_variance has it).
+// Every message counts, whatever its sensor type: one no sensor takes (type 3) adds no sample but, once
+// all three are initialised, builds the filter or moves its time as any other (Parser.cpp:36-62).
 // EV64: FP64 events (the server's stod doubles are what it averages, Parser.cpp:23-25,84-140); their
-// times are absolute, and a type-3 event carries no sample.
+// times are absolute, and the no-message event (padding, ev64_none) is skipped.
 template <bool EV64 = false>
 __global__ __launch_bounds__(kFeBlock) void k_frontend_init(int64_t batch, int64_t n_events,
                                                             const std::conditional_t<EV64, double4, float4> *__restrict__ ev,
@@ -294,8 +296,8 @@ __global__ __launch_bounds__(kFeBlock) void k_frontend_init(int64_t batch, int64
             const EvT v4 = r[k];
             int ty;
             if constexpr (EV64) {
+                if (ev64_none(v4)) continue;  // no message
                 ty = (int)ev64_type(v4);
-                if (ty == 3) continue;  // no sample
                 t = (int64_t)ev64_time(v4);
             } else {
                 const uint32_t word = __float_as_uint(v4.w);

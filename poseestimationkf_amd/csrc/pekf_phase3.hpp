@@ -93,16 +93,21 @@ struct RawRecT<V3> {
 };
 
 // An FP64 event {x, y, z, w}: w's bits are those of the event's time in ns as a float64 (an integer of
-// magnitude < 2^51, so its two lowest mantissa bits are zero) with the type in those two bits (3: no
-// sample, e.g. padding).  Absolute times: any gap or clock step is just the next event's time.
+// magnitude < 2^51, so its two lowest mantissa bits are zero) with the type in those two bits (3: a
+// message no sensor takes).  Absolute times: any gap or clock step is just the next event's time.  No
+// message at all (padding) is w = the bits of -0.0 with type 3, which no time packs to.
 __device__ __forceinline__ uint32_t ev64_type(const double4 &e) {
     return (uint32_t)__double_as_longlong(e.w) & 3u;
 }
 __device__ __forceinline__ double ev64_time(const double4 &e) {
     return __longlong_as_double(__double_as_longlong(e.w) & ~3ll);
 }
-// the padding event (type 3 at time 0: moves nothing)
-__device__ __forceinline__ double4 ev64_null() { return make_double4(0.0, 0.0, 0.0, __longlong_as_double(3ll)); }
+// no message (padding: moves nothing in either phase)
+constexpr unsigned long long kEv64None = 0x8000000000000003ull;
+__device__ __forceinline__ double4 ev64_null() { return make_double4(0.0, 0.0, 0.0, __longlong_as_double((long long)kEv64None)); }
+__device__ __forceinline__ bool ev64_none(const double4 &e) {
+    return (unsigned long long)__double_as_longlong(e.w) == kEv64None;
+}
 
 // The padding event of either form: f32 -- a zero-step time event {0, 0, 0, word 3}; FP64 -- ev64_null.
 template <typename EvT>

@@ -304,6 +304,8 @@ def generate_events(ids, n_events, seed=DEFAULT_SEED, params=SynthParams()):
 
 EV_DT_BITS = 30  # event word = (ns since the previous event << 2) | type
 EV_TIME = 3      # a time event: word == 3, x / y = the float64 clock step (include/pekf.h PEKF_EV_TIME)
+EV_OTHER = 3     # in an event dict: a message of no sensor type (the server parses it, no sensor takes it)
+EV_NONE = 4      # in an event dict: no message at all (padding of a short stream), only its time
 
 
 def pack_events(ev):
@@ -313,34 +315,51 @@ def pack_events(ev):
     event (the first one: to t_init).  A gap the 30-bit field cannot hold (a pause of 2^30 ns or
     more, or a clock that steps back) becomes a time event -- word 3, the gap as a float64 in the
     x / y bits -- followed by the event itself with gap 0; every filter's stream is then padded to
-    the longest with zero-step time events (E' = E + the most time events any filter needs)."""
+    the longest with zero-step time events (E' = E + the most time events any filter needs).
+    Type EV_OTHER (3, a message no sensor takes: it still counts as a message in phase 2, as every
+    message the server parses does, KFS/Parser.cpp:36-62) needs a nonzero gap field, since word 3 is
+    the time event: at a gap of 0 (or one the field cannot hold) it goes after a time event of
+    gap - 1 ns with a gap field of 1.  Type EV_NONE (4, no message) is packed as a time event of its
+    gap: the clock moves, no message is seen."""
     E, K = ev["types"].shape
+    types = np.asarray(ev["types"], np.uint64)
+    if types.size and int(types.max()) > EV_NONE:
+        raise ValueError("event types are 0 acc, 1 gyro, 2 mag, 3 a message of no sensor type, 4 no message")
+    values = np.asarray(ev["values"], np.float32)
     times = np.asarray(ev["times"], np.int64)
     prev = np.concatenate([np.asarray(ev["t_init"], np.int64)[None, :], times[:-1]], axis=0)
     gap = times - prev
+    none = types == EV_NONE
     long_gap = (gap < 0) | (gap >= (1 << EV_DT_BITS))
-    gap_field = np.where(long_gap, 0, gap)
-    word = ((gap_field.astype(np.uint64) << np.uint64(2)) | np.asarray(ev["types"], np.uint64)).astype(np.uint32)
-    if not long_gap.any():
+    other0 = (types == EV_OTHER) & (long_gap | (gap == 0))
+    insert = (long_gap | other0) & ~none             # a time event goes before the event
+    gap_field = np.where(insert, other0.astype(np.int64), gap)
+    word = np.where(none, np.uint64(EV_TIME),
+                    (gap_field.astype(np.uint64) << np.uint64(2)) | types).astype(np.uint32)
+    # an EV_NONE entry is itself a time event: x / y the float64 step
+    step_none = gap.astype(np.float64).view(np.uint32).reshape(E, K, 2).view(np.float32)
+    vals = np.where(none[..., None], np.concatenate([step_none, np.zeros((E, K, 1), np.float32)], axis=2), values)
+    if not insert.any():
         planes = np.empty((E, K, 4), np.float32)
-        planes[..., :3] = ev["values"]
+        planes[..., :3] = vals
         planes[..., 3] = word.view(np.float32)
         return planes
-    shift = np.cumsum(long_gap, axis=0)            # time events inserted up to and including event e
+    shift = np.cumsum(insert, axis=0)              # time events inserted up to and including event e
     planes = np.zeros((E + int(shift[-1].max()), K, 4), np.float32)
     planes[..., 3] = np.uint32(EV_TIME).reshape(1).view(np.float32)[0]   # padding: zero-step time events
     cols = np.broadcast_to(np.arange(K), (E, K))
     row = np.arange(E)[:, None] + shift            # each event's row in the packed stream
-    planes[row, cols, :3] = ev["values"]
+    planes[row, cols, :3] = vals
     planes[row, cols, 3] = word.view(np.float32)
-    e, k = np.nonzero(long_gap)
-    step = gap[e, k].astype(np.float64).view(np.uint32).reshape(-1, 2)   # float64 halves (low, high)
+    e, k = np.nonzero(insert)
+    step = (gap[e, k] - gap_field[e, k]).astype(np.float64).view(np.uint32).reshape(-1, 2)   # float64 halves
     planes[row[e, k] - 1, k, 0] = step[:, 0].view(np.float32)
     planes[row[e, k] - 1, k, 1] = step[:, 1].view(np.float32)
     return planes
 
 
 EV64_T_LIMIT = 1 << 51  # FP64 events: |t| < 2^51 ns keeps the two lowest mantissa bits of t free for the type
+EV64_NONE_W = 0x8000000000000003  # FP64 events: w of "no message" (the bits of -0.0 with type 3; include/pekf.h)
 
 
 def pack_events64(ev, values=None):
@@ -348,20 +367,24 @@ def pack_events64(ev, values=None):
     (PEKF_EV_F64_EVENTS, include/pekf.h): x, y, z the sample as float64 -- `values` if given, else
     ev["values64"] if present (e.g. wire.parse's doubles), else ev["values"] widened -- and w's bits
     those of the event's absolute time in ns as a float64 with the type in its two lowest bits.  32 B
-    per event; times are absolute, so no time events are needed for any gap or clock step."""
+    per event; times are absolute, so no time events are needed for any gap or clock step.  Type
+    EV_OTHER (3) is a message of no sensor type at its time; EV_NONE (4, no message) packs as
+    {0, 0, 0, EV64_NONE_W}."""
     types = np.asarray(ev["types"], np.uint64)
     times = np.asarray(ev["times"], np.int64)
     if values is None:
         values = ev["values64"] if "values64" in ev else ev["values"]
     values = np.asarray(values, np.float64)
-    if times.size and int(np.abs(times).max()) >= EV64_T_LIMIT:
+    if types.size and int(types.max()) > EV_NONE:
+        raise ValueError("event types are 0 acc, 1 gyro, 2 mag, 3 a message of no sensor type, 4 no message")
+    none = types == EV_NONE
+    if times.size and int(np.abs(np.where(none, 0, times)).max()) >= EV64_T_LIMIT:
         raise ValueError("FP64 events need |t| < 2^51 ns")
-    if types.size and int(types.max()) > 3:
-        raise ValueError("event types are 0 acc, 1 gyro, 2 mag, 3 none")
     E, K = types.shape
     planes = np.empty((E, K, 4), np.float64)
-    planes[..., :3] = values
-    planes[..., 3] = (times.astype(np.float64).view(np.uint64) | types).view(np.float64)
+    planes[..., :3] = np.where(none[..., None], 0.0, values)
+    w = times.astype(np.float64).view(np.uint64) | np.where(none, 0, types)
+    planes[..., 3] = np.where(none, np.uint64(EV64_NONE_W), w).view(np.float64)
     return planes
 
 
@@ -386,4 +409,4 @@ def c1_timestamps(dt_ns, t0_ns=1_234_567_890_123):
 
 __all__ = ["DEFAULT_SEED", "SynthParams", "Records", "philox4x32", "reference_vectors", "generate",
            "pack_planes", "unpack_planes", "refs_array", "window_bytes", "c1_timestamps",
-           "MISSING_BIT", "DT_MASK", "DT_ESCAPE", "pack_events", "pack_events64", "has_time_events", "EV_TIME"]
+           "MISSING_BIT", "DT_MASK", "DT_ESCAPE", "pack_events", "pack_events64", "has_time_events", "EV_TIME", "EV_OTHER", "EV_NONE", "EV64_NONE_W"]

@@ -22,6 +22,7 @@ import ctypes
 
 import numpy as np
 
+from . import synth
 from ._lib import check, lib
 
 
@@ -96,18 +97,18 @@ def events_text(types, values, times, phase=3):
 def events_from_wire(texts, init_acc, init_mag, t_init, phase=3):
     """Per-filter wire texts -> the engine's event dict (types (E, K), values64 (E, K, 3) the server's
     doubles, times (E, K), init_acc / init_mag (K, 3), t_init (K,)).  Messages of other phases are
-    dropped; streams of different lengths are padded with type-3 events (no sample), and a message whose
-    sensor type is not 0 / 1 / 2 becomes one too (the server's state machine matches no sensor for it,
-    KFS/Parser.cpp:148-219)."""
+    dropped; a message whose sensor type is not 0 / 1 / 2 keeps its time as type synth.EV_OTHER (3): no
+    sensor takes its sample (KFS/Parser.cpp:148-219), but in phase 2 it is a message like any other
+    (:36-62); streams of different lengths are padded with synth.EV_NONE (4): no message at all."""
     ps = [parse(t) for t in texts]
     ps = [{k: v[p["phase"] == phase] for k, v in p.items()} for p in ps]
     E, K = max((len(p["types"]) for p in ps), default=0), len(ps)
-    types = np.full((E, K), 3, np.uint32)
+    types = np.full((E, K), synth.EV_NONE, np.uint32)
     vals = np.zeros((E, K, 3), np.float64)
     times = np.zeros((E, K), np.int64)
     for k, p in enumerate(ps):
         n = len(p["types"])
-        types[:n, k] = np.where(p["types"] <= 2, p["types"], 3)
+        types[:n, k] = np.where(p["types"] <= 2, p["types"], synth.EV_OTHER)
         vals[:n, k] = p["values"]
         times[:n, k] = p["times"]
         times[n:, k] = p["times"][-1] if n else int(np.asarray(t_init).reshape(-1)[k])

@@ -95,6 +95,50 @@ def test_frontend_kernel_vs_oracle(eng):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("events", ["f32", "f64"])
+def test_frontend_other_messages_and_padding(eng, events):
+    """Phase 3 skips a message no sensor takes (EV_OTHER, Parser.cpp:148-219 matches no Type) -- also one
+    at the previous event's time or after a long pause (f32 events: time events around it) -- and
+    padding (EV_NONE): the records equal the restatement's on the streams with them, and the fused kernel
+    equals the split pipeline bit for bit."""
+    K, E = 200, 900
+    ev = synth.generate_events(np.arange(K), E, seed=17)
+    ty, t = ev["types"].copy(), ev["times"].copy()
+    rng = np.random.default_rng(17)
+    for k in range(K):
+        for e in rng.choice(np.arange(1, E - 100), 12, replace=False):
+            ty[e, k] = synth.EV_OTHER
+            if k % 3 == 0:
+                t[e:, k] -= t[e, k] - t[e - 1, k]
+            elif k % 3 == 1:
+                t[e:, k] += 3 << 30
+        if k % 4 == 1:
+            ty[E - 90:, k] = synth.EV_NONE
+    ev = dict(ev, types=ty, times=t)
+    win, counts = eng.run_frontend(ev, events=events)
+    for k in range(0, K, 7):
+        og, odt, oa, om = _oracle_records(ev, k, server=events == "f64")
+        r = len(odt)
+        assert counts[k] == r and r > 20
+        if events == "f64":
+            g, dt, a, m, _ = win.download_filters([k])
+            assert np.array_equal(g[:r, 0], og) and np.array_equal(dt[:r, 0], odt.astype(np.float64))
+            assert np.abs(a[:r, 0] - oa).max() < 1e-15 and np.abs(m[:r, 0] - om).max() < 1e-15
+        else:
+            rec = win.download_filters([k])
+            assert np.array_equal(rec.gyro[:r, 0], og.astype(np.float32))
+            assert np.array_equal(rec.dt_ns[:r, 0], odt.astype(np.float64))
+            assert _f32_ulps(rec.acc[:r, 0], oa) <= 1 and _f32_ulps(rec.mag[:r, 0], om) <= 1
+    split = eng.BatchedEKF(K)
+    split.run(win)
+    fused = eng.BatchedEKF(K)
+    c, _ = fused.run_events(ev, records="f64" if events == "f64" else "f32", events=events)
+    assert np.array_equal(c, counts)
+    assert np.array_equal(fused.get_state()[0], split.get_state()[0])
+    assert np.array_equal(fused.get_state()[1], split.get_state()[1])
+
+
+@pytest.mark.gpu
 def test_events_to_filter_end_to_end(eng, oracle_c):
     """raw events -> front-end kernel -> fused filter, vs oracle front-end -> C oracle filter."""
     K, E = 256, 1500
@@ -270,6 +314,87 @@ def test_oracle_initial_values_match_numpy_statistics():
             x = ev["values"][:, k][ev["types"][:, k] == ty][:100].astype(np.float64)
             assert np.allclose(o[name], x.mean(0), rtol=1e-15, atol=1e-12)
             assert np.allclose(o["var_" + name], x.var(0, ddof=1), rtol=1e-12, atol=1e-15)
+
+
+def test_oracle_initial_values_other_messages_and_padding():
+    """Any message counts in phase 2 (Parser.cpp:36-62 switches on the phase, not the sensor type): one
+    no sensor takes (EV_OTHER) adds no sample but builds the filter or moves its time; no message
+    (EV_NONE, padding) does neither."""
+    A, G, M, O, N = synth.EV_ACC, synth.EV_GYRO, synth.EV_MAG, synth.EV_OTHER, synth.EV_NONE
+    spec = [(A, 10), (A, 10), (G, 10), (G, 10), (M, 10), (M, 10), (A, 10), (G, 10), (M, 10)]
+    for tail, ready, t_last in (([(O, 10)], True, 100), ([(N, 10)], False, None), ([(N, 10), (O, 30)], True, 130),
+                                ([(O, 10), (O, 0), (N, 50)], True, 100)):
+        ev = _events(1, spec + tail)
+        o = fe.initial_values(ev["types"][:, 0], ev["values"][:, 0], ev["times"][:, 0], n_avg=2)
+        assert o["ready"] == ready, tail
+        assert o["t_init"] == (None if t_last is None else synth.T_INIT_NS + t_last), tail
+    # an EV_OTHER message before the sensors are initialised is no sample
+    ev = _events(1, [(O, 10)] * 3 + spec + [(A, 10)])
+    o = fe.initial_values(ev["types"][:, 0], ev["values"][:, 0], ev["times"][:, 0], n_avg=2)
+    r = fe.initial_values(ev["types"][3:, 0], ev["values"][3:, 0], ev["times"][3:, 0], n_avg=2)
+    assert o["ready"] and o == r
+
+
+def _kalman_event(types, n_avg):
+    """The index of the phase-2 event that builds the KalmanFilter (Parser.cpp:41-55), or None."""
+    cnt, done = {0: 0, 1: 0, 2: 0}, {0: False, 1: False, 2: False}
+    for i, ty in enumerate(types):
+        ty = int(ty)
+        if all(done.values()):
+            return i
+        if ty in cnt:
+            if cnt[ty] < n_avg:
+                cnt[ty] += 1
+            else:
+                done[ty] = True
+    return None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("events", ["f32", "f64"])
+def test_frontend_init_other_messages_and_padding(eng, events):
+    """Phase 2 on streams holding messages no sensor takes (EV_OTHER) -- among them the one that builds
+    the filter, some at the previous event's time (f32 events: gap 0 needs a time event before it) or
+    after a pause of 2^30 ns and more -- and padding (EV_NONE) after the last message: the kernel against
+    the restatement, bit for bit."""
+    from poseestimationkf_amd import wire
+    K, E, n_avg = 96, 700, 100
+    ev = synth.generate_events(np.arange(K), E, seed=13)
+    ty, t = ev["types"].copy(), ev["times"].copy()
+    rng = np.random.default_rng(13)
+    for k in range(K):
+        i = _kalman_event(ty[:, k], n_avg)
+        assert i is not None
+        if k % 2 == 0:
+            ty[i, k] = synth.EV_OTHER                         # the message that builds the filter
+        for e in rng.choice(np.arange(1, E - 60), 5, replace=False):
+            ty[e, k] = synth.EV_OTHER
+            if k % 3 == 0:
+                t[e:, k] -= t[e, k] - t[e - 1, k]             # at the previous event's time
+            elif k % 3 == 1:
+                t[e:, k] += 3 << 30                           # after a long pause
+        if k % 4 == 1:
+            ty[E - 50:, k] = synth.EV_NONE                    # a shorter stream, padded
+        if k % 8 == 5:
+            i = _kalman_event(ty[:, k], n_avg)
+            ty[i:, k] = synth.EV_NONE                         # ends as the last sensor initialises: not ready
+    ev = dict(ev, types=ty, times=t)
+    got = eng.frontend_init(ev, n_avg=n_avg, events=events)
+    vals = wire.server_values(ev["values"]) if events == "f64" else ev["values"].astype(np.float64)
+    n_ready = 0
+    for k in range(K):
+        o = fe.initial_values(ty[:, k], vals[:, k], t[:, k], n_avg=n_avg)
+        assert got["ready"][k] == o["ready"], k
+        assert not (k % 8 == 5 and o["ready"])
+        if not o["ready"]:
+            assert np.isnan(got["init"][k]).all()
+            continue
+        n_ready += 1
+        assert got["t_init"][k] == o["t_init"]
+        assert np.array_equal(got["init"][k], np.array(o["acc"] + o["mag"]))
+        for name in ("acc", "mag", "gyro"):
+            assert np.array_equal(got["var_" + name][k], np.array(o["var_" + name]))
+    assert n_ready >= K // 2
 
 
 @pytest.mark.gpu

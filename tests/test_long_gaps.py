@@ -78,6 +78,39 @@ def test_pack_events_time_events_round_trip():
     assert not synth.has_time_events(synth.pack_events(synth.generate_events(np.arange(K), E, seed=3)))
 
 
+def test_pack_events_other_and_none_round_trip():
+    """A message no sensor takes (EV_OTHER) keeps its time and stays a message -- also at the previous
+    event's time and after a long pause, where word 3 would read as a time event (it goes after a time
+    event of gap - 1 ns, with a gap field of 1) --; no message (EV_NONE) only moves the clock.  FP64 events:
+    EV_OTHER is type 3 at its time, EV_NONE the -0.0 sentinel."""
+    K, E = 5, 30
+    ev = synth.generate_events(np.arange(K), E, seed=5)
+    ty, t = ev["types"].copy(), ev["times"].copy()
+    ty[3, 0] = synth.EV_OTHER
+    ty[7, 1] = synth.EV_OTHER
+    t[7:, 1] -= t[7, 1] - t[6, 1]                      # at the previous event's time: gap 0
+    ty[9, 2] = synth.EV_OTHER
+    t[9:, 2] += 3 << 30                                 # after a pause the gap field cannot hold
+    ty[0, 3] = synth.EV_OTHER                           # the first event, at t_init
+    t[:, 3] -= t[0, 3] - ev["t_init"][3]
+    ty[E - 6:, 3] = synth.EV_NONE                       # padding
+    ty[10, 4] = synth.EV_NONE
+    t[10:, 4] += 5 << 30                                # a no-message clock step past the gap field
+    ev = dict(ev, types=ty, times=t)
+    planes = synth.pack_events(ev)
+    got = _decode_events(planes, ev["t_init"])
+    for k in range(K):
+        assert got[k] == [(int(ty[e, k]), int(t[e, k])) for e in range(E) if ty[e, k] != synth.EV_NONE]
+    p64 = synth.pack_events64(ev)
+    w = np.ascontiguousarray(p64[..., 3]).view(np.uint64)
+    none = ty == synth.EV_NONE
+    assert np.all(w[none] == np.uint64(synth.EV64_NONE_W)) and np.all(p64[none][:, :3] == 0)
+    assert np.array_equal(w[~none] & np.uint64(3), ty[~none].astype(np.uint64))
+    assert np.array_equal((w[~none] & ~np.uint64(3)).view(np.float64), t[~none].astype(np.float64))
+    with pytest.raises(ValueError, match="event types"):
+        synth.pack_events(dict(ev, types=np.full_like(ty, 5)))
+
+
 def test_records_dt_ns_and_oracles_agree_on_escapes(oracle_c):
     rec = _escaped_records(K=16, W=40)
     dt = rec.dt_ns

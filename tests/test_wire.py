@@ -92,18 +92,23 @@ def test_events_from_wire_pads_ragged_streams():
              for k in range(3)]
     got = wire.events_from_wire(texts, ev["init_acc"], ev["init_mag"], ev["t_init"])
     assert got["types"].shape == (50, 3)
-    assert np.all(got["types"][40:, 0] == 3) and np.all(got["types"][:, 2] != 3)
+    assert np.all(got["types"][40:, 0] == synth.EV_NONE) and np.all(got["types"][:, 2] <= 2)
+    # a message of a sensor type no sensor takes keeps its time, as a message (EV_OTHER)
     odd = wire.events_from_wire([wire.message(3, 7, [1, 2, 3], 5) + texts[0]], ev["init_acc"][:1],
                                 ev["init_mag"][:1], ev["t_init"][:1])
-    assert odd["types"][0, 0] == 3 and np.array_equal(odd["types"][1:41, 0], got["types"][:40, 0])
+    assert odd["types"][0, 0] == synth.EV_OTHER and odd["times"][0, 0] == 5
+    assert np.array_equal(odd["types"][1:41, 0], got["types"][:40, 0])
     assert _same_bits(got["values64"][:50, 2], wire.server_values(ev["values"][:, 2]))
-    # padding is no message: the restatements skip it
+    # padding is no message: the restatements skip it, in phase 3 and in phase 2
     k = 0
     o = fe.run_frontend(got["types"][:, k], got["values64"][:, k], got["times"][:, k], ev["init_acc"][k],
                         ev["init_mag"][k], ev["t_init"][k])
     o40 = fe.run_frontend(got["types"][:40, k], got["values64"][:40, k], got["times"][:40, k], ev["init_acc"][k],
                           ev["init_mag"][k], ev["t_init"][k])
     assert all(np.array_equal(a, b) for a, b in zip(o, o40))
+    i = fe.initial_values(got["types"][:, k], got["values64"][:, k], got["times"][:, k], n_avg=2)
+    i40 = fe.initial_values(got["types"][:40, k], got["values64"][:40, k], got["times"][:40, k], n_avg=2)
+    assert i["ready"] and i == i40
 
 
 def test_pack_events64_layout():
