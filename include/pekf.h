@@ -239,6 +239,17 @@ int pekf_log_read_ext(const char *path, int64_t n_records, float *gyro, float *a
  * T[i+1] - T[i] (any value), acc0/mag0[3], t0 (may be NULL). */
 int pekf_log_read64(const char *path, int64_t n_records, double *gyro, double *acc, double *mag, double *dt_ns,
                     double *acc0, double *mag0, double *t0);
+/* The emit side: writes (truncates) path with the lines the server's KalmanFilter writes for one client
+ * (KFS/KalmanFilter.cpp WriteTextFile, :335-340): mag_0 / acc_0 (:26-33), the initial q_gyro / X_k /
+ * Wahba_quart (:55-67), then per record gyro (:265-277), T (the first record: previousT before it,
+ * :136-141), q_gyro (:150-153), Mag_1 / Acc_1 (:279-303), X_k / Wahba_quart (:180-183).  Numbers as
+ * std::to_string prints them in the "C" locale ("%f", the integer ns times).  t_ns[n_records + 1] = T0
+ * then one time per record; gyro/acc/mag[n*3]; acc0/mag0[3]; q_gyro / x_k / wahba[n*4] may be NULL
+ * (written as zeros).  Replaces the server's logging for traces made elsewhere (a batch run's inputs and
+ * outputs, synthetic streams); pekf_log_read* and ReadFile.getData read it back. */
+int pekf_log_write(const char *path, int64_t n_records, const int64_t *t_ns, const double *gyro, const double *acc,
+                   const double *mag, const double *acc0, const double *mag0, const double *q_gyro, const double *x_k,
+                   const double *wahba);
 
 /* ---------------- server front-end: raw phone events -> records ----------------
  * Device kernel.  Per filter, the phase-3 state machine of Parser::WriteKalmanFilterMeasurement

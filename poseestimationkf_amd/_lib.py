@@ -124,6 +124,7 @@ SIGNATURES = {
     "pekf_log_read": [ctypes.c_char_p, _i64, _vp, _vp, _vp, _vp, _dp, _dp, _dp],
     "pekf_log_read_ext": [ctypes.c_char_p, _i64, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_i64), _dp, _dp, _dp],
     "pekf_log_read64": [ctypes.c_char_p, _i64, _vp, _vp, _vp, _vp, _dp, _dp, _dp],
+    "pekf_log_write": [ctypes.c_char_p, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "pekf_quat_to_rpy_dev": [_i64, _vp, _vp, _vp],
     "pekf_synth_dev": [_i64, _i64, _i64, _u32, _int, _dp, _dbl, _vp, _vp, _vp, _vp, _vp],
     "pekf_comm_version": [_ip],

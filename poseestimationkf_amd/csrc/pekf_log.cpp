@@ -1,5 +1,6 @@
 // pekf_log.cpp -- native ingest of the live server's text log into the 40 B record stream
-// (SURVEY.md §8f-1).  Host code (no device work): it feeds pekf_run_dev with recorded phone traces.
+// (SURVEY.md §8f-1), and its emit (pekf_log_write: the lines the server's KalmanFilter writes).  Host
+// code (no device work): it feeds pekf_run_dev with recorded phone traces.
 //
 // Line tags and precedence follow the offline reader (Python Kalman Filter/ReadFile.py:27-45):
 // mag_0, acc_0, Acc_1, Mag_1, q_gyro, gyro, any line containing 'T', Wahba_quart, X_k; values are
@@ -190,6 +191,42 @@ int pekf_log_read64(const char *path, int64_t n_records, double *gyro, double *a
 int pekf_log_read(const char *path, int64_t n_records, float *gyro, float *acc, float *mag, uint32_t *dtw,
                   double *acc0, double *mag0, double *t0) {
     return pekf_log_read_ext(path, n_records, gyro, acc, mag, dtw, nullptr, nullptr, acc0, mag0, t0);
+}
+
+int pekf_log_write(const char *path, int64_t n_records, const int64_t *t_ns, const double *gyro, const double *acc,
+                   const double *mag, const double *acc0, const double *mag0, const double *q_gyro, const double *x_k,
+                   const double *wahba) {
+    if (n_records < 0) return pekf::set_error(PEKF_ERR_INVALID, "negative size");
+    if (!path || !t_ns || !acc0 || !mag0 || (n_records > 0 && (!gyro || !acc || !mag)))
+        return pekf::set_error(PEKF_ERR_INVALID, "null pointer");
+    FILE *f = std::fopen(path, "w");
+    if (!f) return pekf::set_error(PEKF_ERR_INVALID, "cannot open log '%s': %s", path, std::strerror(errno));
+    // std::to_string is "%f" / "%lld" in the server's "C" locale, whatever this process has set
+    const locale_t prev = uselocale(pekf::c_locale());
+    static const double kZero4[4] = {0.0, 0.0, 0.0, 0.0};  // an absent side channel is written as zeros
+    auto vec = [&](const char *tag, const double *v, int n) {
+        std::fprintf(f, "%s : ", tag);
+        for (int k = 0; k < n; ++k) std::fprintf(f, k ? ",%f" : "%f", v[k]);
+        std::fputc('\n', f);
+    };
+    vec("mag_0", mag0, 3);                                           // set_mag_0 (:26-29)
+    vec("acc_0", acc0, 3);                                           // set_acc_0 (:30-33)
+    std::fputs("q_gyro : 1.0, 0.0, 0.0, 0.0\nX_k : 1.0, 0.0, 0.0, 0.0\nWahba_quart : 1.0, 0.0, 0.0, 0.0\n",
+               f);                                                   // compute_initial_params (:55-67)
+    for (int64_t i = 0; i < n_records; ++i) {
+        vec("gyro", gyro + 3 * i, 3);                                // SetAngularVelocity (:265-277)
+        if (i == 0) std::fprintf(f, "T : %lld\n", (long long)t_ns[0]);  // Prediction's first call (:136-141)
+        std::fprintf(f, "T : %lld\n", (long long)t_ns[i + 1]);          // (:150-151)
+        vec("q_gyro", q_gyro ? q_gyro + 4 * i : kZero4, 4);          // (:152-153)
+        vec("Mag_1", mag + 3 * i, 3);                                // SetMagnetometerMeasurements (:279-290)
+        vec("Acc_1", acc + 3 * i, 3);                                // SetAccelerometerMeasurements (:292-303)
+        vec("X_k", x_k ? x_k + 4 * i : kZero4, 4);                   // Correction (:180-183)
+        vec("Wahba_quart", wahba ? wahba + 4 * i : kZero4, 4);
+    }
+    uselocale(prev);
+    const bool bad = std::ferror(f) != 0;
+    if (std::fclose(f) != 0 || bad) return pekf::set_error(PEKF_ERR_INVALID, "cannot write log '%s'", path);
+    return PEKF_OK;
 }
 
 }  // extern "C"

@@ -73,6 +73,22 @@ def write_log(fh, timestamps, gyro, acc, mag, acc0, mag0, q_gyro=None, x_k=None,
             out.close()
 
 
+def write_log_native(path, timestamps, gyro, acc, mag, acc0, mag0, q_gyro=None, x_k=None, wahba=None):
+    """write_log through libpekf's pekf_log_write (the same bytes, C++ on the host, for long traces)."""
+    from ._lib import check, lib
+
+    def arr(a, shape, dtype=np.float64):
+        return None if a is None else np.ascontiguousarray(np.asarray(a, dtype).reshape(shape))
+    n = len(gyro)
+    t = arr(timestamps, (n + 1,), np.int64)
+    g, a, m = arr(gyro, (n, 3)), arr(acc, (n, 3)), arr(mag, (n, 3))
+    a0, m0 = arr(acc0, (3,)), arr(mag0, (3,))
+    sides = [arr(x, (n, 4)) for x in (q_gyro, x_k, wahba)]
+    ptr = lambda x: None if x is None else x.ctypes.data  # noqa: E731
+    check(lib.pekf_log_write(os.fsencode(path), n, ptr(t), ptr(g), ptr(a), ptr(m), ptr(a0), ptr(m0),
+                             *[ptr(x) for x in sides]))
+
+
 def _values(line):
     return [float(tok) for tok in line.split(":")[1].split(",")]
 

@@ -1,10 +1,12 @@
 // Host-only harness for the native log reader (csrc/pekf_log.cpp) under AddressSanitizer and
 // UndefinedBehaviorSanitizer (tests/test_log_sanitizers.py builds and runs it; no GPU, no HIP).
 // Each argument is a log path: scan it, then read it with and without the dt side plane, as float64
-// records, and with one record too many.  pekf::set_error (pekf_capi.hip in the library) is replaced by a printing stub.
+// records, and with one record too many; then write the float64 records back (pekf_log_write) and scan
+// the result.  pekf::set_error (pekf_capi.hip in the library) is replaced by a printing stub.
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <string>
 #include <vector>
 
 #include "pekf.h"
@@ -43,6 +45,18 @@ int main(int argc, char **argv) {
                 pekf_log_read64(argv[i], n + 1, g64.data(), a64.data(), m64.data(), dt64.data(), acc0, mag0, &t0);
             printf(" ext=%d escaped=%lld plain=%d over=%d r64=%d over64=%d", ext, (long long)esc, plain, over, r64,
                    over64);
+            if (r64 == 0) {  // the emit side: the float64 records written back, then scanned again
+                std::vector<int64_t> t(n + 1);
+                t[0] = (int64_t)t0;
+                for (int64_t k = 0; k < n; ++k) t[k + 1] = t[k] + (int64_t)dt64[k];
+                std::vector<double> xk(4 * n, 0.5);  // a side channel (the others absent: zeros)
+                const std::string out = std::string(argv[i]) + ".out";
+                const int w = pekf_log_write(out.c_str(), n, t.data(), g64.data(), a64.data(), m64.data(), acc0, mag0,
+                                             nullptr, xk.data(), nullptr);
+                int64_t n2 = -1;
+                const int s2 = pekf_log_scan(out.c_str(), &n2);
+                printf(" write=%d rescan=%d records=%lld", w, s2, (long long)n2);
+            }
         }
         printf("\n");
     }

@@ -73,6 +73,7 @@ def test_log_reader_under_sanitizers(harness, tmp_path):
     got = dict(zip(files, r.stdout.splitlines()))
     for name in ("good", "long_lines"):
         assert "scan=0 records=120 ext=0 escaped=2 plain=1 over=1 r64=0 over64=1" in got[name], got[name]
+        assert " write=0 rescan=0 records=120" in got[name], got[name]
     assert " scan=0 " in got["trunc"] and " ext=0 " in got["trunc"] and " r64=0 " in got["trunc"]
     for name in ("missing_value", "no_colon", "binary", "empty", "absent"):
         assert " scan=1 " in got[name], got[name]

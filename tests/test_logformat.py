@@ -162,3 +162,45 @@ def test_native_ingest_float64_matches_python_reader(c1_log, tmp_path):
     for x, w in zip(got[:6], want):
         assert np.array_equal(x, w)
     assert (got[1] < 0).any() and got[1].max() > 2 ** 31   # (the writer's "T : %d" keeps integer ns)
+
+
+def test_native_emit_matches_python_writer(tmp_path):
+    """pekf_log_write (C++) writes write_log's bytes -- the server's WriteTextFile lines, std::to_string's
+    "%f" -- for values of every size and sign, with and without the side channels, and the native reader
+    reads the result back at that precision."""
+    from poseestimationkf_amd._lib import PekfError
+    rng = np.random.default_rng(3)
+    n = 300
+    scale = 10.0 ** rng.integers(-9, 11, size=(n, 3))
+    g, a, m = (rng.standard_normal((n, 3)) * scale for _ in range(3))
+    g[0] = [0.0, -0.0, -1e-9]
+    a[1] = [np.inf, -np.inf, 123456789.123456789]
+    t = 1_700_000_000_000_000_000 + np.cumsum(rng.integers(-5, 20_000_000, n + 1))
+    a0, m0 = np.array([0.1, -0.2, 9.8]), np.array([20.5, -1e-7, -40.0])
+    sides = [rng.standard_normal((n, 4)) for _ in range(3)]
+    for kw in ({}, dict(zip(("q_gyro", "x_k", "wahba"), sides))):
+        py, cc = tmp_path / "py.txt", tmp_path / "c.txt"
+        logformat.write_log(str(py), t, g, a, m, a0, m0, **kw)
+        logformat.write_log_native(str(cc), t, g, a, m, a0, m0, **kw)
+        assert cc.read_bytes() == py.read_bytes()
+    # the native float64 reader gets the printed values back ("inf" included, as float() reads it)
+    import ctypes
+    from poseestimationkf_amd._lib import check, lib
+    cnt = ctypes.c_int64()
+    check(lib.pekf_log_scan(os.fsencode(str(cc)), ctypes.byref(cnt)))
+    assert cnt.value == n
+    out = [np.empty((n, 3)) for _ in range(3)]
+    dt, ra0, rm0 = np.empty(n), np.empty(3), np.empty(3)
+    check(lib.pekf_log_read64(os.fsencode(str(cc)), n, out[0].ctypes.data, out[1].ctypes.data, out[2].ctypes.data,
+                              dt.ctypes.data, ra0.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                              rm0.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), None))
+    printed = lambda x: np.vectorize(lambda v: float("%f" % v))(x)  # noqa: E731
+    for got, want in zip(out, (g, a, m)):
+        assert np.array_equal(got, printed(want))
+    assert np.array_equal(ra0, printed(a0)) and np.array_equal(rm0, printed(m0))
+    # T parsed as float64 (ReadFile.py:20,41), so ns times past 2^53 round as the reference's own reader rounds them
+    assert np.array_equal(dt, np.diff(t.astype(np.float64)))
+    with pytest.raises(PekfError, match="cannot open"):
+        logformat.write_log_native(str(tmp_path / "no" / "such" / "dir.txt"), t[:2], g[:1], a[:1], m[:1], a0, m0)
+    logformat.write_log_native(str(cc), t[:1], g[:0], a[:0], m[:0], a0, m0)   # no record: the header only
+    assert cc.read_text().count("\n") == 5
