@@ -38,14 +38,15 @@ def parse(text):
     """Wire text (str or bytes, one message per line) -> dict(phase (n,) uint8, types (n,) uint8,
     values (n, 3) float64, times (n,) int64), as the server's Parser reads it."""
     b = text.encode() if isinstance(text, str) else bytes(text)
+    # one pass: a counted message is '#' and more than 30 characters, so there are at most len / 32 + 1
+    cap = len(b) // 32 + 1
+    ph, ty = np.empty(cap, np.uint8), np.empty(cap, np.uint8)
+    xyz, t = np.empty((cap, 3), np.float64), np.empty(cap, np.int64)
     n = ctypes.c_int64()
-    check(lib.pekf_wire_parse(b, len(b), 0, None, None, None, None, ctypes.byref(n)))
+    check(lib.pekf_wire_parse(b, len(b), cap, ph.ctypes.data, ty.ctypes.data, xyz.ctypes.data, t.ctypes.data,
+                              ctypes.byref(n)))
     n = n.value
-    ph, ty = np.empty(n, np.uint8), np.empty(n, np.uint8)
-    xyz, t = np.empty((n, 3), np.float64), np.empty(n, np.int64)
-    check(lib.pekf_wire_parse(b, len(b), n, ph.ctypes.data, ty.ctypes.data, xyz.ctypes.data, t.ctypes.data,
-                              ctypes.byref(ctypes.c_int64())))
-    return dict(phase=ph, types=ty, values=xyz, times=t)
+    return dict(phase=ph[:n].copy(), types=ty[:n].copy(), values=xyz[:n].copy(), times=t[:n].copy())
 
 
 def java_float_string(f):
