@@ -46,6 +46,127 @@ double wire_value(float f) {
     return pekf::strtod_c(buf, nullptr);
 }
 
+// One parsed message: the phase and type characters, the three stod values and the stoll time.
+struct Message {
+    char ph, ty;
+    double v[3];
+    long long t;
+};
+
+// The powers of ten a double holds exactly
+constexpr double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                               1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+// A plain decimal [+-]digits[.digits][(e|E)[+-]digits] at p, immediately followed by ',' (before mend):
+// true with its value when one IEEE multiply or divide of two exact doubles gives it -- at most 19
+// significant digits with a mantissa <= 2^53 and a decimal exponent within +-22 -- which is then the
+// correctly rounded decimal, strtod's own result; false for anything else (the caller's strtod path).
+// p is left on the ','.
+bool fast_decimal(const char *&p, const char *mend, double &out) {
+    const char *q = p;
+    bool neg = false;
+    if (q < mend && (*q == '+' || *q == '-')) neg = *q++ == '-';
+    uint64_t m = 0;
+    int nd = 0, exp10 = 0;
+    bool any = false;
+    for (; q < mend && (unsigned)(*q - '0') < 10u; ++q) {
+        any = true;
+        if (m || *q != '0') {
+            if (++nd > 19) return false;
+            m = m * 10 + (uint64_t)(*q - '0');
+        }
+    }
+    if (q < mend && *q == '.') {
+        for (++q; q < mend && (unsigned)(*q - '0') < 10u; ++q) {
+            any = true;
+            if (m || *q != '0') {
+                if (++nd > 19) return false;
+                m = m * 10 + (uint64_t)(*q - '0');
+            }
+            --exp10;
+        }
+    }
+    if (!any) return false;
+    if (q < mend && (*q == 'e' || *q == 'E')) {
+        ++q;
+        bool eneg = false;
+        if (q < mend && (*q == '+' || *q == '-')) eneg = *q++ == '-';
+        int e = 0, ne = 0;
+        for (; q < mend && (unsigned)(*q - '0') < 10u; ++q) {
+            if (++ne > 4) return false;
+            e = e * 10 + (*q - '0');
+        }
+        if (!ne) return false;
+        exp10 += eneg ? -e : e;
+    }
+    if (q >= mend || *q != ',') return false;
+    if (m > (1ull << 53) || exp10 < -22 || exp10 > 22) return false;
+    const double d = exp10 < 0 ? (double)m / kPow10[-exp10] : (double)m * kPow10[exp10];
+    out = neg ? -d : d;
+    p = q;
+    return true;
+}
+
+// The client's own message form, "<phase>,<type>:<x>,<y>,<z>,t:<ns>..." with plain decimals (msg = the
+// text after '#', up to mend): parsed in place, with the server's semantics (see parse_general) for the
+// cases it takes; false for anything else.
+bool parse_fast(const char *msg, const char *mend, Message &o) {
+    o.ph = msg[0];
+    const char *s = msg + 2, *colon = s;
+    while (colon < mend && *colon != ':') {
+        if (*colon == '\0') return false;
+        ++colon;
+    }
+    if (colon >= mend) return false;
+    o.ty = colon > s ? s[0] : '\0';
+    const char *p = colon + 1;
+    for (int k = 0; k < 3; ++k) {
+        if (!fast_decimal(p, mend, o.v[k])) return false;
+        ++p;  // past the ','
+    }
+    if (mend - p < 3 || p[0] != 't' || p[1] != ':') return false;
+    const char *q = p + 2;
+    const bool neg = *q == '-';
+    if (neg) ++q;
+    long long t = 0;
+    int nd = 0;
+    for (; q < mend && (unsigned)(*q - '0') < 10u; ++q) {
+        if (++nd > 18) return false;
+        t = t * 10 + (*q - '0');
+    }
+    if (!nd) return false;
+    o.t = neg ? -t : t;
+    return true;
+}
+
+// Any message, as the server reads it: Type = the first character before the first ':'
+// (FindValues(str, ":")[0]), each value std::stod of the text before the next ',' (strtod: leading
+// blanks, a sign, hex, inf / nan, trailing text ignored; ERANGE throws), the time std::stoll of the text
+// after the first "t:" that follows.  false where the server's stod / stoll would throw.
+bool parse_general(std::string &msg, const char *text, int64_t len, Message &o) {
+    msg.assign(text, (size_t)len);
+    o.ph = msg[0];
+    const char *s = msg.c_str() + 2;  // str.substr(2): past "<phase>,"
+    const char *colon = std::strchr(s, ':');
+    o.ty = (colon && colon > s) ? s[0] : '\0';  // FindValues(str, ":")[0]
+    bool ok = colon != nullptr;
+    const char *p = ok ? colon + 1 : s;
+    for (int k = 0; ok && k < 3; ++k) {  // std::stod of the text before each ','
+        const char *comma = std::strchr(p, ',');
+        char *e = nullptr;
+        errno = 0;
+        o.v[k] = pekf::strtod_c(p, &e);
+        ok = comma && e != p && errno != ERANGE;
+        p = comma ? comma + 1 : p;
+    }
+    const char *tp = ok ? std::strstr(p, "t:") : nullptr;  // std::stoll of the text after "t:"
+    if (!tp) return false;
+    char *e = nullptr;
+    errno = 0;
+    o.t = std::strtoll(tp + 2, &e, 10);
+    return e != tp + 2 && errno != ERANGE;
+}
+
 }  // namespace
 
 extern "C" {
@@ -66,51 +187,25 @@ int pekf_wire_parse(const char *text, int64_t len, int64_t max_events, uint8_t *
     std::string msg;
     for (int64_t i = 0; i < len;) {
         // one message: up to and including its newline (the server's 100-byte frame holds the newline)
-        int64_t j = i;
-        while (j < len && text[j] != '\n') ++j;
-        const int64_t end = j < len ? j + 1 : j;
+        const char *nl = static_cast<const char *>(std::memchr(text + i, '\n', (size_t)(len - i)));
+        const int64_t end = nl ? (nl - text) + 1 : len;
         ++line;
         // Parser::run: only messages starting with '#', without it; ProcessString: longer than 30
         if (text[i] == '#' && end - i - 1 > 30) {
-            msg.assign(text + i + 1, (size_t)(end - i - 1));
-            const char ph = msg[0];
-            const char *s = msg.c_str() + 2;  // str.substr(2): past "<phase>,"
-            const char *colon = std::strchr(s, ':');
-            const char ty = (colon && colon > s) ? s[0] : '\0';  // FindValues(str, ":")[0]
-            double v[3] = {0, 0, 0};
-            bool ok = colon != nullptr;
-            const char *p = ok ? colon + 1 : s;
-            for (int k = 0; ok && k < 3; ++k) {  // std::stod of the text before each ','
-                const char *comma = std::strchr(p, ',');
-                char *e = nullptr;
-                errno = 0;
-                v[k] = pekf::strtod_c(p, &e);
-                ok = comma && e != p && errno != ERANGE;
-                p = comma ? comma + 1 : p;
-            }
-            const char *tp = ok ? std::strstr(p, "t:") : nullptr;  // std::stoll of the text after "t:"
-            long long t = 0;
-            if (tp) {
-                char *e = nullptr;
-                errno = 0;
-                t = std::strtoll(tp + 2, &e, 10);
-                ok = e != tp + 2 && errno != ERANGE;
-            } else {
-                ok = false;
-            }
-            if (!ok)  // the server's std::stod / std::stoll would throw here
+            Message m;
+            if (!parse_fast(text + i + 1, text + end, m) && !parse_general(msg, text + i + 1, end - i - 1, m))
                 return pekf::set_error(PEKF_ERR_INVALID, "wire message %lld: not '#<phase>,<type>:<x>,<y>,<z>,t:<ns>'",
-                                       (long long)line);
+                                       (long long)line);  // the server's std::stod / std::stoll would throw here
             if (fill) {
                 if (n >= max_events)
                     return pekf::set_error(PEKF_ERR_INVALID, "more than max_events = %lld messages",
                                            (long long)max_events);
-                phase[n] = (uint8_t)(ph - '0');
-                type[n] = (uint8_t)(ty - '0');
-                xyz[3 * n] = v[0];
-                xyz[3 * n + 1] = v[1];
-                xyz[3 * n + 2] = v[2];
-                t_ns[n] = (int64_t)t;
+                phase[n] = (uint8_t)(m.ph - '0');
+                type[n] = (uint8_t)(m.ty - '0');
+                xyz[3 * n] = m.v[0];
+                xyz[3 * n + 1] = m.v[1];
+                xyz[3 * n + 2] = m.v[2];
+                t_ns[n] = (int64_t)m.t;
             }
             ++n;
         }

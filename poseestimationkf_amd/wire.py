@@ -19,6 +19,8 @@ those doubles; this module produces them, natively (libpekf's host functions, cs
 from __future__ import annotations
 
 import ctypes
+import os
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -101,7 +103,14 @@ def events_from_wire(texts, init_acc, init_mag, t_init, phase=3):
     dropped; a message whose sensor type is not 0 / 1 / 2 keeps its time as type synth.EV_OTHER (3): no
     sensor takes its sample (KFS/Parser.cpp:148-219), but in phase 2 it is a message like any other
     (:36-62); streams of different lengths are padded with synth.EV_NONE (4): no message at all."""
-    ps = [parse(t) for t in texts]
+    texts = list(texts)
+    # one text per thread: the parse runs in libpekf with the GIL released (ctypes)
+    workers = max(1, min(len(texts), os.cpu_count() or 1, 32))
+    if workers > 1:
+        with ThreadPoolExecutor(workers) as pool:
+            ps = list(pool.map(parse, texts))
+    else:
+        ps = [parse(t) for t in texts]
     ps = [{k: v[p["phase"] == phase] for k, v in p.items()} for p in ps]
     E, K = max((len(p["types"]) for p in ps), default=0), len(ps)
     types = np.full((E, K), synth.EV_NONE, np.uint32)

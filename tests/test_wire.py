@@ -149,3 +149,41 @@ def test_f32_events_vs_the_servers_values_through_the_oracle_chain():
         worst_x = max(worst_x, float(np.abs(x32 - x64).max()))
     print("f32 events vs the server's values: records %.2e, final X %.2e" % (worst_rec, worst_x))
     assert 1e-9 < worst_rec < 1e-6 and 1e-11 < worst_x < 1e-7
+
+
+def test_wire_parse_number_forms():
+    """pekf_wire_parse reads the client's plain decimals in place (one IEEE multiply or divide when that is
+    exact) and anything else through strtod, as std::stod does: every form gives strtod's value -- the
+    correctly rounded decimal -- whichever way it went."""
+    rng = np.random.default_rng(11)
+    toks = []
+    for _ in range(3000):
+        nd = int(rng.integers(1, 26))
+        digits = "".join(str(d) for d in rng.integers(0, 10, nd))
+        point = int(rng.integers(0, nd + 1))
+        lead = "0" * int(rng.integers(0, 3))
+        mant = lead + digits[:point] + "." + digits[point:] if rng.random() < 0.8 else lead + digits
+        if mant.startswith(".") and rng.random() < 0.5:
+            mant = "0" + mant
+        exp = ""
+        if rng.random() < 0.4:
+            exp = rng.choice(["e", "E"]) + rng.choice(["", "+", "-"]) + str(int(rng.integers(0, 40)))
+        toks.append(rng.choice(["", "-", "+"]) + mant + exp)
+    toks += ["0.0", "-0.0", "+0.0", "1.", ".5", "-.5", "9007199254740993", "9007199254740992.0", "1e22", "1e23",
+             "123456789012345678901234567890", "0.000000000000000000000000001", "4.9e-300", "1.7976931348623157e308"]
+    toks = [t for t in toks if t.strip("+-.eE")]
+    text = "".join("#3,0:%s,%s,%s,t:%d%s\n" % (a, b, c, i, " " * 40) for i, (a, b, c) in
+                   enumerate(zip(toks[0::3], toks[1::3], toks[2::3])))
+    got = wire.parse(text)
+    want = np.array([float(t) for t in toks[: 3 * (len(toks) // 3)]]).reshape(-1, 3)
+    assert _same_bits(got["values"], want)
+    assert np.array_equal(got["times"], np.arange(len(want)))
+    # forms std::stod takes and the client never prints: strtod's values
+    odd = {" 1.5": 1.5, "0x1p3": 8.0, "inf": np.inf, "-Infinity": -np.inf, "1.5abc": 1.5, "1e": 1.0, "1e+": 1.0,
+           "\t-2.25": -2.25, "1_000": 1.0}
+    text = "".join("#3,1:%s,0.5,0.25,t:%s%s\n" % (k, t, " " * 40) for k, t in zip(odd, ["+5", " 7", "-3", "9x"] * 3))
+    got = wire.parse(text)
+    assert got["values"][:, 0].tolist() == list(odd.values()) and np.all(got["values"][:, 1:] == [0.5, 0.25])
+    assert got["times"].tolist() == [5, 7, -3, 9, 5, 7, -3, 9, 5]
+    nan = wire.parse("#3,1:nan,-NaN,0.25,t:1" + " " * 40 + "\n")["values"][0]
+    assert np.isnan(nan[0]) and np.isnan(nan[1])
