@@ -34,18 +34,6 @@ int set_error(int code, const char *fmt, ...);  // pekf_capi.hip
 
 namespace {
 
-// The double std::stod makes of Float.toString(f).
-double wire_value(float f) {
-    if (!std::isfinite(f) || f == 0.0f) return (double)f;  // "NaN", "Infinity", "0.0", "-0.0": exact
-    char buf[64];
-    auto r = std::to_chars(buf, buf + sizeof(buf) - 1, f, std::chars_format::scientific);
-    int digits = 0;
-    for (const char *p = buf; p < r.ptr && *p != 'e'; ++p) digits += (*p >= '0' && *p <= '9');
-    if (digits == 1) r = std::to_chars(buf, buf + sizeof(buf) - 1, f, std::chars_format::scientific, 1);
-    *r.ptr = '\0';
-    return pekf::strtod_c(buf, nullptr);
-}
-
 // One parsed message: the phase and type characters, the three stod values and the stoll time.
 struct Message {
     char ph, ty;
@@ -57,12 +45,13 @@ struct Message {
 constexpr double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
                                1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
 
-// A plain decimal [+-]digits[.digits][(e|E)[+-]digits] at p, immediately followed by ',' (before mend):
+// A plain decimal [+-]digits[.digits][(e|E)[+-]digits] at p, immediately followed by `term` (',' in a
+// message; '\0': the decimal ends at mend):
 // true with its value when one IEEE multiply or divide of two exact doubles gives it -- at most 19
 // significant digits with a mantissa <= 2^53 and a decimal exponent within +-22 -- which is then the
 // correctly rounded decimal, strtod's own result; false for anything else (the caller's strtod path).
-// p is left on the ','.
-bool fast_decimal(const char *&p, const char *mend, double &out) {
+// p is left on the terminator.
+bool fast_decimal(const char *&p, const char *mend, double &out, char term = ',') {
     const char *q = p;
     bool neg = false;
     if (q < mend && (*q == '+' || *q == '-')) neg = *q++ == '-';
@@ -99,7 +88,7 @@ bool fast_decimal(const char *&p, const char *mend, double &out) {
         if (!ne) return false;
         exp10 += eneg ? -e : e;
     }
-    if (q >= mend || *q != ',') return false;
+    if (term ? (q >= mend || *q != term) : q != mend) return false;
     if (m > (1ull << 53) || exp10 < -22 || exp10 > 22) return false;
     const double d = exp10 < 0 ? (double)m / kPow10[-exp10] : (double)m * kPow10[exp10];
     out = neg ? -d : d;
@@ -165,6 +154,22 @@ bool parse_general(std::string &msg, const char *text, int64_t len, Message &o) 
     errno = 0;
     o.t = std::strtoll(tp + 2, &e, 10);
     return e != tp + 2 && errno != ERANGE;
+}
+
+// The double std::stod makes of Float.toString(f): the printed decimal read back by the exact fast path
+// where it applies, else by strtod.
+double wire_value(float f) {
+    if (!std::isfinite(f) || f == 0.0f) return (double)f;  // "NaN", "Infinity", "0.0", "-0.0": exact
+    char buf[64];
+    auto r = std::to_chars(buf, buf + sizeof(buf) - 1, f, std::chars_format::scientific);
+    int digits = 0;
+    for (const char *p = buf; p < r.ptr && *p != 'e'; ++p) digits += (*p >= '0' && *p <= '9');
+    if (digits == 1) r = std::to_chars(buf, buf + sizeof(buf) - 1, f, std::chars_format::scientific, 1);
+    *r.ptr = '\0';
+    const char *p = buf;
+    double v;
+    if (fast_decimal(p, r.ptr, v, '\0')) return v;
+    return pekf::strtod_c(buf, nullptr);
 }
 
 }  // namespace
