@@ -29,10 +29,24 @@ from ._lib import check, lib
 
 
 def server_values(values):
-    """float32 samples (any shape) -> float64: std::stod(Float.toString(f)) for each."""
+    """float32 samples (any shape) -> float64: std::stod(Float.toString(f)) for each (large arrays in
+    chunks on a thread pool: the conversion runs in libpekf with the GIL released)."""
     f = np.ascontiguousarray(values, np.float32)
     out = np.empty(f.shape, np.float64)
-    check(lib.pekf_f32_wire_values(f.size, f.ctypes.data, out.ctypes.data))
+    fr, orv = f.reshape(-1), out.reshape(-1)
+    chunk = 1 << 20
+    starts = range(0, fr.size, chunk)
+
+    def run(s):
+        n = min(chunk, fr.size - s)
+        check(lib.pekf_f32_wire_values(n, fr[s:].ctypes.data, orv[s:].ctypes.data))
+    workers = max(1, min(len(starts), os.cpu_count() or 1, 32))
+    if workers > 1:
+        with ThreadPoolExecutor(workers) as pool:
+            list(pool.map(run, starts))
+    else:
+        for s in starts:
+            run(s)
     return out
 
 
