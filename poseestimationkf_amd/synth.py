@@ -333,12 +333,14 @@ def pack_events(ev):
     long_gap = (gap < 0) | (gap >= (1 << EV_DT_BITS))
     other0 = (types == EV_OTHER) & (long_gap | (gap == 0))
     insert = (long_gap | other0) & ~none             # a time event goes before the event
-    gap_field = np.where(insert, other0.astype(np.int64), gap)
-    word = np.where(none, np.uint64(EV_TIME),
-                    (gap_field.astype(np.uint64) << np.uint64(2)) | types).astype(np.uint32)
-    # an EV_NONE entry is itself a time event: x / y the float64 step
-    step_none = gap.astype(np.float64).view(np.uint32).reshape(E, K, 2).view(np.float32)
-    vals = np.where(none[..., None], np.concatenate([step_none, np.zeros((E, K, 1), np.float32)], axis=2), values)
+    gap_field = np.where(insert, other0.astype(np.int64), gap) if insert.any() else gap
+    word = ((gap_field.astype(np.uint64) << np.uint64(2)) | types).astype(np.uint32)
+    vals = values
+    if none.any():  # an EV_NONE entry is itself a time event: x / y the float64 step
+        word[none] = EV_TIME
+        vals = values.copy()
+        vals[none, :2] = gap[none].astype(np.float64).view(np.uint32).reshape(-1, 2).view(np.float32)
+        vals[none, 2] = 0.0
     if not insert.any():
         planes = np.empty((E, K, 4), np.float32)
         planes[..., :3] = vals
