@@ -340,6 +340,23 @@ int pekf_frontend_init_ext_dev(int64_t batch, int64_t n_events, const void *ev_p
                                int n_avg, double *init, int64_t *t_init, double *stats, int32_t *ready,
                                uint32_t flags, void *stream);
 
+/* The wire on the device: the clients' 100-byte frames (as MessageSender.java:217-233 sends and Server.cpp:35,84
+ * receives them: "#<phase>,<type>:<x>,<y>,<z>,t:<ns>", spaces to 99 characters, '\n') -> FP64 event planes.
+ * frames: [n_frames][batch][100] bytes (device; 4-byte aligned), phone b's frames in order along the first
+ * axis (a frame not starting with '#' is no message, e.g. padding).  Each phase-2 / phase-3 message of phone b
+ * becomes the next row of ev2 / ev3 ([e2_max][batch] / [e3_max][batch] double4, PEKF_EV_F64_EVENTS' form;
+ * type 3 for a Type no sensor takes); rows after its last message get the no-message event.  n2 / n3[batch]:
+ * messages per phase (more than e_max: *dev_error |= 2, the extra ones dropped); first_t2[batch]: the time of
+ * the first phase-2 message (t_start of pekf_frontend_init_ext_dev; 0 if none).  Values and times equal
+ * pekf_wire_parse's (std::stod / std::stoll) bit for bit for the forms the client prints -- decimals (any
+ * of at most 19 significant digits within 1e-80 .. 1e80 of the exponent; an exact big-integer path where
+ * one IEEE operation is not exact), "NaN", "Infinity", "-Infinity"; a phone's first frame in another form,
+ * or with a time of 2^51 ns or more, stops that phone: bad_frame[b] (may be NULL) = its index (-1: none),
+ * *dev_error |= 1 (parse such a stream with pekf_wire_parse).  Phase-1 and other phases are skipped. */
+int pekf_wire_events_dev(int64_t batch, int64_t n_frames, const void *frames, int64_t e2_max, int64_t e3_max,
+                         void *ev2, void *ev3, int64_t *first_t2, int32_t *n2, int32_t *n3, int32_t *bad_frame,
+                         int *dev_error, void *stream);
+
 /* ---------------- the phone -> server wire: host code ----------------
  * The Android client sends each sample as text, Float.toString of each value
  * (ASC/MessageSender.java:217-233: "#<phase>,<type>:<x>,<y>,<z>,t:<ns>" padded to 99 characters), and

@@ -506,6 +506,55 @@ def run_session(phase2, phase3, filters, n_avg=100, alpha=0.1, records="f64", ev
                 refs=refs.download((K, 6), np.float64))
 
 
+def wire_events(frames, stream=None):
+    """The clients' 100-byte wire frames -> FP64 event planes on the device (pekf_wire_events_dev).
+
+    frames: [n_frames][batch][100] uint8 (wire.frames) as a host array or a (DeviceBuffer, n_frames,
+    batch) triple.  Returns dict(ev2, ev3 DeviceBuffers [n_frames][batch] double4, E2 / E3 the most
+    messages any phone has in phase 2 / 3 -- the rows a consumer needs --, n2 / n3 (batch,) int32,
+    first_t2 DeviceBuffer (batch,) int64 (phase 2's t_start)).  Raises if a phone's frame is not in the
+    client's form (wire.parse on the host reads any form std::stod does)."""
+    if isinstance(frames, tuple):
+        fb, F, K = frames
+    else:
+        fr = np.ascontiguousarray(frames, np.uint8)
+        if fr.ndim != 3 or fr.shape[2] != 100:
+            raise ValueError("frames must be [n_frames][batch][100] bytes")
+        F, K = fr.shape[:2]
+        fb = DeviceBuffer(max(fr.nbytes, 4)).upload(fr)
+    F, K = int(F), int(K)
+    ev2, ev3 = DeviceBuffer(32 * max(F, 1) * K), DeviceBuffer(32 * max(F, 1) * K)
+    t2b, n2b, n3b, badb = DeviceBuffer(8 * K), DeviceBuffer(4 * K), DeviceBuffer(4 * K), DeviceBuffer(4 * K)
+    errb = DeviceBuffer(4).upload(np.zeros(1, np.int32))
+    check(lib.pekf_wire_events_dev(K, F, fb.ptr, F, F, ev2.ptr, ev3.ptr, t2b.ptr, n2b.ptr, n3b.ptr, badb.ptr,
+                                   errb.ptr, stream))
+    check(lib.pekf_device_sync() if stream is None else lib.pekf_stream_sync(stream))
+    n2, n3 = n2b.download((K,), np.int32), n3b.download((K,), np.int32)
+    if int(errb.download((1,), np.int32)[0]) & 1:
+        bad = badb.download((K,), np.int32)
+        k = int(np.argmax(bad >= 0))
+        raise ValueError("phone %d, frame %d: not in the client's message form (wire.parse reads it)" % (k, bad[k]))
+    return dict(ev2=ev2, ev3=ev3, E2=int(n2.max(initial=0)), E3=int(n3.max(initial=0)), n2=n2, n3=n3,
+                first_t2=t2b, frames=fb)
+
+
+def run_wire_session(frames, filters, n_avg=100, alpha=0.1, stream=None):
+    """A whole client session from the clients' wire frames, on the device end to end (KFS/Server.cpp's
+    recv'd frames -> Parser.cpp:28-72): pekf_wire_events_dev (the server's parse into FP64 event planes),
+    pekf_frontend_init_ext_dev (phase 2) and pekf_live_ext_dev (phase 3 + the filter) on the server's own
+    values, no host parse.  filters: a BatchedEKF (FP64, AoS).  Returns run_session's dict."""
+    w = wire_events(frames, stream)
+    K = filters.batch
+    ib, tib, rb = DeviceBuffer(48 * K), DeviceBuffer(8 * K), DeviceBuffer(4 * K)
+    check(lib.pekf_frontend_init_ext_dev(K, w["E2"], w["ev2"].ptr, w["first_t2"].ptr, int(n_avg), ib.ptr, tib.ptr,
+                                         None, rb.ptr, EV_F64_EVENTS, stream))
+    cnt, refs = DeviceBuffer(4 * K), DeviceBuffer(48 * K)
+    filters.run_events_async(w["ev3"], w["E3"], ib, tib, cnt, refs, alpha, stream, flags=EV_F64_EVENTS)
+    check(lib.pekf_device_sync() if stream is None else lib.pekf_stream_sync(stream))
+    return dict(ready=rb.download((K,), np.int32).astype(bool), counts=cnt.download((K,), np.int32),
+                refs=refs.download((K, 6), np.float64))
+
+
 # ------------------------------------------------------------------ the batched filter
 
 class BatchedEKF:

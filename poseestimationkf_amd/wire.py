@@ -136,10 +136,32 @@ def events_from_wire(texts, init_acc, init_mag, t_init, phase=3):
         vals[:n, k] = p["values"]
         times[:n, k] = p["times"]
         times[n:, k] = p["times"][-1] if n else int(np.asarray(t_init).reshape(-1)[k])
-    return dict(types=types, values64=vals, values=vals.astype(np.float32), times=times,
+    with np.errstate(over="ignore"):  # a double beyond the float range is +-inf as a float
+        vals32 = vals.astype(np.float32)
+    return dict(types=types, values64=vals, values=vals32, times=times,
                 init_acc=np.asarray(init_acc, np.float64).reshape(K, 3),
                 init_mag=np.asarray(init_mag, np.float64).reshape(K, 3),
                 t_init=np.asarray(t_init, np.int64).reshape(K))
 
 
-__all__ = ["server_values", "parse", "java_float_string", "message", "events_text", "events_from_wire"]
+FRAME = 100  # bytes per message, as the client sends it and the server receives it (Server.cpp:35,84)
+
+
+def frames(texts, n_frames=None):
+    """Per-phone wire texts -> the [n_frames][K][100] uint8 frame array of engine.wire_events: each text cut
+    into the server's 100-byte recv frames (its length must be a multiple of 100, as the client's messages
+    are); shorter streams are padded with blank frames (no message)."""
+    bs = [t.encode() if isinstance(t, str) else bytes(t) for t in texts]
+    for k, b in enumerate(bs):
+        if len(b) % FRAME:
+            raise ValueError("text %d is %d bytes, not whole %d-byte frames" % (k, len(b), FRAME))
+    F = max((len(b) // FRAME for b in bs), default=0) if n_frames is None else int(n_frames)
+    out = np.full((F, len(bs), FRAME), ord(" "), np.uint8)
+    for k, b in enumerate(bs):
+        a = np.frombuffer(b, np.uint8).reshape(-1, FRAME)[:F]
+        out[:a.shape[0], k] = a
+    return out
+
+
+__all__ = ["server_values", "parse", "java_float_string", "message", "events_text", "events_from_wire", "frames",
+           "FRAME"]

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""The wire on the device at scale: pekf_wire_events_dev on 262,144 phones x 1,024 frames (26.8 GB of
+client text, 1,024 generated phones' phase-3 streams tiled x256), then the device session
+(engine.run_wire_session: frames -> FP64 events -> phase 2 -> k_live) on a smaller set.  Prints one JSON
+line: kernel ms (HIP events, median of reps), frames/s, GB/s of frames read + events written.
+
+usage: python3 scripts/wire_probe.py [reps]
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+from poseestimationkf_amd import engine, synth, wire  # noqa: E402
+from poseestimationkf_amd._lib import check, lib  # noqa: E402
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    K0, E, tile = 1024, 1024, 256
+    t0 = time.time()
+    ev = synth.generate_events(np.arange(K0), E, seed=5)
+    texts = [wire.events_text(ev["types"][:, k], ev["values"][:, k], ev["times"][:, k]) for k in range(K0)]
+    fr0 = wire.frames(texts)                                   # [E][K0][100]
+    fr = np.ascontiguousarray(np.tile(fr0, (1, tile, 1)))       # [E][K0 * tile][100]
+    gen_s = time.time() - t0
+    F, K = fr.shape[:2]
+    fb = engine.DeviceBuffer(fr.nbytes).upload(fr)
+    del fr
+    ev2, ev3 = engine.DeviceBuffer(32), engine.DeviceBuffer(32 * F * K)
+    t2b, n2b, n3b, badb = (engine.DeviceBuffer(8 * K), engine.DeviceBuffer(4 * K), engine.DeviceBuffer(4 * K),
+                           engine.DeviceBuffer(4 * K))
+    errb = engine.DeviceBuffer(4).upload(np.zeros(1, np.int32))
+    st = engine.Stream()
+    e0, e1 = engine.Event(), engine.Event()
+    ms = []
+    for _ in range(reps):
+        e0.record(st.handle)
+        check(lib.pekf_wire_events_dev(K, F, fb.ptr, 0, F, ev2.ptr, ev3.ptr, t2b.ptr, n2b.ptr, n3b.ptr, badb.ptr,
+                                       errb.ptr, st.handle))
+        e1.record(st.handle)
+        e1.sync()
+        ms.append(e0.elapsed_ms(e1))
+    assert int(errb.download((1,), np.int32)[0]) == 0
+    n3 = n3b.download((K,), np.int32)
+    assert np.all(n3 == E)
+    # spot check against the host parse: phone 0 and a tiled copy of it
+    got = ev3.download((F, K, 4), np.float64)[:, [0, K0 * 7]]
+    want = synth.pack_events64(wire.events_from_wire(texts[:1], np.zeros((1, 3)), np.zeros((1, 3)), [0]))
+    assert np.array_equal(got[:, 0].view(np.uint64), want[:, 0].view(np.uint64))
+    assert np.array_equal(got[:, 1].view(np.uint64), want[:, 0].view(np.uint64))
+    med = float(np.median(ms[1:] if len(ms) > 1 else ms))
+    frames = F * K
+    byts = frames * (100 + 32)
+    print(json.dumps(dict(kernel="k_wire_events", phones=K, frames_per_phone=F, kernel_ms=med, ms=ms,
+                          frames_per_s=frames / med * 1e3, gbs=byts / med / 1e6, hbm_frac=byts / med / 1e6 / 8000,
+                          bytes_per_frame="100 read + 32 written", text_gen_s=gen_s)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,167 @@
+"""The wire on the device (csrc/pekf_wire_dev.hip, engine.wire_events / run_wire_session): the clients'
+100-byte frames parsed into the FP64 event planes by the GPU, checked against the host parse of the same
+text (pekf_wire_parse: the server's std::stod / std::stoll, itself checked against Python in
+tests/test_wire.py) bit for bit, and the whole device session against engine.run_session on the host's
+events."""
+import numpy as np
+import pytest
+
+from poseestimationkf_amd import synth, wire
+
+
+def _frame(tokens, t, phase=3, ty=0):
+    s = "#%d,%s:%s,%s,%s,t:%s" % (phase, ty, tokens[0], tokens[1], tokens[2], t)
+    assert len(s) <= 99
+    return s.ljust(99) + "\n"
+
+
+def test_frames_layout():
+    a = wire.message(3, 0, [1, 2, 3], 5) + wire.message(2, 1, [4, 5, 6], 7)
+    b = wire.message(3, 2, [7, 8, 9], 9)
+    fr = wire.frames([a, b])
+    assert fr.shape == (2, 2, 100) and fr.dtype == np.uint8
+    assert bytes(fr[1, 0]) == a[100:].encode() and bytes(fr[0, 1]) == b.encode()
+    assert np.all(fr[1, 1] == ord(" "))                      # padding: a blank frame, no message
+    with pytest.raises(ValueError, match="whole 100-byte frames"):
+        wire.frames([a[:-1]])
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from poseestimationkf_amd import engine
+    from poseestimationkf_amd._lib import device_count
+    assert device_count() > 0, "GPU tests need a HIP device"
+    return engine
+
+
+def _host_planes(texts, phase, E):
+    ev = wire.events_from_wire(texts, np.zeros((len(texts), 3)), np.zeros((len(texts), 3)),
+                               np.zeros(len(texts), np.int64), phase=phase)
+    p = synth.pack_events64(ev)
+    out = np.empty((E, len(texts), 4))
+    out[...] = np.uint64(synth.EV64_NONE_W).view(np.float64)
+    out[..., :3] = 0.0
+    n = min(E, p.shape[0])
+    out[:n] = p[:n]
+    return out
+
+
+def _same(a, b):
+    return np.array_equal(np.ascontiguousarray(a).view(np.uint64), np.ascontiguousarray(b).view(np.uint64))
+
+
+@pytest.mark.gpu
+def test_wire_events_equal_the_host_parse(eng):
+    """Phase-2 and phase-3 messages of ragged streams with phase-1 messages, blank and non-'#' frames,
+    sensor types no sensor takes and every kind of float the client prints (Float.toString: plain and
+    computerized forms, 1.4E-45 .. 3.4028235E38, NaN, Infinity): the device planes equal the host's,
+    bit for bit, and so do the counts and phase 2's first time."""
+    rng = np.random.default_rng(21)
+    K = 150
+    texts = []
+    for k in range(K):
+        n2, n3 = int(rng.integers(0, 60)), int(rng.integers(0, 90))
+        vals = rng.standard_normal((n2 + n3, 3)) * 10.0 ** rng.integers(-40, 38, (n2 + n3, 3))
+        vals = vals.astype(np.float32)
+        vals[rng.random(vals.shape) < 0.01] = np.nan
+        vals[rng.random(vals.shape) < 0.01] = np.inf
+        vals[rng.random(vals.shape) < 0.01] = -np.inf
+        vals[rng.random(vals.shape) < 0.01] = np.float32(1.4e-45)
+        t = 10 ** 12 + np.cumsum(rng.integers(0, 3_000_000, n2 + n3))
+        types = rng.integers(0, 3, n2 + n3).astype(str).astype(object)
+        types[rng.random(n2 + n3) < 0.03] = "7"
+        msgs = [wire.message(2 if i < n2 else 3, types[i], vals[i], t[i]) for i in range(n2 + n3)]
+        if k % 5 == 0:
+            msgs.insert(int(rng.integers(0, len(msgs) + 1)), wire.message(1, 2, [1, 2, 3], 42))
+        if k % 7 == 0:
+            msgs.insert(int(rng.integers(0, len(msgs) + 1)), " " * 99 + "\n")
+        if k % 11 == 0:
+            msgs.insert(int(rng.integers(0, len(msgs) + 1)), "x" * 99 + "\n")
+        texts.append("".join(msgs))
+    fr = wire.frames(texts)
+    w = eng.wire_events(fr)
+    F = fr.shape[0]
+    host2, host3 = _host_planes(texts, 2, F), _host_planes(texts, 3, F)
+    assert _same(w["ev2"].download((F, K, 4), np.float64), host2)
+    assert _same(w["ev3"].download((F, K, 4), np.float64), host3)
+    for k, tx in enumerate(texts):
+        p = wire.parse(tx)
+        assert w["n2"][k] == (p["phase"] == 2).sum() and w["n3"][k] == (p["phase"] == 3).sum()
+        t2 = p["times"][p["phase"] == 2]
+        assert w["first_t2"].download((K,), np.int64)[k] == (t2[0] if t2.size else 0)
+    assert w["E3"] == int(w["n3"].max())
+
+
+@pytest.mark.gpu
+def test_wire_events_number_forms(eng):
+    """Decimals the client never prints but the device parser takes: up to 19 significant digits, exponents
+    to +-80 -- one IEEE operation where that is exact, the big-integer path elsewhere (also near halfway
+    points) --, signs, leading zeros: strtod's value (the host parse's) bit for bit."""
+    rng = np.random.default_rng(22)
+    toks = []
+    for _ in range(4000):
+        nd = int(rng.integers(1, 20))
+        digits = "".join(str(d) for d in rng.integers(0, 10, nd))
+        point = int(rng.integers(0, nd + 1))
+        mant = digits[:point] + ("." + digits[point:] if point < nd or rng.random() < 0.3 else "")
+        if not mant.strip("."):
+            mant = "0"
+        e = int(rng.integers(-60, 60))
+        toks.append(rng.choice(["", "-", "+"]) + mant + ("e%d" % e if rng.random() < 0.8 else ""))
+    # halfway cases between adjacent doubles, written out in full, and their neighbours
+    for v in rng.standard_normal(300) * 10.0 ** rng.integers(-30, 30, 300):
+        a = np.float64(v)
+        b = np.nextafter(a, np.inf)
+        mid = (np.longdouble(a) + np.longdouble(b)) / 2
+        toks.append(np.format_float_scientific(mid, precision=18, unique=False))
+    toks += ["1.4E-45", "3.4028235E38", "9007199254740993", "1e22", "1e23", "0e80", "-0.0", "1e-80", "9e80"]
+    rows = []
+    for i in range(0, len(toks) - 2, 3):
+        rows.append(_frame(toks[i:i + 3], i))
+    K = 64
+    texts = ["".join(rows[k::K]) for k in range(K)]
+    fr = wire.frames(texts)
+    w = eng.wire_events(fr)
+    F = fr.shape[0]
+    assert _same(w["ev3"].download((F, K, 4), np.float64), _host_planes(texts, 3, F))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tok,t", [(" 1.5", "5"), ("0x1p3", "5"), ("1.5abc", "5"), ("12345678901234567890", "5"),
+                                   ("1e81", "5"), ("inf", "5"), ("-NaN", "5"), ("1.5", "+5"), ("1.5", " 5"),
+                                   ("1.5", "99999999999999999999"), ("1.5", "")])
+def test_wire_events_report_other_forms(eng, tok, t):
+    """A frame the client would never send -- a number in a form strtod reads but Float.toString never
+    prints, or text std::stod / std::stoll throws on -- stops its phone and is reported (the host parse
+    takes the forms strtod reads)."""
+    good = _frame(["1.0", "2.0", "3.0"], 7)
+    texts = [good * 3, good + _frame([tok, "2.0", "3.0"], t) + good]
+    with pytest.raises(ValueError, match="phone 1, frame 1"):
+        eng.wire_events(wire.frames(texts))
+
+
+@pytest.mark.gpu
+def test_wire_session_equals_the_host_session(eng):
+    """The whole session from wire frames on the device (run_wire_session) equals run_session on the host's
+    parse of the same text (wire.events_from_wire, events="f64") bit for bit: ready, counts, refs, X, P."""
+    K = 96
+    ph2 = synth.generate_events(np.arange(K), 700, seed=61)
+    ph3 = synth.generate_events(np.arange(K), 500, seed=62)
+    ph3 = dict(ph3, times=ph3["times"] - ph3["t_init"][None, :] + ph2["times"][-1][None, :])
+    texts = []
+    for k in range(K):
+        n3 = 500 - 9 * (k % 5)
+        texts.append(wire.events_text(ph2["types"][:, k], ph2["values"][:, k], ph2["times"][:, k], phase=2) +
+                     wire.events_text(ph3["types"][:n3, k], ph3["values"][:n3, k], ph3["times"][:n3, k], phase=3))
+    f_dev = eng.BatchedEKF(K)
+    out_dev = eng.run_wire_session(wire.frames(texts), f_dev)
+    t0 = ph2["times"][0]
+    e2 = wire.events_from_wire(texts, np.zeros((K, 3)), np.zeros((K, 3)), t0, phase=2)
+    e3 = wire.events_from_wire(texts, np.zeros((K, 3)), np.zeros((K, 3)), t0, phase=3)
+    f_host = eng.BatchedEKF(K)
+    out_host = eng.run_session(e2, e3, f_host, events="f64")
+    assert out_dev["ready"].all() and out_dev["counts"].min() > 0
+    for key in ("ready", "counts", "refs"):
+        assert np.array_equal(out_dev[key], out_host[key]), key
+    for a, b in zip(f_dev.get_state(), f_host.get_state()):
+        assert np.array_equal(a, b)
