@@ -128,7 +128,6 @@ __device__ double decimal_exact(uint64_t m, int e10) {
 // decimals).  Returns false for any other form; i is left on the ','.
 __device__ bool wire_number(const uint8_t *fr, int &i, double &out) {
     auto ch = [&](int j) -> unsigned { return j < kWireFrame ? fr[j] : 0u; };  // past the frame: none
-    auto digit = [&](int j) { return ch(j) - '0' < 10u; };
     bool neg = false;
     if (ch(i) == '-' || ch(i) == '+') neg = ch(i++) == '-';
     if (ch(i) == 'N' || ch(i) == 'I') {  // "NaN" (strtod: the positive quiet NaN), "[-]Infinity"
@@ -142,37 +141,39 @@ __device__ bool wire_number(const uint8_t *fr, int &i, double &out) {
         out = nan ? __longlong_as_double(0x7ff8000000000000ll) : (neg ? -__builtin_huge_val() : __builtin_huge_val());
         return true;
     }
+    // the digits and one '.': a loop whose body has no branch (the lanes of a wave run it together);
+    // leading zeros are not significant digits; more than 19 of them is not the client's form (m wraps
+    // then, and the token is refused below)
     uint64_t m = 0;
-    int nd = 0, e10 = 0;
-    bool any = false;
-    for (; digit(i); ++i) {
-        any = true;
-        if (m || ch(i) != '0') {
-            if (++nd > 19) return false;
-            m = m * 10 + (ch(i) - '0');
-        }
+    int nd = 0, nf = 0;
+    bool any = false, frac = false;
+    for (;;) {
+        const unsigned c = ch(i), d = c - '0';
+        const bool dig = d < 10u, pt = c == '.' && !frac;
+        if (!dig && !pt) break;
+        const bool sig = dig && (m != 0 || d != 0);
+        m = sig ? m * 10 + d : m;
+        nd += sig;
+        nf += dig && frac;
+        any |= dig;
+        frac |= pt;
+        ++i;
     }
-    if (ch(i) == '.') {
-        for (++i; digit(i); ++i) {
-            any = true;
-            if (m || ch(i) != '0') {
-                if (++nd > 19) return false;
-                m = m * 10 + (ch(i) - '0');
-            }
-            --e10;
-        }
-    }
-    if (!any) return false;
+    if (!any || nd > 19) return false;
+    int e10 = -nf;
     if (ch(i) == 'e' || ch(i) == 'E') {
         ++i;
         bool eneg = false;
         if (ch(i) == '+' || ch(i) == '-') eneg = ch(i++) == '-';
         int e = 0, ne = 0;
-        for (; digit(i); ++i) {
-            if (++ne > 4) return false;
-            e = e * 10 + (int)(ch(i) - '0');
+        for (;;) {
+            const unsigned d = ch(i) - '0';
+            if (d >= 10u) break;
+            e = e * 10 + (int)d;
+            ++ne;
+            ++i;
         }
-        if (!ne) return false;
+        if (ne == 0 || ne > 4) return false;
         e10 += eneg ? -e : e;
     }
     if (ch(i) != ',') return false;
@@ -219,16 +220,24 @@ __device__ int wire_frame(const uint8_t *fr, WireMsg &m) {
     if (neg) ++i;
     uint64_t t = 0;
     int nd = 0;
-    for (; ch(i) - '0' < 10u; ++i) {
-        if (++nd > 19) return 2;
-        t = t * 10 + (ch(i) - '0');
+    for (;;) {
+        const unsigned d = ch(i) - '0';
+        if (d >= 10u) break;
+        t = t * 10 + d;  // (wraps past 19 digits: refused below)
+        ++nd;
+        ++i;
     }
-    if (!nd || t > (neg ? (1ull << 63) : (1ull << 63) - 1)) return 2;  // std::stoll: ERANGE throws
+    if (!nd || nd > 19 || t > (neg ? (1ull << 63) : (1ull << 63) - 1)) return 2;  // std::stoll: ERANGE throws
     m.t = neg ? (long long)(0 - t) : (long long)t;
     return 0;
 }
 
-__global__ __launch_bounds__(kWireBlock) void k_wire_events(int64_t batch, int64_t n_frames,
+// Held to 3 waves per SIMD (168 VGPRs, 4 of them spilled on the rare big-integer path; the compiler's
+// choice was 201 = 2 waves): the parse is a chain of dependent LDS reads and divergent branches, and the
+// third wave hides part of it.  262,144 phones x 1,024 frames, same box (profiles/r6/wire_dev/): 29.8 ms
+// (byte loops with early exits, 2 waves) -> 27.5 (branch-free digit loops) -> 25.4 ms (and 3 waves); a
+// dword-window reader instead of byte reads was slower (36.6 against 29.8 ms on another box).
+__global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_wire_events(int64_t batch, int64_t n_frames,
                                                             const uint32_t *__restrict__ frames, int64_t e2_max,
                                                             int64_t e3_max, double4 *__restrict__ ev2,
                                                             double4 *__restrict__ ev3, int64_t *__restrict__ first_t2,

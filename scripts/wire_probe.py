@@ -4,7 +4,7 @@ client text, 1,024 generated phones' phase-3 streams tiled x256), then the devic
 (engine.run_wire_session: frames -> FP64 events -> phase 2 -> k_live) on a smaller set.  Prints one JSON
 line: kernel ms (HIP events, median of reps), frames/s, GB/s of frames read + events written.
 
-usage: python3 scripts/wire_probe.py [reps]
+usage: python3 scripts/wire_probe.py [reps] [--session]
 """
 from __future__ import annotations
 
@@ -63,5 +63,56 @@ def main():
                           bytes_per_frame="100 read + 32 written", text_gen_s=gen_s)))
 
 
+def session(reps):
+    """frames -> FP64 events -> phase 2 -> phase 3 + filter on the device (engine.run_wire_session's
+    launches, each timed): 65,536 phones x (700 phase-2 + 1,024 phase-3 frames), 1,024 generated phones
+    tiled x64."""
+    K0, tile, E2, E3 = 1024, 64, 700, 1024
+    ph2 = synth.generate_events(np.arange(K0), E2, seed=71)
+    ph3 = synth.generate_events(np.arange(K0), E3, seed=72)
+    ph3 = dict(ph3, times=ph3["times"] - ph3["t_init"][None, :] + ph2["times"][-1][None, :])
+    texts = [wire.events_text(ph2["types"][:, k], ph2["values"][:, k], ph2["times"][:, k], phase=2) +
+             wire.events_text(ph3["types"][:, k], ph3["values"][:, k], ph3["times"][:, k], phase=3)
+             for k in range(K0)]
+    fr = np.ascontiguousarray(np.tile(wire.frames(texts), (1, tile, 1)))
+    F, K = fr.shape[:2]
+    fb = engine.DeviceBuffer(fr.nbytes).upload(fr)
+    del fr
+    from poseestimationkf_amd._lib import EV_F64_EVENTS
+    ev2, ev3 = engine.DeviceBuffer(32 * F * K), engine.DeviceBuffer(32 * F * K)
+    t2b, n2b, n3b = engine.DeviceBuffer(8 * K), engine.DeviceBuffer(4 * K), engine.DeviceBuffer(4 * K)
+    errb = engine.DeviceBuffer(4).upload(np.zeros(1, np.int32))
+    ib, tib, rb = engine.DeviceBuffer(48 * K), engine.DeviceBuffer(8 * K), engine.DeviceBuffer(4 * K)
+    cnt, refs = engine.DeviceBuffer(4 * K), engine.DeviceBuffer(48 * K)
+    f = engine.BatchedEKF(K)
+    st = engine.Stream()
+    ev = [engine.Event() for _ in range(4)]
+    rows = []
+    for _ in range(reps):
+        f.reset()
+        ev[0].record(st.handle)
+        check(lib.pekf_wire_events_dev(K, F, fb.ptr, F, F, ev2.ptr, ev3.ptr, t2b.ptr, n2b.ptr, n3b.ptr, None,
+                                       errb.ptr, st.handle))
+        ev[1].record(st.handle)
+        check(lib.pekf_frontend_init_ext_dev(K, E2, ev2.ptr, t2b.ptr, 100, ib.ptr, tib.ptr, None, rb.ptr,
+                                             EV_F64_EVENTS, st.handle))
+        ev[2].record(st.handle)
+        f.run_events_async(ev3, E3, ib, tib, cnt, refs, 0.1, st.handle, flags=EV_F64_EVENTS)
+        ev[3].record(st.handle)
+        ev[3].sync()
+        rows.append([ev[i].elapsed_ms(ev[i + 1]) for i in range(3)])
+    assert int(errb.download((1,), np.int32)[0]) == 0
+    assert np.all(n2b.download((K,), np.int32) == E2) and np.all(n3b.download((K,), np.int32) == E3)
+    assert rb.download((K,), np.int32).all()
+    med = np.median(np.array(rows[1:] if len(rows) > 1 else rows), axis=0)
+    print(json.dumps(dict(kernel="wire session", phones=K, frames_per_phone=F, wire_ms=float(med[0]),
+                          phase2_ms=float(med[1]), live_ms=float(med[2]), total_ms=float(med.sum()),
+                          messages_per_s=K * F / float(med.sum()) * 1e3,
+                          records=int(cnt.download((K,), np.int32).sum()))))
+
+
 if __name__ == "__main__":
-    main()
+    if "--session" in sys.argv:
+        session(int(sys.argv[1]) if sys.argv[1:2] and sys.argv[1].isdigit() else 5)
+    else:
+        main()
