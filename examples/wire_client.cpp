@@ -8,10 +8,13 @@
 // then Prediction + Correction per record).  Phase-1 messages (magnetometer calibration, a no-op in the
 // reference) are skipped.
 //
-// usage: wire_client <out.txt> <phone0.txt> [phone1.txt ...]
-//        writes one line per phone: records applied, then the final quaternion (%.17g).
-// tests/test_c_client.py runs the library form (pekf_wire_example_run) on the GPU and compares with
-// engine.run_session(..., events="f64") on wire.events_from_wire of the same texts, bit for bit.
+// usage: wire_client [--device] <out.txt> <phone0.txt> [phone1.txt ...]
+//        writes one line per phone: records applied, then the final quaternion (%.17g).  --device: the
+//        texts are cut into the server's 100-byte frames and parsed on the GPU (pekf_wire_events_dev)
+//        into the same planes instead of by pekf_wire_parse on the host.
+// tests/test_c_client.py runs the library form (pekf_wire_example_run_mode, both parses) on the GPU and
+// compares with engine.run_session(..., events="f64") on wire.events_from_wire of the same texts, bit for
+// bit.
 //
 // build: g++ -O2 -std=c++17 examples/wire_client.cpp -Iinclude -Lposeestimationkf_amd -lpekf
 //        -Wl,-rpath,$PWD/poseestimationkf_amd -o build/wire_client
@@ -108,21 +111,71 @@ int planes(const std::vector<Messages> &ms, uint8_t p, void **dev, int64_t *E, s
     return 0;
 }
 
-int run(const std::vector<const char *> &paths, std::FILE *o) {
+// The device form: each phone's text cut into the server's 100-byte recv frames ([F][K][100] bytes, short
+// streams padded with blank frames), parsed on the GPU into the same FP64 event planes
+// (pekf_wire_events_dev); phase 2 starts from each phone's first phase-2 time, as above.
+int device_planes(const std::vector<const char *> &paths, void **ev2, int64_t *E2, void **ev3, int64_t *E3,
+                  void **d_ts) {
     const int64_t K = (int64_t)paths.size();
-    std::vector<Messages> ms(K);
+    std::vector<std::string> texts(K);
+    int64_t F = 0;
     for (int64_t k = 0; k < K; ++k) {
-        std::string text;
-        if (!read_text(paths[k], text)) return 2;
-        if (int st = parse(text, ms[k])) return st;
+        if (!read_text(paths[k], texts[k]) || texts[k].size() % 100) return 2;
+        if ((int64_t)texts[k].size() / 100 > F) F = (int64_t)texts[k].size() / 100;
     }
-    void *ev2 = nullptr, *ev3 = nullptr;
+    std::vector<char> frames((size_t)(F > 0 ? F : 1) * K * 100, ' ');
+    for (int64_t k = 0; k < K; ++k)
+        for (int64_t f = 0; f < (int64_t)texts[k].size() / 100; ++f)
+            std::memcpy(&frames[(size_t)(f * K + k) * 100], texts[k].data() + f * 100, 100);
+    void *d_frames, *d_n2, *d_n3, *d_err;
+    CHECK(pekf_malloc(&d_frames, frames.size()));
+    CHECK(pekf_memcpy_h2d(d_frames, frames.data(), frames.size(), nullptr));
+    const int64_t rows = F > 0 ? F : 1;
+    CHECK(pekf_malloc(ev2, 32 * rows * K));
+    CHECK(pekf_malloc(ev3, 32 * rows * K));
+    CHECK(pekf_malloc(d_ts, 8 * K));
+    CHECK(pekf_malloc(&d_n2, 4 * K));
+    CHECK(pekf_malloc(&d_n3, 4 * K));
+    CHECK(pekf_malloc(&d_err, 4));
+    const int zero = 0;
+    CHECK(pekf_memcpy_h2d(d_err, &zero, 4, nullptr));
+    CHECK(pekf_wire_events_dev(K, F, d_frames, F, F, *ev2, *ev3, (int64_t *)*d_ts, (int32_t *)d_n2, (int32_t *)d_n3,
+                               nullptr, (int *)d_err, nullptr));
+    std::vector<int32_t> n2(K), n3(K);
+    int err = 0;
+    CHECK(pekf_memcpy_d2h(n2.data(), d_n2, 4 * K, nullptr));
+    CHECK(pekf_memcpy_d2h(n3.data(), d_n3, 4 * K, nullptr));
+    CHECK(pekf_memcpy_d2h(&err, d_err, 4, nullptr));
+    for (void *q : {d_frames, d_n2, d_n3, d_err}) CHECK(pekf_free(q));
+    if (err) return 3;  // a frame the device parser does not take: use the host form
+    *E2 = *E3 = 0;
+    for (int64_t k = 0; k < K; ++k) {
+        if (n2[k] > *E2) *E2 = n2[k];
+        if (n3[k] > *E3) *E3 = n3[k];
+    }
+    return 0;
+}
+
+int run(const std::vector<const char *> &paths, std::FILE *o, bool device = false) {
+    const int64_t K = (int64_t)paths.size();
+    void *ev2 = nullptr, *ev3 = nullptr, *d_ts = nullptr;
     int64_t E2 = 0, E3 = 0;
-    std::vector<int64_t> t_start;
-    if (int st = planes(ms, 2, &ev2, &E2, &t_start)) return st;
-    if (int st = planes(ms, 3, &ev3, &E3, nullptr)) return st;
-    void *d_ts, *d_init, *d_tinit, *d_ready, *d_X, *d_P, *d_counts, *d_refs;
-    CHECK(pekf_malloc(&d_ts, 8 * K));
+    if (device) {
+        if (int st = device_planes(paths, &ev2, &E2, &ev3, &E3, &d_ts)) return st;
+    } else {
+        std::vector<Messages> ms(K);
+        for (int64_t k = 0; k < K; ++k) {
+            std::string text;
+            if (!read_text(paths[k], text)) return 2;
+            if (int st = parse(text, ms[k])) return st;
+        }
+        std::vector<int64_t> t_start;
+        if (int st = planes(ms, 2, &ev2, &E2, &t_start)) return st;
+        if (int st = planes(ms, 3, &ev3, &E3, nullptr)) return st;
+        CHECK(pekf_malloc(&d_ts, 8 * K));
+        CHECK(pekf_memcpy_h2d(d_ts, t_start.data(), 8 * K, nullptr));
+    }
+    void *d_init, *d_tinit, *d_ready, *d_X, *d_P, *d_counts, *d_refs;
     CHECK(pekf_malloc(&d_init, 48 * K));
     CHECK(pekf_malloc(&d_tinit, 8 * K));
     CHECK(pekf_malloc(&d_ready, 4 * K));
@@ -130,7 +183,6 @@ int run(const std::vector<const char *> &paths, std::FILE *o) {
     CHECK(pekf_malloc(&d_P, 128 * K));
     CHECK(pekf_malloc(&d_counts, 4 * K));
     CHECK(pekf_malloc(&d_refs, 48 * K));
-    CHECK(pekf_memcpy_h2d(d_ts, t_start.data(), 8 * K, nullptr));
     // phase 2: the means of each sensor's first 100 samples and the time phase 3 continues from
     CHECK(pekf_frontend_init_ext_dev(K, E2, ev2, (const int64_t *)d_ts, 100, (double *)d_init, (int64_t *)d_tinit,
                                      nullptr, (int32_t *)d_ready, PEKF_EV_F64_EVENTS, nullptr));
@@ -153,8 +205,8 @@ int run(const std::vector<const char *> &paths, std::FILE *o) {
 }  // namespace
 
 #ifdef PEKF_EXAMPLE_LIBRARY
-// paths: phone text files separated by '\n'
-extern "C" int pekf_wire_example_run(const char *paths, const char *outputs) {
+// paths: phone text files separated by '\n'; device: parse on the GPU (pekf_wire_events_dev)
+extern "C" int pekf_wire_example_run_mode(const char *paths, const char *outputs, int device) {
     std::vector<std::string> names;
     for (const char *p = paths; *p;) {
         const char *e = std::strchr(p, '\n');
@@ -166,16 +218,20 @@ extern "C" int pekf_wire_example_run(const char *paths, const char *outputs) {
         if (!n.empty()) v.push_back(n.c_str());
     std::FILE *o = std::fopen(outputs, "w");
     if (!o) return 2;
-    const int st = run(v, o);
+    const int st = run(v, o, device != 0);
     std::fclose(o);
     return st;
 }
+extern "C" int pekf_wire_example_run(const char *paths, const char *outputs) {
+    return pekf_wire_example_run_mode(paths, outputs, 0);
+}
 #else
 int main(int argc, char **argv) {
-    if (argc < 3) return 2;
-    std::FILE *o = std::fopen(argv[1], "w");
+    const bool device = argc > 1 && std::strcmp(argv[1], "--device") == 0;
+    if (argc < 3 + device) return 2;
+    std::FILE *o = std::fopen(argv[1 + device], "w");
     if (!o) return 2;
-    const int st = run(std::vector<const char *>(argv + 2, argv + argc), o);
+    const int st = run(std::vector<const char *>(argv + 2 + device, argv + argc), o, device);
     std::fclose(o);
     return st;
 }

@@ -82,8 +82,9 @@ def test_c_client_matches_python_engine(tmp_path):
 @pytest.mark.gpu
 def test_wire_client_matches_python_session(tmp_path):
     """examples/wire_client.cpp: K phones' wire text (phase-2 then phase-3 messages, as the Android
-    client sends them) -> pekf_wire_parse -> FP64 event planes -> pekf_frontend_init_ext_dev ->
-    pekf_live_ext_dev, all from C++; the same texts through wire.events_from_wire and
+    client sends them) -> pekf_wire_parse on the host, or the 100-byte frames -> pekf_wire_events_dev on
+    the GPU -> FP64 event planes -> pekf_frontend_init_ext_dev -> pekf_live_ext_dev, all from C++; both
+    parses give the same result, and the same texts through wire.events_from_wire and
     engine.run_session(events="f64") give the same counts and quaternions, bit for bit."""
     from poseestimationkf_amd import engine, wire
     K = 24
@@ -102,11 +103,14 @@ def test_wire_client_matches_python_session(tmp_path):
         p.write_text(text)
         paths.append(str(p))
     client = ctypes.CDLL(WIRE_PREBUILT)  # built by csrc/Makefile with the library
-    client.pekf_wire_example_run.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
-    res = tmp_path / "out.txt"
-    assert client.pekf_wire_example_run("\n".join(paths).encode(), os.fsencode(res)) == 0
-    got = np.array([[float(v) for v in line.split()] for line in res.read_text().strip().splitlines()])
-    assert got.shape == (K, 5)
+    client.pekf_wire_example_run_mode.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+    outs = []
+    for device in (0, 1):  # the host parse (pekf_wire_parse), then the device parse (pekf_wire_events_dev)
+        res = tmp_path / ("out%d.txt" % device)
+        assert client.pekf_wire_example_run_mode("\n".join(paths).encode(), os.fsencode(res), device) == 0
+        outs.append(np.array([[float(v) for v in line.split()] for line in res.read_text().strip().splitlines()]))
+    got = outs[0]
+    assert got.shape == (K, 5) and np.array_equal(outs[1], got)
 
     texts = [open(p).read() for p in paths]
     t0 = ph2["times"][0]
