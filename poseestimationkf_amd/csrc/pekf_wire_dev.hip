@@ -165,16 +165,17 @@ __device__ bool wire_number(const uint8_t *fr, int &i, double &out) {
         ++i;
         bool eneg = false;
         if (ch(i) == '+' || ch(i) == '-') eneg = ch(i++) == '-';
-        int e = 0, ne = 0;
+        unsigned e = 0;  // (wraps past 9 digits: refused below)
+        int ne = 0;
         for (;;) {
             const unsigned d = ch(i) - '0';
             if (d >= 10u) break;
-            e = e * 10 + (int)d;
+            e = e * 10 + d;
             ++ne;
             ++i;
         }
         if (ne == 0 || ne > 4) return false;
-        e10 += eneg ? -e : e;
+        e10 += eneg ? -(int)e : (int)e;
     }
     if (ch(i) != ',') return false;
     double v;
@@ -237,12 +238,10 @@ __device__ int wire_frame(const uint8_t *fr, WireMsg &m) {
 // third wave hides part of it.  262,144 phones x 1,024 frames, same box (profiles/r6/wire_dev/): 29.8 ms
 // (byte loops with early exits, 2 waves) -> 27.5 (branch-free digit loops) -> 25.4 ms (and 3 waves); a
 // dword-window reader instead of byte reads was slower (36.6 against 29.8 ms on another box).
-__global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_wire_events(int64_t batch, int64_t n_frames,
-                                                            const uint32_t *__restrict__ frames, int64_t e2_max,
-                                                            int64_t e3_max, double4 *__restrict__ ev2,
-                                                            double4 *__restrict__ ev3, int64_t *__restrict__ first_t2,
-                                                            int32_t *__restrict__ n2, int32_t *__restrict__ n3,
-                                                            int32_t *__restrict__ bad_frame, int *__restrict__ err) {
+__global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_wire_events(
+    int64_t batch, int64_t n_frames, const uint32_t *__restrict__ frames, int64_t e2_max, int64_t e3_max,
+    double4 *__restrict__ ev2, double4 *__restrict__ ev3, int64_t *__restrict__ first_t2, int32_t *__restrict__ n2,
+    int32_t *__restrict__ n3, int32_t *__restrict__ bad_frame, int *__restrict__ err) {
     __shared__ uint32_t lds[kWireDwords];
     const int lane = threadIdx.x;
     const int64_t k0 = (int64_t)blockIdx.x * kWireBlock;
@@ -319,7 +318,8 @@ extern "C" int pekf_wire_events_dev(int64_t batch, int64_t n_frames, const void 
     PEKF_CHECK_ARG((ev2 || e2_max == 0) && (ev3 || e3_max == 0) && first_t2 && n2 && n3, "null pointer");
     PEKF_CHECK_ARG((uintptr_t)frames % 4 == 0 && (uintptr_t)ev2 % 16 == 0 && (uintptr_t)ev3 % 16 == 0,
                    "misaligned buffers");
-    PEKF_CHECK_ARG(e2_max < ((int64_t)1 << 31) && e3_max < ((int64_t)1 << 31), "e_max must be < 2^31");
+    PEKF_CHECK_ARG(n_frames < ((int64_t)1 << 31) && e2_max < ((int64_t)1 << 31) && e3_max < ((int64_t)1 << 31),
+                   "n_frames and e_max must be < 2^31");
     hipLaunchKernelGGL(k_wire_events, dim3(grid_for(batch, kWireBlock)), dim3(kWireBlock), 0, as_stream(stream),
                        batch, n_frames, static_cast<const uint32_t *>(frames), e2_max, e3_max,
                        static_cast<double4 *>(ev2), static_cast<double4 *>(ev3), first_t2, n2, n3, bad_frame,
