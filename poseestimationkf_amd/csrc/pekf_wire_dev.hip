@@ -127,7 +127,10 @@ __device__ double decimal_exact(uint64_t m, int e10) {
 // A number token at fr[i..], up to the ',' that must follow it: Float.toString's forms (and plain
 // decimals).  Returns false for any other form; i is left on the ','.
 __device__ bool wire_number(const uint8_t *fr, int &i, double &out) {
-    auto ch = [&](int j) -> unsigned { return j < kWireFrame ? fr[j] : 0u; };  // past the frame: none
+    auto ch = [&](int j) -> unsigned {  // past the frame: none (the address clamped into it)
+        const unsigned c = fr[j < kWireFrame ? j : kWireFrame - 1];
+        return j < kWireFrame ? c : 0u;
+    };
     bool neg = false;
     if (ch(i) == '-' || ch(i) == '+') neg = ch(i++) == '-';
     if (ch(i) == 'N' || ch(i) == 'I') {  // "NaN" (strtod: the positive quiet NaN), "[-]Infinity"
@@ -146,18 +149,19 @@ __device__ bool wire_number(const uint8_t *fr, int &i, double &out) {
     // then, and the token is refused below)
     uint64_t m = 0;
     int nd = 0, nf = 0;
-    bool any = false, frac = false;
-    for (;;) {
+    bool any = false, frac = false, act = true;
+    for (;;) {  // until no lane of the wave is in its digits: the exit is wave-uniform, not per lane
         const unsigned c = ch(i), d = c - '0';
         const bool dig = d < 10u, pt = c == '.' && !frac;
-        if (!dig && !pt) break;
-        const bool sig = dig && (m != 0 || d != 0);
+        act = act && (dig || pt);
+        if (!__any(act)) break;
+        const bool sig = act && dig && (m != 0 || d != 0);
         m = sig ? m * 10 + d : m;
         nd += sig;
-        nf += dig && frac;
-        any |= dig;
-        frac |= pt;
-        ++i;
+        nf += act && dig && frac;
+        any |= act && dig;
+        frac |= act && pt;
+        i += act;
     }
     if (!any || nd > 19) return false;
     int e10 = -nf;
@@ -167,12 +171,14 @@ __device__ bool wire_number(const uint8_t *fr, int &i, double &out) {
         if (ch(i) == '+' || ch(i) == '-') eneg = ch(i++) == '-';
         unsigned e = 0;  // (wraps past 9 digits: refused below)
         int ne = 0;
+        bool eact = true;
         for (;;) {
             const unsigned d = ch(i) - '0';
-            if (d >= 10u) break;
-            e = e * 10 + d;
-            ++ne;
-            ++i;
+            eact = eact && d < 10u;
+            if (!__any(eact)) break;
+            e = eact ? e * 10 + d : e;
+            ne += eact;
+            i += eact;
         }
         if (ne == 0 || ne > 4) return false;
         e10 += eneg ? -(int)e : (int)e;
@@ -200,15 +206,22 @@ struct WireMsg {
 
 // 0: a message (m filled); 1: no message (no '#': Parser::run skips it); 2: not parsed here (see above)
 __device__ int wire_frame(const uint8_t *fr, WireMsg &m) {
-    auto ch = [&](int j) -> unsigned { return j < kWireFrame ? fr[j] : 0u; };
+    auto ch = [&](int j) -> unsigned {
+        const unsigned c = fr[j < kWireFrame ? j : kWireFrame - 1];
+        return j < kWireFrame ? c : 0u;
+    };
     if (fr[0] != '#') return 1;
     m.phase = fr[1];
     int i = 3;  // str.substr(2) of the text after '#'
-    while (i < kWireFrame && fr[i] != ':') {
-        if (fr[i] == 0) return 2;
-        ++i;
+    bool cact = true, nul = false;
+    for (;;) {  // to the first ':' (a NUL before it: strchr's end, not the server's message)
+        const unsigned c = ch(i);
+        nul |= cact && c == 0 && i < kWireFrame;
+        cact = cact && i < kWireFrame && c != ':' && c != 0;
+        if (!__any(cact)) break;
+        i += cact;
     }
-    if (i >= kWireFrame) return 2;
+    if (nul || i >= kWireFrame) return 2;
     m.type = i > 3 ? fr[3] : 0;  // FindValues(str, ":")[0]
     ++i;
     for (int k = 0; k < 3; ++k) {
@@ -221,12 +234,14 @@ __device__ int wire_frame(const uint8_t *fr, WireMsg &m) {
     if (neg) ++i;
     uint64_t t = 0;
     int nd = 0;
+    bool tact = true;
     for (;;) {
         const unsigned d = ch(i) - '0';
-        if (d >= 10u) break;
-        t = t * 10 + d;  // (wraps past 19 digits: refused below)
-        ++nd;
-        ++i;
+        tact = tact && d < 10u;
+        if (!__any(tact)) break;
+        t = tact ? t * 10 + d : t;  // (wraps past 19 digits: refused below)
+        nd += tact;
+        i += tact;
     }
     if (!nd || nd > 19 || t > (neg ? (1ull << 63) : (1ull << 63) - 1)) return 2;  // std::stoll: ERANGE throws
     m.t = neg ? (long long)(0 - t) : (long long)t;
@@ -236,8 +251,11 @@ __device__ int wire_frame(const uint8_t *fr, WireMsg &m) {
 // Held to 3 waves per SIMD (168 VGPRs, 4 of them spilled on the rare big-integer path; the compiler's
 // choice was 201 = 2 waves): the parse is a chain of dependent LDS reads and divergent branches, and the
 // third wave hides part of it.  262,144 phones x 1,024 frames, same box (profiles/r6/wire_dev/): 29.8 ms
-// (byte loops with early exits, 2 waves) -> 27.5 (branch-free digit loops) -> 25.4 ms (and 3 waves); a
-// dword-window reader instead of byte reads was slower (36.6 against 29.8 ms on another box).
+// (byte loops with early exits, 2 waves) -> 27.5 (branch-free digit loops) -> 25.4 ms (and 3 waves) ->
+// 23.6 ms (the character loops exit when no lane of the wave is still in them, __any, instead of lane by
+// lane).  Measured and not kept: a dword-window reader instead of byte reads (36.6 against 29.8 ms), and
+// every check of a token as a status flag instead of an exit (35.2 against 23.7 ms: the division and the
+// big-integer path then run for every lane, and the registers spill).
 __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_wire_events(
     int64_t batch, int64_t n_frames, const uint32_t *__restrict__ frames, int64_t e2_max, int64_t e3_max,
     double4 *__restrict__ ev2, double4 *__restrict__ ev3, int64_t *__restrict__ first_t2, int32_t *__restrict__ n2,
