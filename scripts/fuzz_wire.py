@@ -12,7 +12,7 @@ host does (the same phase-2 / phase-3 events bit for bit, counts and first phase
 phone's first frame it does not take; that frame must be one of the corrupted ones, and the frames
 before it must match the host's.
 
-usage: python3 scripts/fuzz_wire.py [--cases N] [--seed S]   (exit status 1 on any difference)
+usage: python3 scripts/fuzz_wire.py [--cases N] [--seed S] [--corrupt P]   (exit status 1 on any difference)
 """
 from __future__ import annotations
 
@@ -41,8 +41,9 @@ def rand_decimal(rng):
 ODD = [" 1.5", "\t2", "0x1p-3", "inf", "-inf", "nan", "1.5abc", "1e", "1e+", ".", "-", "1..2", "++1", "1,5"]
 
 
-def phone_text(rng, n):
-    vals = (rng.standard_normal((n, 3)) * 10.0 ** rng.integers(-45, 39, (n, 3))).astype(np.float32)
+def phone_text(rng, n, corrupt_rate=0.05):
+    with np.errstate(over="ignore"):  # beyond the float range: +-inf, printed "Infinity"
+        vals = (rng.standard_normal((n, 3)) * 10.0 ** rng.integers(-45, 39, (n, 3))).astype(np.float32)
     for special in (np.nan, np.inf, -np.inf, np.float32(1.4e-45), np.float32(-0.0)):
         vals[rng.random(vals.shape) < 0.01] = special
     t = int(rng.integers(0, 10 ** 13)) + np.cumsum(rng.integers(0, 4_000_000, n))
@@ -57,16 +58,16 @@ def phone_text(rng, n):
         ty = str(rng.choice(["0", "1", "2", "0", "1", "2", "7", "x"]))
         toks = [wire.java_float_string(v) for v in vals[i]]
         bad = False
-        if rng.random() < 0.05:
+        if rng.random() < corrupt_rate:
             k = int(rng.integers(0, 3))
             toks[k] = rand_decimal(rng) if rng.random() < 0.7 else str(rng.choice(ODD))
             bad = True
         s = "#%d,%s:%s,%s,%s,t:%d" % (phase, ty, toks[0], toks[1], toks[2], t[i])
-        if rng.random() < 0.01:
+        if rng.random() < corrupt_rate / 5:
             j = int(rng.integers(1, len(s)))
             s = s[:j] + s[j + 1:]
             bad = True
-        if rng.random() < 0.005:
+        if rng.random() < corrupt_rate / 10:
             j = int(rng.integers(0, len(s)))
             s = s[:j] + chr(int(rng.integers(1, 127))) + s[j + 1:]
             bad = True
@@ -96,6 +97,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", type=int, default=20)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--corrupt", type=float, default=0.05, help="per-frame probability of a replaced number")
     a = ap.parse_args(argv)
     rng = np.random.default_rng(a.seed)
     n_frames = n_bad_phones = differ = 0
@@ -103,7 +105,7 @@ def main(argv=None):
         K = int(rng.integers(64, 301))
         texts, corr = [], []
         for _ in range(K):
-            fr, c = phone_text(rng, int(rng.integers(1, 120)))
+            fr, c = phone_text(rng, int(rng.integers(1, 120)), a.corrupt)
             texts.append(fr)
             corr.append(c)
         F = max(len(t) for t in texts)
