@@ -14,6 +14,9 @@
 // type} (type 3 for a Type no sensor takes); the rows after a phone's last message get the no-message
 // event.
 //
+// Frames in the client's own form are parsed without a character loop (wire_frame_fast: digit masks of
+// 16-byte windows, 8 digits per SWAR conversion); any other frame by wire_frame, the general parser.
+//
 // The values are std::stod's -- strtod's correctly rounded double of the decimal -- bit for bit: a
 // decimal of at most 19 significant digits m and exponent e with m <= 2^53 and |e| <= 22 is one IEEE
 // multiply or divide of two exact doubles (the case of every sensor reading); any other m < 2^64 with
@@ -204,6 +207,136 @@ struct WireMsg {
     long long t;
 };
 
+// ---- the client's own form, without a character loop ----
+// Every frame the client prints has one shape: "#p,T:" then three Float.toString numbers
+// ([-]D+.D+ or [-]D.D+E[-]D+, at most 9 significant digits) and "t:" with the decimal time.  Each
+// token is classified from a window of its bytes at once -- a 16- or 20-bit mask of the digit bytes,
+// found 4 bytes per dword operation -- and its digit runs converted 8 at a time (SWAR: byte pairs, then
+// quads, then the 8 digits, shifts and 24-bit multiplies).  A token in any other form, or longer than
+// the window, sends the frame to wire_frame, which decides it; where this path accepts a frame,
+// wire_frame would produce the same message bit for bit: the same integer mantissa m < 10^15 and
+// exponent, and the same one IEEE multiply or divide.
+
+// bit j (j < 4): byte j of x is not a decimal digit
+__device__ __forceinline__ uint32_t other_bits4(uint32_t x) {
+    const uint32_t y = x ^ 0x30303030u;                                         // a digit: a byte below 10
+    const uint32_t a = ((((y & 0x7f7f7f7fu) + 0x76767676u) | y) & 0x80808080u) >> 7;  // bits 0, 8, 16, 24
+    const uint32_t b = a | (a >> 7);                                            // bytes 0, 1 at bits 0, 1
+    return (b | (b >> 14)) & 0xfu;                                              // bytes 2, 3 at bits 2, 3
+}
+
+// the value of 8 decimal digits, byte 0 of lo the most significant (each byte 0..9)
+__device__ __forceinline__ uint32_t swar8(uint32_t lo, uint32_t hi) {
+    auto quad = [](uint32_t x) {  // (24-bit multiplies: full rate)
+        const uint32_t pr = (x & 0x00ff00ffu) * 10u + ((x >> 8) & 0x00ff00ffu);  // 10 a + b, 10 c + d
+        return (pr & 0xffffu) * 100u + (pr >> 16);                               // 100 (10 a + b) + 10 c + d
+    };
+    return quad(lo) * 10000u + quad(hi);
+}
+
+// the value of the L (1..8) digit characters in bytes 0..L-1 of (hi:lo)
+__device__ __forceinline__ uint32_t digits_value(uint32_t lo, uint32_t hi, int L) {
+    // per dword: a byte below the digits never borrows (each digit byte is >= '0')
+    uint64_t v = ((uint64_t)(hi - 0x30303030u) << 32) | (uint32_t)(lo - 0x30303030u);
+    v <<= 8 * (8 - L);  // the bytes past the digits leave at the top, leading zeros come in below
+    return swar8((uint32_t)v, (uint32_t)(v >> 32));
+}
+
+// 8 bytes of the frame from byte pos (fr32: the frame's dwords in LDS)
+__device__ __forceinline__ void wire_rd64(const uint32_t *fr32, int pos, uint32_t &lo, uint32_t &hi) {
+    const int a = pos >> 2, s = pos & 3;
+    const uint32_t d0 = fr32[a], d1 = fr32[a + 1], d2 = fr32[a + 2];
+    lo = __builtin_amdgcn_alignbyte(d1, d0, s);
+    hi = __builtin_amdgcn_alignbyte(d2, d1, s);
+}
+
+// A number at byte i of the form [-]D{1,8}.D{1,15}(E[-]D{1,2})? with at most 15 digits, all within 16
+// bytes including the ',' after it, and |e10| <= 22.  i moves past the ','.  False: not this form.
+__device__ __forceinline__ bool wire_number_fast(const uint32_t *fr32, const double *p10, int &i, double &out) {
+    const int a = i >> 2, s = i & 3;
+    const uint32_t d0 = fr32[a], d1 = fr32[a + 1], d2 = fr32[a + 2], d3 = fr32[a + 3], d4 = fr32[a + 4];
+    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, s), w1 = __builtin_amdgcn_alignbyte(d2, d1, s),
+                   w2 = __builtin_amdgcn_alignbyte(d3, d2, s), w3 = __builtin_amdgcn_alignbyte(d4, d3, s);
+    // bit j: byte j is not a digit (every bit from 16 up is set: past the window)
+    const uint32_t nd =
+        other_bits4(w0) | other_bits4(w1) << 4 | other_bits4(w2) << 8 | other_bits4(w3) << 12 | 0xffff0000u;
+    const int o = (w0 & 0xffu) == '-';
+    const int p = __builtin_ctz(nd >> o << o);                 // the '.'
+    const int q = __builtin_ctz(nd >> (p + 1) << (p + 1));     // past the fraction: 'E' or ','
+    const int nI = p - o, nF = q - p - 1;
+    const uint32_t wp = p < 4 ? w0 : (p < 8 ? w1 : w2);        // (p <= 9 where nI <= 8)
+    bool ok = nI >= 1 && nI <= 8 && ((wp >> (8 * (p & 3))) & 0xffu) == '.' && nF >= 1 && nI + nF <= 15;
+    uint32_t elo, ehi;
+    wire_rd64(fr32, i + q, elo, ehi);
+    const uint64_t ev = ((uint64_t)ehi << 32) | elo;
+    const bool has_e = (elo & 0xffu) == 'E';
+    const int eneg = has_e && ((elo >> 8) & 0xffu) == '-';
+    const int r0 = q + 1 + eneg;
+    const int r = has_e ? __builtin_ctz(nd >> r0 << r0) : q;   // the ','
+    const int ne = r - r0;
+    const uint64_t ex = ev >> (8 * (r0 - q));
+    const int x0 = (int)(ex & 0xffu) - '0', x1 = (int)((ex >> 8) & 0xffu) - '0';
+    const int e = ne == 2 ? x0 * 10 + x1 : x0;
+    const int rq = r - q < 7 ? r - q : 7;
+    ok = ok && ((ev >> (8 * rq)) & 0xffu) == ',' && r <= 15 && (!has_e || (ne >= 1 && ne <= 2));
+    const int e10 = (has_e ? (eneg ? -e : e) : 0) - nF;
+    ok = ok && e10 >= -22 && e10 <= 22;
+    // m = I 10^nF + FA 10^(nF - 8) + FB: the integer digits, the first 8 and the rest of the fraction
+    auto clamp = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
+    const uint32_t I = digits_value(__builtin_amdgcn_alignbyte(w1, w0, o), __builtin_amdgcn_alignbyte(w2, w1, o),
+                                    clamp(nI, 1, 8));
+    uint32_t flo, fhi, glo, ghi;
+    wire_rd64(fr32, i + p + 1, flo, fhi);
+    wire_rd64(fr32, i + p + 9, glo, ghi);
+    const int LB = clamp(nF - 8, 0, 8);
+    const uint32_t FA = digits_value(flo, fhi, clamp(nF, 1, 8));
+    const uint32_t FB = LB > 0 ? digits_value(glo, ghi, LB) : 0u;
+    const double F = fma((double)FA, p10[LB], (double)FB);      // exact: integers below 10^15
+    const double m = fma((double)I, p10[clamp(nF, 0, 22)], F);
+    const double v = e10 < 0 ? m / p10[clamp(-e10, 0, 22)] : m * p10[clamp(e10, 0, 22)];
+    out = o ? -v : v;
+    i += (r < 15 ? r : 15) + 1;
+    return ok;
+}
+
+// "t:" and 1..16 digits at byte i, then any non-digit
+__device__ __forceinline__ bool wire_time_fast(const uint32_t *fr32, int i, long long &t) {
+    const int a = i >> 2, s = i & 3;
+    const uint32_t d0 = fr32[a], d1 = fr32[a + 1], d2 = fr32[a + 2], d3 = fr32[a + 3], d4 = fr32[a + 4],
+                   d5 = fr32[a + 5];
+    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, s), w1 = __builtin_amdgcn_alignbyte(d2, d1, s),
+                   w2 = __builtin_amdgcn_alignbyte(d3, d2, s), w3 = __builtin_amdgcn_alignbyte(d4, d3, s),
+                   w4 = __builtin_amdgcn_alignbyte(d5, d4, s);
+    const uint32_t nd = other_bits4(w0) | other_bits4(w1) << 4 | other_bits4(w2) << 8 | other_bits4(w3) << 12 |
+                        other_bits4(w4) << 16 | 0xfff00000u;
+    const int n = __builtin_ctz(nd & ~3u) - 2;  // digits from byte 2
+    const bool ok = (w0 & 0xffffu) == ('t' | ':' << 8) && n >= 1 && n <= 16;
+    // the last min(n, 8) digits and those before them
+    const int LA = n - 8 > 0 ? n - 8 : 0, LB = n < 8 ? (n > 0 ? n : 1) : 8;
+    uint32_t lo, hi;
+    wire_rd64(fr32, i + 2 + LA, lo, hi);
+    const uint32_t B = digits_value(lo, hi, LB);
+    wire_rd64(fr32, i + 2, lo, hi);
+    const uint32_t A = LA > 0 ? digits_value(lo, hi, LA < 8 ? LA : 8) : 0u;
+    t = (long long)((uint64_t)A * 100000000ull + B);
+    return ok;
+}
+
+// 0: a message; 1: no message (no '#'); 3: not the client's own form: wire_frame decides
+__device__ __forceinline__ int wire_frame_fast(const uint32_t *fr32, const double *p10, WireMsg &m) {
+    const uint32_t h0 = fr32[0], h1 = fr32[1];
+    if ((h0 & 0xffu) != '#') return 1;
+    m.phase = (uint8_t)(h0 >> 8);
+    m.type = (uint8_t)(h0 >> 24);
+    bool ok = (h1 & 0xffu) == ':' && m.type != ':' && m.type != 0;  // one Type character, the first ':'
+    int i = 5;
+    ok = wire_number_fast(fr32, p10, i, m.v[0]) && ok;
+    ok = wire_number_fast(fr32, p10, i, m.v[1]) && ok;
+    ok = wire_number_fast(fr32, p10, i, m.v[2]) && ok;
+    ok = wire_time_fast(fr32, i, m.t) && ok;
+    return ok ? 0 : 3;
+}
+
 // 0: a message (m filled); 1: no message (no '#': Parser::run skips it); 2: not parsed here (see above)
 __device__ int wire_frame(const uint8_t *fr, WireMsg &m) {
     auto ch = [&](int j) -> unsigned {
@@ -248,57 +381,53 @@ __device__ int wire_frame(const uint8_t *fr, WireMsg &m) {
     return 0;
 }
 
-// Held to 3 waves per SIMD (168 VGPRs, 4 of them spilled on the rare big-integer path; the compiler's
-// choice was 201 = 2 waves): the parse is a chain of dependent LDS reads and divergent branches, and the
-// third wave hides part of it.  262,144 phones x 1,024 frames, same box (profiles/r6/wire_dev/): 29.8 ms
-// (byte loops with early exits, 2 waves) -> 27.5 (branch-free digit loops) -> 25.4 ms (and 3 waves) ->
-// 23.6 ms (the character loops exit when no lane of the wave is still in them, __any, instead of lane by
-// lane).  Measured and not kept: a dword-window reader instead of byte reads (36.6 against 29.8 ms), and
-// every check of a token as a status flag instead of an exit (35.2 against 23.7 ms: the division and the
-// big-integer path then run for every lane, and the registers spill).
-__global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_wire_events(
+// Two loops over the frame indices: the client's own form (wire_frame_fast) for every phone, then, for the
+// phones that met a frame in another form, wire_frame from that frame on.  Held to 4 waves per SIMD
+// (128 VGPRs: the fast loop needs 126 and does not spill; the second loop's big-integer path does).
+// 262,144 phones x 1,024 frames, same box (profiles/r6/wire_dev/): the character loops of wire_frame
+// alone took 29.8 ms (byte loops with early exits, 2 waves) -> 27.5 (branch-free digit loops) -> 25.4 ms
+// (3 waves) -> 23.6 ms (loop exits wave-uniform, __any); the fast form, 7.9 ms (926 VALU per wave and frame
+// against 1,302 VALU + 1,352 SALU, and no chain of dependent one-byte LDS reads).  Measured and not
+// kept: a dword-window reader instead of byte reads (36.6 against 29.8 ms), and every check of a token as a
+// status flag instead of an exit (35.2 against 23.7 ms: the division and the big-integer path then run for
+// every lane, and the registers spill).
+__global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_wire_events(
     int64_t batch, int64_t n_frames, const uint32_t *__restrict__ frames, int64_t e2_max, int64_t e3_max,
     double4 *__restrict__ ev2, double4 *__restrict__ ev3, int64_t *__restrict__ first_t2, int32_t *__restrict__ n2,
     int32_t *__restrict__ n3, int32_t *__restrict__ bad_frame, int *__restrict__ err) {
     __shared__ uint32_t lds[kWireDwords];
+    __shared__ double p10[23];
     const int lane = threadIdx.x;
+    if (lane < 23) p10[lane] = kWirePow10[lane];
     const int64_t k0 = (int64_t)blockIdx.x * kWireBlock;
     const int64_t b = k0 + lane;
     const int nk = batch - k0 < kWireBlock ? (int)(batch - k0) : kWireBlock;  // phones in this block
     const int nd = nk * (kWireFrame / 4);  // dwords of one frame index
-    // dword j of frame index f of this block's phones (frames of one index are contiguous across phones)
+    // dword j of frame index f of this block's phones (frames of one index are contiguous across phones),
+    // through a buffer resource of exactly those frames: a lane past the block's last phone reads 0
     auto load = [&](int64_t f, uint32_t (&r)[kWireDwords / kWireBlock]) {
-        const uint32_t *src = frames + (f * batch + k0) * (kWireFrame / 4);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t *>(frames + (f * batch + k0) * (kWireFrame / 4)), 0, nd * 4, 0x00020000);
 #pragma unroll
-        for (int c = 0; c < kWireDwords / kWireBlock; ++c) {
-            const int j = c * kWireBlock + lane;
-            r[c] = j < nd ? __builtin_nontemporal_load(src + j) : 0u;
-        }
+        for (int c = 0; c < kWireDwords / kWireBlock; ++c)
+            r[c] = __builtin_amdgcn_raw_buffer_load_b32(rs, (c * kWireBlock + lane) * 4, 0, 2);
     };
     const uint8_t *fr = reinterpret_cast<const uint8_t *>(lds) + lane * kWireFrame;
-    int32_t c2 = 0, c3 = 0, bad = -1;
+    const uint32_t *fr32 = lds + lane * (kWireFrame / 4);
+    int32_t c2 = 0, c3 = 0, bad = -1, resume = -1;
     int64_t t2 = 0;
     const double4 none = ev64_null();
-    uint32_t cur[kWireDwords / kWireBlock];
-    if (n_frames > 0) load(0, cur);
-    for (int64_t f = 0; f < n_frames; ++f) {
-        __syncthreads();  // the previous index's frames are parsed
-#pragma unroll
-        for (int c = 0; c < kWireDwords / kWireBlock; ++c) lds[c * kWireBlock + lane] = cur[c];
-        __syncthreads();
-        if (f + 1 < n_frames) load(f + 1, cur);  // in flight while this index is parsed
-        if (b >= batch || bad >= 0) continue;
-        WireMsg m;
-        const int st = wire_frame(fr, m);
+    // one parsed frame: a message to its phase's plane, a refused frame ends the phone
+    auto take = [&](int st, const WireMsg &m, int64_t f) {
         if (st == 2) {
             bad = (int32_t)f;
-            continue;
+            return;
         }
-        if (st != 0 || (m.phase != '2' && m.phase != '3')) continue;  // phase 1 (calibration) and others: skipped
+        if (st != 0 || (m.phase != '2' && m.phase != '3')) return;  // phase 1 (calibration) and others: skipped
         const double td = (double)m.t;
         if (!(fabs(td) < 2251799813685248.0)) {  // the FP64 event's time limit, 2^51 ns
             bad = (int32_t)f;
-            continue;
+            return;
         }
         const uint32_t ty = (m.type >= '0' && m.type <= '2') ? (uint32_t)(m.type - '0') : 3u;
         const double4 e = make_double4(m.v[0], m.v[1], m.v[2],
@@ -311,6 +440,38 @@ __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(3)))
             if (c3 < e3_max) ev3[(int64_t)c3 * batch + b] = e;
             ++c3;
         }
+    };
+    uint32_t cur[kWireDwords / kWireBlock];
+    if (n_frames > 0) load(0, cur);
+    for (int64_t f = 0; f < n_frames; ++f) {
+        __syncthreads();  // the previous index's frames are parsed
+#pragma unroll
+        for (int c = 0; c < kWireDwords / kWireBlock; ++c) lds[c * kWireBlock + lane] = cur[c];
+        __syncthreads();
+        if (f + 1 < n_frames) load(f + 1, cur);  // in flight while this index is parsed
+        if (b >= batch || bad >= 0 || resume >= 0) continue;
+        WireMsg m;
+        const int st = wire_frame_fast(fr32, p10, m);
+        if (st == 3) {
+            resume = (int32_t)f;  // a frame in another form: this phone goes on below
+            continue;
+        }
+        take(st, m, f);
+    }
+    // The phones that met a frame in another form go on from it with wire_frame, the block's frames from
+    // the first such index staged again (a separate loop: the two parsers' registers are not live at once)
+    int f0 = resume >= 0 ? resume : INT_MAX;
+    for (int d = 1; d < kWireBlock; d <<= 1) f0 = min(f0, __shfl_xor(f0, d));
+    for (int64_t f = f0; f < n_frames; ++f) {
+        __syncthreads();
+        load(f, cur);
+#pragma unroll
+        for (int c = 0; c < kWireDwords / kWireBlock; ++c) lds[c * kWireBlock + lane] = cur[c];
+        __syncthreads();
+        if (b >= batch || bad >= 0 || resume < 0 || f < resume) continue;
+        WireMsg m;
+        const int st = wire_frame(fr, m);
+        take(st, m, f);
     }
     if (b >= batch) return;
     for (int64_t e = c2; e < e2_max; ++e) ev2[e * batch + b] = none;

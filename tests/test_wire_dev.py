@@ -126,6 +126,61 @@ def test_wire_events_number_forms(eng):
     assert _same(w["ev3"].download((F, K, 4), np.float64), _host_planes(texts, 3, F))
 
 
+def _fast_form(rng):
+    """A number of the device's fast form: [-]D{1,8}.D+(E[-]D{1,2})? with at most 15 digits."""
+    nI = int(rng.integers(1, 9))
+    nF = int(rng.integers(1, 16 - nI))
+    s = ("-" if rng.random() < 0.5 else "") + "".join(str(d) for d in rng.integers(0, 10, nI)) + "." + \
+        "".join(str(d) for d in rng.integers(0, 10, nF))
+    if rng.random() < 0.5:
+        s += "E" + ("-" if rng.random() < 0.5 else "") + str(int(rng.integers(0, 23 if rng.random() < 0.5 else 60)))
+    return s
+
+
+# at the edges of the fast form and just past them (wire_frame takes those): width, digit counts, exponents
+_EDGE_NUMBERS = ["12345678.5", "123456789.5", "12345678.1234567", "12345678.12345678", "1.23456789012345",
+                 "1.234567890123456", "0.00000000000001", "0.000000000000001", "-1234567.123456",
+                 "-1234567.1234567", "1.5E22", "1.5E-21", "1.5E-23", "9.9E-22", "1.5E79", "1.5E+5", "1.5e5",
+                 "1.5E005", "+1.5", "1.", ".5", "5", "-0.0", "0.0E-99", "1.4E-45", "3.4028235E38", "NaN",
+                 "-Infinity", "00000001.5", "1.5E-0"]
+_EDGE_TIMES = ["0", "7", "12345678", "123456789", "2251799813685247", "0000000000000005", "00000000000000005",
+               "-5", "-0"]
+
+
+@pytest.mark.gpu
+def test_wire_events_fast_form_edges(eng):
+    """The device parses the client's own form without character loops and hands every other frame to the
+    general parser -- per lane, in the same waves, a phone going on from its first such frame with the
+    general parser.  Fast-form numbers and times at their limits, the forms just past them, and frames
+    whose Type field is empty or longer, interleaved at random over 64 phones: every plane, count and
+    first phase-2 time equals the host parse bit for bit."""
+    rng = np.random.default_rng(23)
+    K = 64
+    texts = []
+    for k in range(K):
+        rows = []
+        for i in range(int(rng.integers(20, 60))):
+            u = rng.random()
+            toks = [_fast_form(rng) if rng.random() < 0.7 else str(rng.choice(_EDGE_NUMBERS)) for _ in range(3)]
+            if u < 0.85 or k % 4 == 0:      # some phones stay in the fast form throughout
+                toks = [_fast_form(rng) for _ in range(3)]
+            t = str(int(rng.integers(0, 10 ** int(rng.integers(1, 16))))) if rng.random() < 0.8 \
+                else str(rng.choice(_EDGE_TIMES))
+            ty = str(rng.choice(["0", "1", "2", "7", "12", ""])) if rng.random() < 0.2 else str(rng.integers(0, 3))
+            rows.append(_frame(toks, t, phase=int(rng.choice([2, 3, 3, 1])), ty=ty))
+        texts.append("".join(rows))
+    fr = wire.frames(texts)
+    w = eng.wire_events(fr)
+    F = fr.shape[0]
+    assert _same(w["ev2"].download((F, K, 4), np.float64), _host_planes(texts, 2, F))
+    assert _same(w["ev3"].download((F, K, 4), np.float64), _host_planes(texts, 3, F))
+    t2 = w["first_t2"].download((K,), np.int64)
+    for k, tx in enumerate(texts):
+        p = wire.parse(tx)
+        assert w["n2"][k] == (p["phase"] == 2).sum() and w["n3"][k] == (p["phase"] == 3).sum()
+        assert t2[k] == (p["times"][p["phase"] == 2][0] if (p["phase"] == 2).any() else 0)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("tok,t", [(" 1.5", "5"), ("0x1p3", "5"), ("1.5abc", "5"), ("12345678901234567890", "5"),
                                    ("1e81", "5"), ("inf", "5"), ("-NaN", "5"), ("1.5", "+5"), ("1.5", " 5"),
