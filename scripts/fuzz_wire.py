@@ -7,7 +7,10 @@ as Float.toString prints them (plain and computerized forms, subnormals, NaN, In
 (1, 2, 3, others), sensor types (0-2 and others), blank and non-'#' frames -- and, with some probability per
 frame, a corruption: a number replaced by a random decimal (1-25 digits, exponents to +-120, signs,
 leading zeros), by a form strtod reads but the client never prints (blanks, hex, inf, trailing text), a
-deleted character, or a random byte.  Per phone the device must either parse every frame exactly as the
+deleted character, or a random byte other than '\n'.  (The server takes each 100-byte recv as one message,
+KFS/Server.cpp:84-98, as the device does; the host parse splits its text at newlines -- the two agree on
+every frame without an inner newline, and a newline in the Type field would be a message to the one and
+two lines to the other.)  Per phone the device must either parse every frame exactly as the
 host does (the same phase-2 / phase-3 events bit for bit, counts and first phase-2 time), or report the
 phone's first frame it does not take; that frame must be one of the corrupted ones, and the frames
 before it must match the host's.
@@ -69,7 +72,8 @@ def phone_text(rng, n, corrupt_rate=0.05):
             bad = True
         if rng.random() < corrupt_rate / 10:
             j = int(rng.integers(0, len(s)))
-            s = s[:j] + chr(int(rng.integers(1, 127))) + s[j + 1:]
+            c = int(rng.integers(1, 126))
+            s = s[:j] + chr(c + (c >= 10)) + s[j + 1:]  # not '\n': see the module docstring
             bad = True
         if len(s) > 99:
             s = s[:99]

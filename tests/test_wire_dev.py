@@ -196,6 +196,21 @@ def test_wire_events_report_other_forms(eng, tok, t):
 
 
 @pytest.mark.gpu
+def test_wire_events_frame_is_the_message(eng):
+    """The server takes each 100-byte recv as one message (KFS/Server.cpp:84-98), and so does the device: a
+    newline inside a frame does not split it, and a Type field of '\\n' is a message of a type no sensor
+    takes (the host's line parse, made for the client's own text, would read two lines there)."""
+    good = _frame(["1.0", "2.0", "3.0"], 7, phase=2)
+    odd = "#2,\n:1.5,-2.5,3.5E-3,t:9".ljust(99) + "\n"
+    w = eng.wire_events(wire.frames([good + odd]))
+    assert w["n2"][0] == 2
+    ev = w["ev2"].download((2, 1, 4), np.float64)[1, 0]
+    assert ev[:3].tolist() == [1.5, -2.5, 3.5e-3]
+    bits = int(ev[3:4].view(np.uint64)[0])
+    assert bits & 3 == synth.EV_OTHER and np.uint64(bits & ~3).view(np.float64) == 9.0
+
+
+@pytest.mark.gpu
 def test_wire_session_equals_the_host_session(eng):
     """The whole session from wire frames on the device (run_wire_session) equals run_session on the host's
     parse of the same text (wire.events_from_wire, events="f64") bit for bit: ready, counts, refs, X, P."""
