@@ -211,27 +211,31 @@ struct WireMsg {
 // Every frame the client prints has one shape: "#p,T:" then three Float.toString numbers
 // ([-]D+.D+ or [-]D.D+E[-]D+, at most 9 significant digits) and "t:" with the decimal time.  Each
 // token is classified from a window of its bytes at once -- a 16- or 20-bit mask of the digit bytes,
-// found 4 bytes per dword operation -- and its digit runs converted 8 at a time (SWAR: byte pairs, then
-// quads, then the 8 digits, shifts and 24-bit multiplies).  A token in any other form, or longer than
+// found 4 bytes per dword operation -- and its digit runs converted 8 at a time (SWAR: 4-digit groups by
+// two byte dot products and a 24-bit multiply-add each).  A token in any other form, or longer than
 // the window, sends the frame to wire_frame, which decides it; where this path accepts a frame,
 // wire_frame would produce the same message bit for bit: the same integer mantissa m < 10^15 and
 // exponent, and the same one IEEE multiply or divide.
 
-// bit j (j < 4): byte j of x is not a decimal digit
-__device__ __forceinline__ uint32_t other_bits4(uint32_t x) {
-    const uint32_t y = x ^ 0x30303030u;                                         // a digit: a byte below 10
-    const uint32_t a = ((((y & 0x7f7f7f7fu) + 0x76767676u) | y) & 0x80808080u) >> 7;  // bits 0, 8, 16, 24
-    const uint32_t b = a | (a >> 7);                                            // bytes 0, 1 at bits 0, 1
-    return (b | (b >> 14)) & 0xfu;                                              // bytes 2, 3 at bits 2, 3
+// bit 7 of byte j: byte j of x is not a decimal digit
+__device__ __forceinline__ uint32_t other_flags(uint32_t x) {
+    const uint32_t y = x ^ 0x30303030u;                              // a digit: a byte below 10
+    return (((y & 0x7f7f7f7fu) + 0x76767676u) | y) & 0x80808080u;   // bit 7: y >= 10
+}
+// the flags of 8 bytes (two dwords) as bits 7..14 (dot products with 1, 2, 4, ... 128: 4 bytes an op)
+__device__ __forceinline__ uint32_t other_bits8(uint32_t x0, uint32_t x1) {
+    return __builtin_amdgcn_udot4(other_flags(x1), 0x80402010u,
+                                  __builtin_amdgcn_udot4(other_flags(x0), 0x08040201u, 0u, false), false);
 }
 
 // the value of 8 decimal digits, byte 0 of lo the most significant (each byte 0..9)
 __device__ __forceinline__ uint32_t swar8(uint32_t lo, uint32_t hi) {
-    auto quad = [](uint32_t x) {  // (24-bit multiplies: full rate)
-        const uint32_t pr = (x & 0x00ff00ffu) * 10u + ((x >> 8) & 0x00ff00ffu);  // 10 a + b, 10 c + d
-        return (pr & 0xffffu) * 100u + (pr >> 16);                               // 100 (10 a + b) + 10 c + d
+    // (the masks only tell the compiler that the products are 24-bit: full-rate multiplies)
+    auto quad = [](uint32_t x) {  // 100 (10 a + b) + 10 c + d: two dot products of the bytes, a 24-bit mad
+        return (__builtin_amdgcn_udot4(x, 0x0000010au, 0u, false) & 0xffu) * 100u +
+               __builtin_amdgcn_udot4(x, 0x010a0000u, 0u, false);
     };
-    return quad(lo) * 10000u + quad(hi);
+    return (quad(lo) & 0x3fffu) * 10000u + quad(hi);
 }
 
 // the value of the L (1..8) digit characters in bytes 0..L-1 of (hi:lo)
@@ -258,8 +262,7 @@ __device__ __forceinline__ bool wire_number_fast(const uint32_t *fr32, const dou
     const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, s), w1 = __builtin_amdgcn_alignbyte(d2, d1, s),
                    w2 = __builtin_amdgcn_alignbyte(d3, d2, s), w3 = __builtin_amdgcn_alignbyte(d4, d3, s);
     // bit j: byte j is not a digit (every bit from 16 up is set: past the window)
-    const uint32_t nd =
-        other_bits4(w0) | other_bits4(w1) << 4 | other_bits4(w2) << 8 | other_bits4(w3) << 12 | 0xffff0000u;
+    const uint32_t nd = (other_bits8(w0, w1) >> 7) | (other_bits8(w2, w3) << 1) | 0xffff0000u;
     const int o = (w0 & 0xffu) == '-';
     const int p = __builtin_ctz(nd >> o << o);                 // the '.'
     const int q = __builtin_ctz(nd >> (p + 1) << (p + 1));     // past the fraction: 'E' or ','
@@ -307,8 +310,8 @@ __device__ __forceinline__ bool wire_time_fast(const uint32_t *fr32, int i, long
     const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, s), w1 = __builtin_amdgcn_alignbyte(d2, d1, s),
                    w2 = __builtin_amdgcn_alignbyte(d3, d2, s), w3 = __builtin_amdgcn_alignbyte(d4, d3, s),
                    w4 = __builtin_amdgcn_alignbyte(d5, d4, s);
-    const uint32_t nd = other_bits4(w0) | other_bits4(w1) << 4 | other_bits4(w2) << 8 | other_bits4(w3) << 12 |
-                        other_bits4(w4) << 16 | 0xfff00000u;
+    const uint32_t nd = (other_bits8(w0, w1) >> 7) | (other_bits8(w2, w3) << 1) |
+                        (__builtin_amdgcn_udot4(other_flags(w4), 0x08040201u, 0u, false) << 9) | 0xfff00000u;
     const int n = __builtin_ctz(nd & ~3u) - 2;  // digits from byte 2
     const bool ok = (w0 & 0xffffu) == ('t' | ':' << 8) && n >= 1 && n <= 16;
     // the last min(n, 8) digits and those before them
@@ -386,8 +389,9 @@ __device__ int wire_frame(const uint8_t *fr, WireMsg &m) {
 // (128 VGPRs: the fast loop needs 126 and does not spill; the second loop's big-integer path does).
 // 262,144 phones x 1,024 frames, same box (profiles/r6/wire_dev/): the character loops of wire_frame
 // alone took 29.8 ms (byte loops with early exits, 2 waves) -> 27.5 (branch-free digit loops) -> 25.4 ms
-// (3 waves) -> 23.6 ms (loop exits wave-uniform, __any); the fast form, 7.9 ms (926 VALU per wave and frame
-// against 1,302 VALU + 1,352 SALU, and no chain of dependent one-byte LDS reads).  Measured and not
+// (3 waves) -> 23.6 ms (loop exits wave-uniform, __any); the fast form, 7.9 ms (800 VALU per wave and frame
+// against 1,302 VALU + 1,352 SALU, and no chain of dependent one-byte LDS reads), 7.8 ms with dot products
+// for the mask gathers and SWAR steps (656 VALU; what it waits for is each lane's chain of token windows).  Measured and not
 // kept: a dword-window reader instead of byte reads (36.6 against 29.8 ms), and every check of a token as a
 // status flag instead of an exit (35.2 against 23.7 ms: the division and the big-integer path then run for
 // every lane, and the registers spill).
