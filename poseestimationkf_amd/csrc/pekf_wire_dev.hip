@@ -391,7 +391,8 @@ __device__ int wire_frame(const uint8_t *fr, WireMsg &m) {
 // alone took 29.8 ms (byte loops with early exits, 2 waves) -> 27.5 (branch-free digit loops) -> 25.4 ms
 // (3 waves) -> 23.6 ms (loop exits wave-uniform, __any); the fast form, 7.9 ms (800 VALU per wave and frame
 // against 1,302 VALU + 1,352 SALU, and no chain of dependent one-byte LDS reads), 7.8 ms with dot products
-// for the mask gathers and SWAR steps (656 VALU; what it waits for is each lane's chain of token windows).  Measured and not
+// for the mask gathers and SWAR steps (656 VALU).  Not kept: the frame's commas found first so the four
+// token windows are independent (+90 VALU, 1 % slower).  Measured and not
 // kept: a dword-window reader instead of byte reads (36.6 against 29.8 ms), and every check of a token as a
 // status flag instead of an exit (35.2 against 23.7 ms: the division and the big-integer path then run for
 // every lane, and the registers spill).
