@@ -343,7 +343,8 @@ int pekf_frontend_init_ext_dev(int64_t batch, int64_t n_events, const void *ev_p
 /* The wire on the device: the clients' 100-byte frames (as MessageSender.java:217-233 sends and Server.cpp:35,84
  * receives them: "#<phase>,<type>:<x>,<y>,<z>,t:<ns>", spaces to 99 characters, '\n') -> FP64 event planes.
  * frames: [n_frames][batch][100] bytes (device; 4-byte aligned), phone b's frames in order along the first
- * axis (a frame not starting with '#' is no message, e.g. padding).  Each phase-2 / phase-3 message of phone b
+ * axis (a frame not starting with '#' is no message, e.g. padding; a frame is one message whatever it holds,
+ * as the server takes each recv -- a newline inside it does not split it).  Each phase-2 / phase-3 message of phone b
  * becomes the next row of ev2 / ev3 ([e2_max][batch] / [e3_max][batch] double4, PEKF_EV_F64_EVENTS' form;
  * type 3 for a Type no sensor takes); rows after its last message get the no-message event.  n2 / n3[batch]:
  * messages per phase (more than e_max: *dev_error |= 2, the extra ones dropped); first_t2[batch]: the time of
