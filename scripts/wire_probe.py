@@ -4,7 +4,7 @@ client text, 1,024 generated phones' phase-3 streams tiled x256), then the devic
 (engine.run_wire_session: frames -> FP64 events -> phase 2 -> k_live) on a smaller set.  Prints one JSON
 line: kernel ms (HIP events, median of reps), frames/s, GB/s of frames read + events written.
 
-usage: python3 scripts/wire_probe.py [reps] [--session]
+usage: python3 scripts/wire_probe.py [reps] [--session] [--tile T (phones = 1,024 T; default 256)]
 """
 from __future__ import annotations
 
@@ -22,8 +22,9 @@ from poseestimationkf_amd._lib import check, lib  # noqa: E402
 
 
 def main():
-    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    K0, E, tile = 1024, 1024, 256
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 5
+    tile = int(sys.argv[sys.argv.index("--tile") + 1]) if "--tile" in sys.argv else 256
+    K0, E = 1024, 1024
     t0 = time.time()
     ev = synth.generate_events(np.arange(K0), E, seed=5)
     texts = [wire.events_text(ev["types"][:, k], ev["values"][:, k], ev["times"][:, k]) for k in range(K0)]
