@@ -8,8 +8,8 @@
 // (Parser::run, KFS/Parser.cpp:357-363) and parses them in ProcessString (:12-26): phase = the first
 // character, Type = the first character before the first ':', each value std::stod of the text before the
 // next ',', the time std::stoll of the text after "t:".  One lane per phone walks its frames in order
-// ([n_frames][batch][100] bytes: a wave's 64 frames of one index are 6,400 contiguous bytes, staged
-// through LDS with coalesced dword loads, the next index's in flight while this one is parsed), and
+// ([n_frames][batch][100] bytes: a wave's 64 frames of one index are 6,400 contiguous bytes, brought
+// into LDS by buffer loads to LDS, the next index's in flight while this one is parsed), and
 // appends each phase-2 / phase-3 message to that phase's plane as the FP64 event {x, y, z, bits(t) |
 // type} (type 3 for a Type no sensor takes); the rows after a phone's last message get the no-message
 // event.
@@ -33,6 +33,10 @@ namespace pekf {
 constexpr int kWireFrame = 100;  // bytes per message, as sent and as received
 constexpr int kWireBlock = 64;   // one wave per block: 6,400 B of frames in LDS
 constexpr int kWireDwords = kWireFrame * kWireBlock / 4;  // 1,600
+// The fast form reads at most a frame's first 76 bytes: tokens of at most 16 bytes from byte 5, the time's
+// window of 20 from at most byte 53 (see wire_frame_fast)
+constexpr int kFastDwords = 19;
+constexpr int kFastSlot = kFastDwords * kWireBlock;  // 1,216 dwords: 64 frames' first 76 bytes
 
 __constant__ double kWirePow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
                                       1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
@@ -391,17 +395,22 @@ __device__ int wire_frame(const uint8_t *fr, WireMsg &m) {
 // alone took 29.8 ms (byte loops with early exits, 2 waves) -> 27.5 (branch-free digit loops) -> 25.4 ms
 // (3 waves) -> 23.6 ms (loop exits wave-uniform, __any); the fast form, 7.9 ms (800 VALU per wave and frame
 // against 1,302 VALU + 1,352 SALU, and no chain of dependent one-byte LDS reads), 7.8 ms with dot products
-// for the mask gathers and SWAR steps (656 VALU).  Not kept: the frame's commas found first so the four
-// token windows are independent (+90 VALU, 1 % slower).  Measured and not
-// kept: a dword-window reader instead of byte reads (36.6 against 29.8 ms), and every check of a token as a
+// for the mask gathers and SWAR steps (656 VALU), 7.7 ms with the frames' first 76 bytes brought into a
+// two-slot LDS ring by buffer loads to LDS (no registers for the frame in flight; parsing without loads
+// at all takes 5.4 ms).  Not kept: the frame's commas found first so the four token windows are
+// independent (+90 VALU, 1 % slower); two frames per lane and step at low occupancy (no gain); a
+// dword-window reader instead of byte reads (36.6 against 29.8 ms), and every check of a token as a
 // status flag instead of an exit (35.2 against 23.7 ms: the division and the big-integer path then run for
 // every lane, and the registers spill).
 __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_wire_events(
     int64_t batch, int64_t n_frames, const uint32_t *__restrict__ frames, int64_t e2_max, int64_t e3_max,
     double4 *__restrict__ ev2, double4 *__restrict__ ev3, int64_t *__restrict__ first_t2, int32_t *__restrict__ n2,
     int32_t *__restrict__ n3, int32_t *__restrict__ bad_frame, int *__restrict__ err) {
-    __shared__ uint32_t lds[kWireDwords];
-    __shared__ double p10[23];
+    // One LDS array (a second __shared__ object can make the compiler drain the DMA ring, vmcnt(0)):
+    // the fast loop's ring of two slots of 64 frames' first 76 bytes, written by buffer loads to LDS; the
+    // second loop's 64 whole frames; the powers of ten at the end.
+    __shared__ __attribute__((aligned(16))) uint32_t lds[2 * kFastSlot + 46];
+    double *p10 = reinterpret_cast<double *>(lds + 2 * kFastSlot);
     const int lane = threadIdx.x;
     if (lane < 23) p10[lane] = kWirePow10[lane];
     const int64_t k0 = (int64_t)blockIdx.x * kWireBlock;
@@ -410,15 +419,42 @@ __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4)))
     const int nd = nk * (kWireFrame / 4);  // dwords of one frame index
     // dword j of frame index f of this block's phones (frames of one index are contiguous across phones),
     // through a buffer resource of exactly those frames: a lane past the block's last phone reads 0
+    // (6 x 16 bytes per lane, 1 KiB per wave-instruction, and one dword: the 6,400 bytes of a frame index)
     auto load = [&](int64_t f, uint32_t (&r)[kWireDwords / kWireBlock]) {
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint32_t *>(frames + (f * batch + k0) * (kWireFrame / 4)), 0, nd * 4, 0x00020000);
 #pragma unroll
-        for (int c = 0; c < kWireDwords / kWireBlock; ++c)
-            r[c] = __builtin_amdgcn_raw_buffer_load_b32(rs, (c * kWireBlock + lane) * 4, 0, 2);
+        for (int c = 0; c < 6; ++c) {
+            const uint4 v = __builtin_bit_cast(
+                uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, c * 1024 + lane * 16, 0, 2));
+            r[4 * c] = v.x, r[4 * c + 1] = v.y, r[4 * c + 2] = v.z, r[4 * c + 3] = v.w;
+        }
+        r[24] = __builtin_amdgcn_raw_buffer_load_b32(rs, 6144 + lane * 4, 0, 2);
+    };
+    auto stage = [&](const uint32_t (&r)[kWireDwords / kWireBlock]) {
+#pragma unroll
+        for (int c = 0; c < 6; ++c)
+            *reinterpret_cast<uint4 *>(lds + 256 * c + 4 * lane) = make_uint4(r[4 * c], r[4 * c + 1], r[4 * c + 2],
+                                                                              r[4 * c + 3]);
+        lds[1536 + lane] = r[24];
+    };
+    // The fast loop's DMA: dword j (j < 64 x 19) of a slot is dword j % 19 of the block's frame j / 19
+    uint32_t off[kFastDwords];
+#pragma unroll
+    for (int c = 0; c < kFastDwords; ++c) {
+        const int j = c * kWireBlock + lane;
+        off[c] = (uint32_t)((j / kFastDwords) * kWireFrame + (j % kFastDwords) * 4);
+    }
+    auto dma = [&](int64_t f, int slot) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t *>(frames + (f * batch + k0) * (kWireFrame / 4)), 0, nd * 4, 0x00020000);
+#pragma unroll
+        for (int c = 0; c < kFastDwords; ++c)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, (__attribute__((address_space(3))) void *)(lds + slot * kFastSlot + c * kWireBlock), 4, off[c],
+                0, 0, 2);
     };
     const uint8_t *fr = reinterpret_cast<const uint8_t *>(lds) + lane * kWireFrame;
-    const uint32_t *fr32 = lds + lane * (kWireFrame / 4);
     int32_t c2 = 0, c3 = 0, bad = -1, resume = -1;
     int64_t t2 = 0;
     const double4 none = ev64_null();
@@ -446,17 +482,21 @@ __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4)))
             ++c3;
         }
     };
-    uint32_t cur[kWireDwords / kWireBlock];
-    if (n_frames > 0) load(0, cur);
+    // One wave per block: no barrier (its fence would wait for the ring, vmcnt(0)); the wave's own waits
+    // order its DMA and its LDS reads.  Frame index f + 1's DMA is in flight while f is parsed; loads
+    // return in order, so at most 19 outstanding vector memory operations (whatever event stores are among
+    // them) means that all of f's have landed.
+    if (n_frames > 0) dma(0, 0);
     for (int64_t f = 0; f < n_frames; ++f) {
-        __syncthreads();  // the previous index's frames are parsed
-#pragma unroll
-        for (int c = 0; c < kWireDwords / kWireBlock; ++c) lds[c * kWireBlock + lane] = cur[c];
-        __syncthreads();
-        if (f + 1 < n_frames) load(f + 1, cur);  // in flight while this index is parsed
+        if (f + 1 < n_frames) {
+            dma(f + 1, (int)((f + 1) & 1));
+            asm volatile("s_waitcnt vmcnt(19)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         if (b >= batch || bad >= 0 || resume >= 0) continue;
         WireMsg m;
-        const int st = wire_frame_fast(fr32, p10, m);
+        const int st = wire_frame_fast(lds + (f & 1) * kFastSlot + lane * kFastDwords, p10, m);
         if (st == 3) {
             resume = (int32_t)f;  // a frame in another form: this phone goes on below
             continue;
@@ -467,11 +507,11 @@ __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4)))
     // the first such index staged again (a separate loop: the two parsers' registers are not live at once)
     int f0 = resume >= 0 ? resume : INT_MAX;
     for (int d = 1; d < kWireBlock; d <<= 1) f0 = min(f0, __shfl_xor(f0, d));
+    uint32_t cur[kWireDwords / kWireBlock];
     for (int64_t f = f0; f < n_frames; ++f) {
         __syncthreads();
         load(f, cur);
-#pragma unroll
-        for (int c = 0; c < kWireDwords / kWireBlock; ++c) lds[c * kWireBlock + lane] = cur[c];
+        stage(cur);
         __syncthreads();
         if (b >= batch || bad >= 0 || resume < 0 || f < resume) continue;
         WireMsg m;
