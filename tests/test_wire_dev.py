@@ -196,6 +196,38 @@ def test_wire_events_report_other_forms(eng, tok, t):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("K,F", [(1, 1), (65, 1), (65, 2), (64, 3), (129, 5)])
+def test_wire_events_ring_edges(eng, K, F):
+    """The two-slot LDS ring at its ends -- one or two frame indices, a last block of one phone --, with
+    phase-2 and phase-3 messages, blank frames and, on some phones, a frame for the general parser in the
+    middle: the planes, counts and first phase-2 times equal the host parse's."""
+    rng = np.random.default_rng(K * 10 + F)
+    texts = []
+    for k in range(K):
+        rows = []
+        for i in range(F):
+            u = rng.random()
+            if u < 0.15:
+                rows.append(" " * 99 + "\n")
+            else:
+                toks = [_fast_form(rng) for _ in range(3)]
+                if k % 3 == 1 and i == F // 2:
+                    toks[1] = "+1.5e3"                      # not the fast form: the general parser takes it
+                rows.append(_frame(toks, int(rng.integers(0, 10 ** 12)), phase=int(rng.choice([2, 3])),
+                                   ty=int(rng.integers(0, 3))))
+        texts.append("".join(rows))
+    fr = wire.frames(texts)
+    w = eng.wire_events(fr)
+    assert _same(w["ev2"].download((F, K, 4), np.float64), _host_planes(texts, 2, F))
+    assert _same(w["ev3"].download((F, K, 4), np.float64), _host_planes(texts, 3, F))
+    t2 = w["first_t2"].download((K,), np.int64)
+    for k, tx in enumerate(texts):
+        p = wire.parse(tx)
+        assert w["n2"][k] == (p["phase"] == 2).sum() and w["n3"][k] == (p["phase"] == 3).sum()
+        assert t2[k] == (p["times"][p["phase"] == 2][0] if (p["phase"] == 2).any() else 0)
+
+
+@pytest.mark.gpu
 def test_wire_events_frame_is_the_message(eng):
     """The server takes each 100-byte recv as one message (KFS/Server.cpp:84-98), and so does the device: a
     newline inside a frame does not split it, and a Type field of '\\n' is a message of a type no sensor
