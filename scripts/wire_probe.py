@@ -4,7 +4,7 @@ client text, 1,024 generated phones' phase-3 streams tiled x256), then the devic
 (engine.run_wire_session: frames -> FP64 events -> phase 2 -> k_live) on a smaller set.  Prints one JSON
 line: kernel ms (HIP events, median of reps), frames/s, GB/s of frames read + events written.
 
-usage: python3 scripts/wire_probe.py [reps] [--session] [--tile T (phones = 1,024 T; default 256)] [--no-check]
+usage: python3 scripts/wire_probe.py [reps] [--session] [--tile T (phones = 1,024 T; default 256)] [--drift D] [--no-check]
 """
 from __future__ import annotations
 
@@ -28,13 +28,21 @@ def main():
     t0 = time.time()
     ev = synth.generate_events(np.arange(K0), E, seed=5)
     texts = [wire.events_text(ev["types"][:, k], ev["values"][:, k], ev["times"][:, k]) for k in range(K0)]
-    fr0 = wire.frames(texts)                                   # [E][K0][100]
+    drift = int(sys.argv[sys.argv.index("--drift") + 1]) if "--drift" in sys.argv else 0
+    if drift:  # up to `drift` blank frames at random places in each phone's stream: its rows drift apart
+        rng = np.random.default_rng(6)
+        for k in range(K0):
+            rows = [texts[k][i:i + 100] for i in range(0, len(texts[k]), 100)]
+            for _ in range(int(rng.integers(0, drift + 1))):
+                rows.insert(int(rng.integers(0, len(rows) + 1)), " " * 99 + "\n")
+            texts[k] = "".join(rows)
+    fr0 = wire.frames(texts)                                   # [F][K0][100]
     fr = np.ascontiguousarray(np.tile(fr0, (1, tile, 1)))       # [E][K0 * tile][100]
     gen_s = time.time() - t0
     F, K = fr.shape[:2]
     fb = engine.DeviceBuffer(fr.nbytes).upload(fr)
     del fr
-    ev2, ev3 = engine.DeviceBuffer(32), engine.DeviceBuffer(32 * F * K)
+    ev2, ev3 = engine.DeviceBuffer(32), engine.DeviceBuffer(32 * E * K)  # E phase-3 messages per phone
     t2b, n2b, n3b, badb = (engine.DeviceBuffer(8 * K), engine.DeviceBuffer(4 * K), engine.DeviceBuffer(4 * K),
                            engine.DeviceBuffer(4 * K))
     errb = engine.DeviceBuffer(4).upload(np.zeros(1, np.int32))
@@ -43,7 +51,7 @@ def main():
     ms = []
     for _ in range(reps):
         e0.record(st.handle)
-        check(lib.pekf_wire_events_dev(K, F, fb.ptr, 0, F, ev2.ptr, ev3.ptr, t2b.ptr, n2b.ptr, n3b.ptr, badb.ptr,
+        check(lib.pekf_wire_events_dev(K, F, fb.ptr, 0, E, ev2.ptr, ev3.ptr, t2b.ptr, n2b.ptr, n3b.ptr, badb.ptr,
                                        errb.ptr, st.handle))
         e1.record(st.handle)
         e1.sync()
@@ -53,16 +61,16 @@ def main():
     n3 = n3b.download((K,), np.int32) if check_out else np.full(K, E)
     assert np.all(n3 == E)
     # spot check against the host parse: phone 0 and a tiled copy of it
-    got = ev3.download((F, K, 4), np.float64)[:, [0, K0 * 7]]
+    got = ev3.download((E, K, 4), np.float64)[:, [0, K0 * 7]]
     want = synth.pack_events64(wire.events_from_wire(texts[:1], np.zeros((1, 3)), np.zeros((1, 3)), [0]))
     assert not check_out or np.array_equal(got[:, 0].view(np.uint64), want[:, 0].view(np.uint64))
     assert not check_out or np.array_equal(got[:, 1].view(np.uint64), want[:, 0].view(np.uint64))
     med = float(np.median(ms[1:] if len(ms) > 1 else ms))
     frames = F * K
-    byts = frames * (100 + 32)
-    print(json.dumps(dict(kernel="k_wire_events", phones=K, frames_per_phone=F, kernel_ms=med, ms=ms,
+    byts = frames * 100 + E * K * 32
+    print(json.dumps(dict(kernel="k_wire_events", phones=K, frames_per_phone=F, drift=drift, kernel_ms=med, ms=ms,
                           frames_per_s=frames / med * 1e3, gbs=byts / med / 1e6, hbm_frac=byts / med / 1e6 / 8000,
-                          bytes_per_frame="100 read + 32 written", text_gen_s=gen_s)))
+                          bytes_per_frame="100 read + 32 written per message", text_gen_s=gen_s)))
 
 
 def session(reps):
