@@ -486,6 +486,7 @@ __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4)))
     // order its DMA and its LDS reads.  Frame index f + 1's DMA is in flight while f is parsed; loads
     // return in order, so at most 19 outstanding vector memory operations (whatever event stores are among
     // them) means that all of f's have landed.
+    static_assert(kFastDwords == 19, "the vmcnt below counts one frame index's DMA instructions");
     if (n_frames > 0) dma(0, 0);
     for (int64_t f = 0; f < n_frames; ++f) {
         if (f + 1 < n_frames) {
