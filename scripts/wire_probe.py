@@ -4,7 +4,7 @@ client text, 1,024 generated phones' phase-3 streams tiled x256), then the devic
 (engine.run_wire_session: frames -> FP64 events -> phase 2 -> k_live) on a smaller set.  Prints one JSON
 line: kernel ms (HIP events, median of reps), frames/s, GB/s of frames read + events written.
 
-usage: python3 scripts/wire_probe.py [reps] [--session] [--tile T (phones = 1,024 T; default 256)] [--drift D] [--no-check]
+usage: python3 scripts/wire_probe.py [reps] [--session] [--tile T (phones = 1,024 T; default 256)] [--drift D] [--phones K (at most 1,024 T)] [--no-check]
 """
 from __future__ import annotations
 
@@ -38,6 +38,8 @@ def main():
             texts[k] = "".join(rows)
     fr0 = wire.frames(texts)                                   # [F][K0][100]
     fr = np.ascontiguousarray(np.tile(fr0, (1, tile, 1)))       # [E][K0 * tile][100]
+    if "--phones" in sys.argv:  # any batch (e.g. one whose row pitch, 32 B x phones, is no power of two)
+        fr = np.ascontiguousarray(fr[:, :int(sys.argv[sys.argv.index("--phones") + 1])])
     gen_s = time.time() - t0
     F, K = fr.shape[:2]
     fb = engine.DeviceBuffer(fr.nbytes).upload(fr)
