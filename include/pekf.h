@@ -357,6 +357,17 @@ int pekf_frontend_init_ext_dev(int64_t batch, int64_t n_events, const void *ev_p
 int pekf_wire_events_dev(int64_t batch, int64_t n_frames, const void *frames, int64_t e2_max, int64_t e3_max,
                          void *ev2, void *ev3, int64_t *first_t2, int32_t *n2, int32_t *n3, int32_t *bad_frame,
                          int *dev_error, void *stream);
+/* pekf_wire_events_dev with flags.  PEKF_WIRE_FRAME_ROWS: the planes get a row per frame index instead of
+ * a row per message -- row f of ev2 / ev3 holds frame f's message if it is one of that phase, else the
+ * no-message event, which phase 2 (pekf_frontend_init_ext_dev) and phase 3 (pekf_live_ext_dev) skip, so
+ * they give the same results on n_frames rows as on the compacted planes.  Every lane of a wave then
+ * stores the same row: for phones whose rows would drift apart (phase-1 / phase-2 parts of different
+ * lengths), at 32 B more written per frame.  Needs e2_max, e3_max >= n_frames; n2 / n3 still count the
+ * messages.  A phone's rows from its refused frame on are no-message events. */
+#define PEKF_WIRE_FRAME_ROWS 0x1u
+int pekf_wire_events_ext_dev(int64_t batch, int64_t n_frames, const void *frames, int64_t e2_max, int64_t e3_max,
+                             void *ev2, void *ev3, int64_t *first_t2, int32_t *n2, int32_t *n3, int32_t *bad_frame,
+                             int *dev_error, uint32_t flags, void *stream);
 
 /* ---------------- the phone -> server wire: host code ----------------
  * The Android client sends each sample as text, Float.toString of each value

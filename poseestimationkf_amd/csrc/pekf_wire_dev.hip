@@ -402,6 +402,9 @@ __device__ int wire_frame(const uint8_t *fr, WireMsg &m) {
 // dword-window reader instead of byte reads (36.6 against 29.8 ms), and every check of a token as a
 // status flag instead of an exit (35.2 against 23.7 ms: the division and the big-integer path then run for
 // every lane, and the registers spill).
+// ROWS (PEKF_WIRE_FRAME_ROWS): frame f's message goes to row f of its phase's plane and the no-message
+// event to row f of the other, so every lane of a wave stores the same row (see pekf.h).
+template <bool ROWS>
 __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_wire_events(
     int64_t batch, int64_t n_frames, const uint32_t *__restrict__ frames, int64_t e2_max, int64_t e3_max,
     double4 *__restrict__ ev2, double4 *__restrict__ ev3, int64_t *__restrict__ first_t2, int32_t *__restrict__ n2,
@@ -458,28 +461,41 @@ __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4)))
     int32_t c2 = 0, c3 = 0, bad = -1, resume = -1;
     int64_t t2 = 0;
     const double4 none = ev64_null();
-    // one parsed frame: a message to its phase's plane, a refused frame ends the phone
+    // One parsed frame: a message to its phase's next row (ROWS: to row f, and the no-message event to
+    // row f of the other plane); a refused frame ends the phone
     auto take = [&](int st, const WireMsg &m, int64_t f) {
+        double4 e2r = none, e3r = none;  // (ROWS) row f of each plane
         if (st == 2) {
             bad = (int32_t)f;
-            return;
+        } else if (st == 0 && (m.phase == '2' || m.phase == '3')) {  // phase 1 (calibration), others: skipped
+            const double td = (double)m.t;
+            if (!(fabs(td) < 2251799813685248.0)) {  // the FP64 event's time limit, 2^51 ns
+                bad = (int32_t)f;
+            } else {
+                const uint32_t ty = (m.type >= '0' && m.type <= '2') ? (uint32_t)(m.type - '0') : 3u;
+                const double4 e = make_double4(m.v[0], m.v[1], m.v[2],
+                                               __longlong_as_double(__double_as_longlong(td) | (long long)ty));
+                if (m.phase == '2') {
+                    if (c2 == 0) t2 = m.t;
+                    if constexpr (ROWS)
+                        e2r = e;
+                    else if (c2 < e2_max)
+                        ev2[(int64_t)c2 * batch + b] = e;
+                    ++c2;
+                } else {
+                    if constexpr (ROWS)
+                        e3r = e;
+                    else if (c3 < e3_max)
+                        ev3[(int64_t)c3 * batch + b] = e;
+                    ++c3;
+                }
+            }
         }
-        if (st != 0 || (m.phase != '2' && m.phase != '3')) return;  // phase 1 (calibration) and others: skipped
-        const double td = (double)m.t;
-        if (!(fabs(td) < 2251799813685248.0)) {  // the FP64 event's time limit, 2^51 ns
-            bad = (int32_t)f;
-            return;
-        }
-        const uint32_t ty = (m.type >= '0' && m.type <= '2') ? (uint32_t)(m.type - '0') : 3u;
-        const double4 e = make_double4(m.v[0], m.v[1], m.v[2],
-                                       __longlong_as_double(__double_as_longlong(td) | (long long)ty));
-        if (m.phase == '2') {
-            if (c2 == 0) t2 = m.t;
-            if (c2 < e2_max) ev2[(int64_t)c2 * batch + b] = e;
-            ++c2;
-        } else {
-            if (c3 < e3_max) ev3[(int64_t)c3 * batch + b] = e;
-            ++c3;
+        if constexpr (ROWS) {
+            if (bad < 0) {  // (a stopped phone's rows are filled at the end)
+                ev2[f * batch + b] = e2r;
+                ev3[f * batch + b] = e3r;
+            }
         }
     };
     // One wave per block: no barrier (its fence would wait for the ring, vmcnt(0)); the wave's own waits
@@ -520,8 +536,14 @@ __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4)))
         take(st, m, f);
     }
     if (b >= batch) return;
-    for (int64_t e = c2; e < e2_max; ++e) ev2[e * batch + b] = none;
-    for (int64_t e = c3; e < e3_max; ++e) ev3[e * batch + b] = none;
+    if constexpr (ROWS) {  // rows from the frame that stopped the phone, or past the last frame
+        const int64_t r0 = bad >= 0 ? bad : n_frames;
+        for (int64_t e = r0; e < e2_max; ++e) ev2[e * batch + b] = none;
+        for (int64_t e = r0; e < e3_max; ++e) ev3[e * batch + b] = none;
+    } else {
+        for (int64_t e = c2; e < e2_max; ++e) ev2[e * batch + b] = none;
+        for (int64_t e = c3; e < e3_max; ++e) ev3[e * batch + b] = none;
+    }
     n2[b] = c2;
     n3[b] = c3;
     first_t2[b] = t2;
@@ -534,10 +556,15 @@ __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4)))
 
 using namespace pekf;
 
-extern "C" int pekf_wire_events_dev(int64_t batch, int64_t n_frames, const void *frames, int64_t e2_max,
-                                    int64_t e3_max, void *ev2, void *ev3, int64_t *first_t2, int32_t *n2,
-                                    int32_t *n3, int32_t *bad_frame, int *dev_error, void *stream) {
+extern "C" int pekf_wire_events_ext_dev(int64_t batch, int64_t n_frames, const void *frames, int64_t e2_max,
+                                        int64_t e3_max, void *ev2, void *ev3, int64_t *first_t2, int32_t *n2,
+                                        int32_t *n3, int32_t *bad_frame, int *dev_error, uint32_t flags,
+                                        void *stream) {
     PEKF_CHECK_ARG(batch >= 0 && n_frames >= 0 && e2_max >= 0 && e3_max >= 0, "negative size");
+    PEKF_CHECK_ARG((flags & ~(uint32_t)PEKF_WIRE_FRAME_ROWS) == 0, "unknown flags");
+    const bool rows = flags & PEKF_WIRE_FRAME_ROWS;
+    PEKF_CHECK_ARG(!rows || (e2_max >= n_frames && e3_max >= n_frames),
+                   "PEKF_WIRE_FRAME_ROWS: the planes need a row per frame index (e_max >= n_frames)");
     if (batch == 0) return PEKF_OK;
     PEKF_CHECK_ARG(frames || n_frames == 0, "null pointer");
     PEKF_CHECK_ARG((ev2 || e2_max == 0) && (ev3 || e3_max == 0) && first_t2 && n2 && n3, "null pointer");
@@ -545,11 +572,23 @@ extern "C" int pekf_wire_events_dev(int64_t batch, int64_t n_frames, const void 
                    "misaligned buffers");
     PEKF_CHECK_ARG(n_frames < ((int64_t)1 << 31) && e2_max < ((int64_t)1 << 31) && e3_max < ((int64_t)1 << 31),
                    "n_frames and e_max must be < 2^31");
-    hipLaunchKernelGGL(k_wire_events, dim3(grid_for(batch, kWireBlock)), dim3(kWireBlock), 0, as_stream(stream),
-                       batch, n_frames, static_cast<const uint32_t *>(frames), e2_max, e3_max,
-                       static_cast<double4 *>(ev2), static_cast<double4 *>(ev3), first_t2, n2, n3, bad_frame,
-                       dev_error);
+    auto launch = [&](auto kernel) {
+        hipLaunchKernelGGL(kernel, dim3(grid_for(batch, kWireBlock)), dim3(kWireBlock), 0, as_stream(stream), batch,
+                           n_frames, static_cast<const uint32_t *>(frames), e2_max, e3_max, static_cast<double4 *>(ev2),
+                           static_cast<double4 *>(ev3), first_t2, n2, n3, bad_frame, dev_error);
+    };
+    if (rows)
+        launch(k_wire_events<true>);
+    else
+        launch(k_wire_events<false>);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_wire_events");
     return PEKF_OK;
+}
+
+extern "C" int pekf_wire_events_dev(int64_t batch, int64_t n_frames, const void *frames, int64_t e2_max,
+                                    int64_t e3_max, void *ev2, void *ev3, int64_t *first_t2, int32_t *n2,
+                                    int32_t *n3, int32_t *bad_frame, int *dev_error, void *stream) {
+    return pekf_wire_events_ext_dev(batch, n_frames, frames, e2_max, e3_max, ev2, ev3, first_t2, n2, n3, bad_frame,
+                                    dev_error, 0u, stream);
 }

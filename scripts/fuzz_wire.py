@@ -15,7 +15,7 @@ host does (the same phase-2 / phase-3 events bit for bit, counts and first phase
 phone's first frame it does not take; that frame must be one of the corrupted ones, and the frames
 before it must match the host's.
 
-usage: python3 scripts/fuzz_wire.py [--cases N] [--seed S] [--corrupt P]   (exit status 1 on any difference)
+usage: python3 scripts/fuzz_wire.py [--cases N] [--seed S] [--corrupt P] [--rows]   (exit status 1 on any difference)
 """
 from __future__ import annotations
 
@@ -102,6 +102,7 @@ def main(argv=None):
     ap.add_argument("--cases", type=int, default=20)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--corrupt", type=float, default=0.05, help="per-frame probability of a replaced number")
+    ap.add_argument("--rows", action="store_true", help="PEKF_WIRE_FRAME_ROWS planes (compacted here to compare)")
     a = ap.parse_args(argv)
     rng = np.random.default_rng(a.seed)
     n_frames = n_bad_phones = differ = 0
@@ -120,8 +121,8 @@ def main(argv=None):
         t2b, n2b, n3b, badb = (engine.DeviceBuffer(8 * K), engine.DeviceBuffer(4 * K), engine.DeviceBuffer(4 * K),
                                engine.DeviceBuffer(4 * K))
         errb = engine.DeviceBuffer(4).upload(np.zeros(1, np.int32))
-        check(lib.pekf_wire_events_dev(K, F, fb.ptr, F, F, ev2.ptr, ev3.ptr, t2b.ptr, n2b.ptr, n3b.ptr, badb.ptr,
-                                       errb.ptr, None))
+        check(lib.pekf_wire_events_ext_dev(K, F, fb.ptr, F, F, ev2.ptr, ev3.ptr, t2b.ptr, n2b.ptr, n3b.ptr,
+                                           badb.ptr, errb.ptr, 1 if a.rows else 0, None))
         check(lib.pekf_device_sync())
         d2, d3 = ev2.download((F, K, 4), np.float64), ev3.download((F, K, 4), np.float64)
         n2, n3 = n2b.download((K,), np.int32), n3b.download((K,), np.int32)
@@ -141,7 +142,16 @@ def main(argv=None):
                     print("case %d phone %d: the device took a frame the host parse rejects" % (case, k))
                     differ += 1
                     break
-                got = dev[:h.shape[0], k]
+                if a.rows:  # a row per frame index: the rows that are not the no-message event, in order
+                    col = dev[:, k]
+                    got = col[col[:, 3:4].view(np.uint64)[:, 0] != np.uint64(synth.EV64_NONE_W)]
+                    if got.shape[0] != h.shape[0]:
+                        print("case %d phone %d phase %d: %d rows, the host %d" % (case, k, phase, got.shape[0],
+                                                                                 h.shape[0]))
+                        differ += 1
+                        continue
+                else:
+                    got = dev[:h.shape[0], k]
                 ok = n[k] == h.shape[0] and np.array_equal(got.view(np.uint64), h.view(np.uint64))
                 if phase == 2 and h.shape[0]:
                     first = (h[0:1, 3].view(np.uint64) & ~np.uint64(3)).view(np.float64)[0]

@@ -4,7 +4,7 @@ client text, 1,024 generated phones' phase-3 streams tiled x256), then the devic
 (engine.run_wire_session: frames -> FP64 events -> phase 2 -> k_live) on a smaller set.  Prints one JSON
 line: kernel ms (HIP events, median of reps), frames/s, GB/s of frames read + events written.
 
-usage: python3 scripts/wire_probe.py [reps] [--session] [--tile T (phones = 1,024 T; default 256)] [--drift D] [--phones K (at most 1,024 T)] [--no-check]
+usage: python3 scripts/wire_probe.py [reps] [--session] [--tile T (phones = 1,024 T; default 256)] [--drift D] [--phones K (at most 1,024 T)] [--rows] [--no-check]
 """
 from __future__ import annotations
 
@@ -44,7 +44,9 @@ def main():
     F, K = fr.shape[:2]
     fb = engine.DeviceBuffer(fr.nbytes).upload(fr)
     del fr
-    ev2, ev3 = engine.DeviceBuffer(32), engine.DeviceBuffer(32 * E * K)  # E phase-3 messages per phone
+    rows = "--rows" in sys.argv  # PEKF_WIRE_FRAME_ROWS: a row per frame index in both planes
+    ev2 = engine.DeviceBuffer(32 * F * K if rows else 32)
+    ev3 = engine.DeviceBuffer(32 * (F if rows else E) * K)  # E phase-3 messages per phone
     t2b, n2b, n3b, badb = (engine.DeviceBuffer(8 * K), engine.DeviceBuffer(4 * K), engine.DeviceBuffer(4 * K),
                            engine.DeviceBuffer(4 * K))
     errb = engine.DeviceBuffer(4).upload(np.zeros(1, np.int32))
@@ -53,8 +55,9 @@ def main():
     ms = []
     for _ in range(reps):
         e0.record(st.handle)
-        check(lib.pekf_wire_events_dev(K, F, fb.ptr, 0, E, ev2.ptr, ev3.ptr, t2b.ptr, n2b.ptr, n3b.ptr, badb.ptr,
-                                       errb.ptr, st.handle))
+        check(lib.pekf_wire_events_ext_dev(K, F, fb.ptr, F if rows else 0, F if rows else E, ev2.ptr, ev3.ptr,
+                                           t2b.ptr, n2b.ptr, n3b.ptr, badb.ptr, errb.ptr, 1 if rows else 0,
+                                           st.handle))
         e1.record(st.handle)
         e1.sync()
         ms.append(e0.elapsed_ms(e1))
@@ -63,14 +66,18 @@ def main():
     n3 = n3b.download((K,), np.int32) if check_out else np.full(K, E)
     assert np.all(n3 == E)
     # spot check against the host parse: phone 0 and a tiled copy of it
-    got = ev3.download((E, K, 4), np.float64)[:, [0, K0 * 7]]
+    got = ev3.download((F if rows else E, K, 4), np.float64)[:, [0, K0 * 7]]
+    if rows:  # the rows that are not the no-message event (one phone's and its copy's: the same frames)
+        keep = got[:, 0, 3:4].view(np.uint64)[:, 0] != np.uint64(synth.EV64_NONE_W)
+        got = got[keep]
     want = synth.pack_events64(wire.events_from_wire(texts[:1], np.zeros((1, 3)), np.zeros((1, 3)), [0]))
     assert not check_out or np.array_equal(got[:, 0].view(np.uint64), want[:, 0].view(np.uint64))
     assert not check_out or np.array_equal(got[:, 1].view(np.uint64), want[:, 0].view(np.uint64))
     med = float(np.median(ms[1:] if len(ms) > 1 else ms))
     frames = F * K
-    byts = frames * 100 + E * K * 32
-    print(json.dumps(dict(kernel="k_wire_events", phones=K, frames_per_phone=F, drift=drift, kernel_ms=med, ms=ms,
+    byts = frames * 100 + (2 * F if rows else E) * K * 32
+    print(json.dumps(dict(kernel="k_wire_events", phones=K, frames_per_phone=F, drift=drift, frame_rows=rows,
+                          kernel_ms=med, ms=ms,
                           frames_per_s=frames / med * 1e3, gbs=byts / med / 1e6, hbm_frac=byts / med / 1e6 / 8000,
                           bytes_per_frame="100 read + 32 written per message", text_gen_s=gen_s)))
 
@@ -83,9 +90,14 @@ def session(reps):
     ph2 = synth.generate_events(np.arange(K0), E2, seed=71)
     ph3 = synth.generate_events(np.arange(K0), E3, seed=72)
     ph3 = dict(ph3, times=ph3["times"] - ph3["t_init"][None, :] + ph2["times"][-1][None, :])
-    texts = [wire.events_text(ph2["types"][:, k], ph2["values"][:, k], ph2["times"][:, k], phase=2) +
+    # --drift D: phase-2 parts of E2 - (0..D) messages, so that the phones' phase-3 rows drift apart
+    drift = int(sys.argv[sys.argv.index("--drift") + 1]) if "--drift" in sys.argv else 0
+    n2k = E2 - np.random.default_rng(8).integers(0, drift + 1, K0)
+    texts = [wire.events_text(ph2["types"][:n2k[k], k], ph2["values"][:n2k[k], k], ph2["times"][:n2k[k], k],
+                              phase=2) +
              wire.events_text(ph3["types"][:, k], ph3["values"][:, k], ph3["times"][:, k], phase=3)
              for k in range(K0)]
+    rows_mode = "--rows" in sys.argv
     fr = np.ascontiguousarray(np.tile(wire.frames(texts), (1, tile, 1)))
     F, K = fr.shape[:2]
     fb = engine.DeviceBuffer(fr.nbytes).upload(fr)
@@ -103,21 +115,22 @@ def session(reps):
     for _ in range(reps):
         f.reset()
         ev[0].record(st.handle)
-        check(lib.pekf_wire_events_dev(K, F, fb.ptr, F, F, ev2.ptr, ev3.ptr, t2b.ptr, n2b.ptr, n3b.ptr, None,
-                                       errb.ptr, st.handle))
+        check(lib.pekf_wire_events_ext_dev(K, F, fb.ptr, F, F, ev2.ptr, ev3.ptr, t2b.ptr, n2b.ptr, n3b.ptr, None,
+                                           errb.ptr, 1 if rows_mode else 0, st.handle))
         ev[1].record(st.handle)
-        check(lib.pekf_frontend_init_ext_dev(K, E2, ev2.ptr, t2b.ptr, 100, ib.ptr, tib.ptr, None, rb.ptr,
-                                             EV_F64_EVENTS, st.handle))
+        check(lib.pekf_frontend_init_ext_dev(K, F if rows_mode else E2, ev2.ptr, t2b.ptr, 100, ib.ptr, tib.ptr, None,
+                                             rb.ptr, EV_F64_EVENTS, st.handle))
         ev[2].record(st.handle)
-        f.run_events_async(ev3, E3, ib, tib, cnt, refs, 0.1, st.handle, flags=EV_F64_EVENTS)
+        f.run_events_async(ev3, F if rows_mode else E3, ib, tib, cnt, refs, 0.1, st.handle, flags=EV_F64_EVENTS)
         ev[3].record(st.handle)
         ev[3].sync()
         rows.append([ev[i].elapsed_ms(ev[i + 1]) for i in range(3)])
     assert int(errb.download((1,), np.int32)[0]) == 0
-    assert np.all(n2b.download((K,), np.int32) == E2) and np.all(n3b.download((K,), np.int32) == E3)
+    assert np.array_equal(n2b.download((K,), np.int32), np.tile(n2k, tile)) and np.all(n3b.download((K,), np.int32) == E3)
     assert rb.download((K,), np.int32).all()
     med = np.median(np.array(rows[1:] if len(rows) > 1 else rows), axis=0)
-    print(json.dumps(dict(kernel="wire session", phones=K, frames_per_phone=F, wire_ms=float(med[0]),
+    print(json.dumps(dict(kernel="wire session", phones=K, frames_per_phone=F, drift=drift, frame_rows=rows_mode,
+                          wire_ms=float(med[0]),
                           phase2_ms=float(med[1]), live_ms=float(med[2]), total_ms=float(med.sum()),
                           messages_per_s=K * F / float(med.sum()) * 1e3,
                           records=int(cnt.download((K,), np.int32).sum()))))

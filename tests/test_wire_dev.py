@@ -227,6 +227,76 @@ def test_wire_events_ring_edges(eng, K, F):
         assert t2[k] == (p["times"][p["phase"] == 2][0] if (p["phase"] == 2).any() else 0)
 
 
+def _compact(planes, K):
+    """[F][K] frame-row planes -> each phone's rows that are not the no-message event, in order."""
+    w = np.ascontiguousarray(planes[..., 3]).view(np.uint64)
+    return [planes[w[:, k] != np.uint64(synth.EV64_NONE_W), k] for k in range(K)]
+
+
+@pytest.mark.gpu
+def test_wire_events_frame_rows(eng):
+    """PEKF_WIRE_FRAME_ROWS: row f of each plane is frame f's message of that phase or the no-message
+    event; without those rows each phone's planes are the compacted planes bit for bit, with the same
+    counts and first phase-2 times, on streams whose rows drift apart (phase-2 parts of different
+    lengths, blank and phase-1 frames) and with a refused frame (its phone's rows from there on are
+    no-message events)."""
+    rng = np.random.default_rng(31)
+    K = 150
+    texts = []
+    for k in range(K):
+        rows = []
+        for ph, n in ((2, int(rng.integers(0, 40))), (3, int(rng.integers(0, 60)))):
+            for i in range(n):
+                if rng.random() < 0.1:
+                    rows.append(" " * 99 + "\n" if rng.random() < 0.5 else wire.message(1, 2, [1, 2, 3], 42))
+                rows.append(_frame([_fast_form(rng) for _ in range(3)], int(rng.integers(0, 10 ** 12)), phase=ph,
+                                   ty=str(rng.choice(["0", "1", "2", "7"]))))
+        texts.append("".join(rows))
+    fr = wire.frames(texts)
+    F = fr.shape[0]
+    a = eng.wire_events(fr)
+    r = eng.wire_events(fr, frame_rows=True)
+    assert r["E2"] == r["E3"] == F
+    assert np.array_equal(a["n2"], r["n2"]) and np.array_equal(a["n3"], r["n3"])
+    assert _same(a["first_t2"].download((K,), np.int64), r["first_t2"].download((K,), np.int64))
+    for plane, n in (("ev2", "n2"), ("ev3", "n3")):
+        comp = a[plane].download((F, K, 4), np.float64)
+        rows = r[plane].download((F, K, 4), np.float64)
+        for k, got in enumerate(_compact(rows, K)):
+            assert got.shape[0] == a[n][k] and _same(got, comp[:a[n][k], k])
+    # a refused frame: its phone's rows from there on are no-message events
+    bad_texts = [texts[0], _frame(["1.0", "2.0", "3.0"], 5, phase=3) + _frame(["1.5abc", "2.0", "3.0"], 6) +
+                 _frame(["1.0", "2.0", "3.0"], 7, phase=3)]
+    fb = wire.frames(bad_texts)
+    with pytest.raises(ValueError, match="phone 1, frame 1"):
+        eng.wire_events(fb, frame_rows=True)
+
+
+@pytest.mark.gpu
+def test_wire_session_frame_rows(eng):
+    """run_wire_session with frame-row planes (phase 2 and phase 3 skipping the no-message rows) equals
+    the compacted session bit for bit -- ready, counts, refs, X, P -- on phones whose phase-2 parts differ
+    in length, so that their phase-3 rows drift apart."""
+    K = 96
+    ph2 = synth.generate_events(np.arange(K), 700, seed=63)
+    ph3 = synth.generate_events(np.arange(K), 500, seed=64)
+    ph3 = dict(ph3, times=ph3["times"] - ph3["t_init"][None, :] + ph2["times"][-1][None, :])
+    texts = []
+    for k in range(K):
+        n2, n3 = 640 + 4 * (k % 13), 500 - 9 * (k % 5)
+        texts.append(wire.events_text(ph2["types"][:n2, k], ph2["values"][:n2, k], ph2["times"][:n2, k], phase=2) +
+                     wire.events_text(ph3["types"][:n3, k], ph3["values"][:n3, k], ph3["times"][:n3, k], phase=3))
+    fr = wire.frames(texts)
+    fa, fb = eng.BatchedEKF(K), eng.BatchedEKF(K)
+    oa = eng.run_wire_session(fr, fa)
+    ob = eng.run_wire_session(fr, fb, frame_rows=True)
+    assert oa["ready"].sum() > K // 2 and oa["counts"][oa["ready"]].min() > 0
+    for key in ("ready", "counts", "refs"):
+        assert np.array_equal(oa[key], ob[key], equal_nan=key == "refs"), key
+    for x, y in zip(fa.get_state(), fb.get_state()):
+        assert np.array_equal(x, y)
+
+
 @pytest.mark.gpu
 def test_wire_events_frame_is_the_message(eng):
     """The server takes each 100-byte recv as one message (KFS/Server.cpp:84-98), and so does the device: a
