@@ -363,7 +363,10 @@ int pekf_wire_events_dev(int64_t batch, int64_t n_frames, const void *frames, in
  * they give the same results on n_frames rows as on the compacted planes.  Every lane of a wave then
  * stores the same row: for phones whose rows would drift apart (phase-1 / phase-2 parts of different
  * lengths), at 32 B more written per frame.  Needs e2_max, e3_max >= n_frames; n2 / n3 still count the
- * messages.  A phone's rows from its refused frame on are no-message events. */
+ * messages.  A phone's rows from its refused frame on are no-message events.  Where the grid leaves the
+ * GPU's SIMDs short of 4 waves, the frames are split into chunks parsed by separate waves (a stream-ordered
+ * allocation of 24 B per phone and chunk holds their counts until a second kernel combines them;
+ * PEKF_WIRE_CHUNKS=n in the environment forces n chunks). */
 #define PEKF_WIRE_FRAME_ROWS 0x1u
 int pekf_wire_events_ext_dev(int64_t batch, int64_t n_frames, const void *frames, int64_t e2_max, int64_t e3_max,
                              void *ev2, void *ev3, int64_t *first_t2, int32_t *n2, int32_t *n3, int32_t *bad_frame,

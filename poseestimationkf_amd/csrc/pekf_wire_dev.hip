@@ -408,7 +408,12 @@ template <bool ROWS>
 __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_wire_events(
     int64_t batch, int64_t n_frames, const uint32_t *__restrict__ frames, int64_t e2_max, int64_t e3_max,
     double4 *__restrict__ ev2, double4 *__restrict__ ev3, int64_t *__restrict__ first_t2, int32_t *__restrict__ n2,
-    int32_t *__restrict__ n3, int32_t *__restrict__ bad_frame, int *__restrict__ err) {
+    int32_t *__restrict__ n3, int32_t *__restrict__ bad_frame, int *__restrict__ err, int64_t f_per_chunk,
+    int4 *__restrict__ part, int64_t *__restrict__ part_t2) {
+    // (ROWS, f_per_chunk > 0: block row blockIdx.y parses frames [fb, fe) and leaves its counts, first
+    // phase-2 time and refused frame in part / part_t2 [chunk][batch] for k_wire_rows_finalize)
+    const int64_t fb = f_per_chunk > 0 ? (int64_t)blockIdx.y * f_per_chunk : 0;
+    const int64_t fe = f_per_chunk > 0 && fb + f_per_chunk < n_frames ? fb + f_per_chunk : n_frames;
     // One LDS array (a second __shared__ object can make the compiler drain the DMA ring, vmcnt(0)):
     // the fast loop's ring of two slots of 64 frames' first 76 bytes, written by buffer loads to LDS; the
     // second loop's 64 whole frames; the powers of ten at the end.
@@ -503,9 +508,9 @@ __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4)))
     // return in order, so at most 19 outstanding vector memory operations (whatever event stores are among
     // them) means that all of f's have landed.
     static_assert(kFastDwords == 19, "the vmcnt below counts one frame index's DMA instructions");
-    if (n_frames > 0) dma(0, 0);
-    for (int64_t f = 0; f < n_frames; ++f) {
-        if (f + 1 < n_frames) {
+    if (fb < fe) dma(fb, (int)(fb & 1));
+    for (int64_t f = fb; f < fe; ++f) {
+        if (f + 1 < fe) {
             dma(f + 1, (int)((f + 1) & 1));
             asm volatile("s_waitcnt vmcnt(19)" ::: "memory");
         } else {
@@ -525,7 +530,7 @@ __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4)))
     int f0 = resume >= 0 ? resume : INT_MAX;
     for (int d = 1; d < kWireBlock; d <<= 1) f0 = min(f0, __shfl_xor(f0, d));
     uint32_t cur[kWireDwords / kWireBlock];
-    for (int64_t f = f0; f < n_frames; ++f) {
+    for (int64_t f = f0; f < fe; ++f) {
         __syncthreads();
         load(f, cur);
         stage(cur);
@@ -536,6 +541,11 @@ __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4)))
         take(st, m, f);
     }
     if (b >= batch) return;
+    if (part) {
+        part[(int64_t)blockIdx.y * batch + b] = make_int4(c2, c3, bad, 0);
+        part_t2[(int64_t)blockIdx.y * batch + b] = t2;
+        return;
+    }
     if constexpr (ROWS) {  // rows from the frame that stopped the phone, or past the last frame
         const int64_t r0 = bad >= 0 ? bad : n_frames;
         for (int64_t e = r0; e < e2_max; ++e) ev2[e * batch + b] = none;
@@ -550,6 +560,40 @@ __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4)))
     if (bad_frame) bad_frame[b] = bad;
     const int flags = (bad >= 0 ? 1 : 0) | (c2 > e2_max || c3 > e3_max ? 2 : 0);
     if (flags && err) atomicOr(err, flags);
+}
+
+// A phone's chunks in frame order: its counts up to its first refused frame, its first phase-2 time,
+// and no-message rows from the refused frame (or the last frame) on.
+__global__ __launch_bounds__(256) void k_wire_rows_finalize(int64_t batch, int64_t n_frames, int64_t n_chunks,
+                                                            const int4 *__restrict__ part,
+                                                            const int64_t *__restrict__ part_t2, int64_t e2_max,
+                                                            int64_t e3_max, double4 *__restrict__ ev2,
+                                                            double4 *__restrict__ ev3, int64_t *__restrict__ first_t2,
+                                                            int32_t *__restrict__ n2, int32_t *__restrict__ n3,
+                                                            int32_t *__restrict__ bad_frame, int *__restrict__ err) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= batch) return;
+    int32_t c2 = 0, c3 = 0, bad = -1;
+    int64_t t2 = 0;
+    for (int64_t ch = 0; ch < n_chunks; ++ch) {
+        const int4 p = part[ch * batch + b];
+        if (c2 == 0 && p.x > 0) t2 = part_t2[ch * batch + b];
+        c2 += p.x;
+        c3 += p.y;
+        if (p.z >= 0) {  // the phone stopped here: later chunks' frames are not its messages
+            bad = p.z;
+            break;
+        }
+    }
+    const double4 none = ev64_null();
+    const int64_t r0 = bad >= 0 ? bad : n_frames;
+    for (int64_t e = r0; e < e2_max; ++e) ev2[e * batch + b] = none;
+    for (int64_t e = r0; e < e3_max; ++e) ev3[e * batch + b] = none;
+    n2[b] = c2;
+    n3[b] = c3;
+    first_t2[b] = t2;
+    if (bad_frame) bad_frame[b] = bad;
+    if (bad >= 0 && err) atomicOr(err, 1);
 }
 
 }  // namespace pekf
@@ -572,10 +616,41 @@ extern "C" int pekf_wire_events_ext_dev(int64_t batch, int64_t n_frames, const v
                    "misaligned buffers");
     PEKF_CHECK_ARG(n_frames < ((int64_t)1 << 31) && e2_max < ((int64_t)1 << 31) && e3_max < ((int64_t)1 << 31),
                    "n_frames and e_max must be < 2^31");
+    // Frame rows need no count before a frame's store: where the grid leaves SIMDs short of 4 waves, the
+    // frames are split into chunks parsed by separate waves (PEKF_WIRE_CHUNKS=n forces n) and their
+    // counts combined after.
+    const int64_t waves = grid_for(batch, kWireBlock);
+    int64_t chunks = 1;
+    if (rows) {
+        const char *ec = getenv("PEKF_WIRE_CHUNKS");
+        if (ec && atoi(ec) > 0) {
+            chunks = atoi(ec);
+        } else {
+            int dev = 0, cus = 0;
+            if (hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+                chunks = ((int64_t)cus * 16 + waves - 1) / waves;
+            const int64_t most = n_frames / 128;  // chunks of at least 128 frame indices
+            chunks = chunks < most ? chunks : most;
+            chunks = chunks < 16 ? chunks : 16;
+        }
+        chunks = chunks < n_frames ? chunks : n_frames;
+        if (chunks < 1) chunks = 1;
+    }
+    const int64_t per = chunks > 1 ? (n_frames + chunks - 1) / chunks : 0;
+    if (per) chunks = (n_frames + per - 1) / per;
+    int4 *part = nullptr;
+    int64_t *part_t2 = nullptr;
+    hipStream_t st = as_stream(stream);
+    if (per) {
+        hipError_t a = hipMallocAsync(reinterpret_cast<void **>(&part), (size_t)(chunks * batch) * 24, st);
+        if (a != hipSuccess) return hip_fail(a, "k_wire_events chunk counts");
+        part_t2 = reinterpret_cast<int64_t *>(part + chunks * batch);
+    }
     auto launch = [&](auto kernel) {
-        hipLaunchKernelGGL(kernel, dim3(grid_for(batch, kWireBlock)), dim3(kWireBlock), 0, as_stream(stream), batch,
-                           n_frames, static_cast<const uint32_t *>(frames), e2_max, e3_max, static_cast<double4 *>(ev2),
-                           static_cast<double4 *>(ev3), first_t2, n2, n3, bad_frame, dev_error);
+        hipLaunchKernelGGL(kernel, dim3(waves, per ? chunks : 1), dim3(kWireBlock), 0, st, batch, n_frames,
+                           static_cast<const uint32_t *>(frames), e2_max, e3_max, static_cast<double4 *>(ev2),
+                           static_cast<double4 *>(ev3), first_t2, n2, n3, bad_frame, dev_error, per, part, part_t2);
     };
     if (rows)
         launch(k_wire_events<true>);
@@ -583,6 +658,15 @@ extern "C" int pekf_wire_events_ext_dev(int64_t batch, int64_t n_frames, const v
         launch(k_wire_events<false>);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_wire_events");
+    if (per) {
+        hipLaunchKernelGGL(k_wire_rows_finalize, dim3(grid_for(batch, 256)), dim3(256), 0, st, batch, n_frames, chunks,
+                           part, part_t2, e2_max, e3_max, static_cast<double4 *>(ev2), static_cast<double4 *>(ev3),
+                           first_t2, n2, n3, bad_frame, dev_error);
+        e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(e, "k_wire_rows_finalize");
+        e = hipFreeAsync(part, st);
+        if (e != hipSuccess) return hip_fail(e, "k_wire_events chunk counts");
+    }
     return PEKF_OK;
 }
 

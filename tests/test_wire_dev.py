@@ -234,12 +234,16 @@ def _compact(planes, K):
 
 
 @pytest.mark.gpu
-def test_wire_events_frame_rows(eng):
+@pytest.mark.parametrize("chunks", [None, "3", "7"])
+def test_wire_events_frame_rows(eng, chunks, monkeypatch):
     """PEKF_WIRE_FRAME_ROWS: row f of each plane is frame f's message of that phase or the no-message
     event; without those rows each phone's planes are the compacted planes bit for bit, with the same
     counts and first phase-2 times, on streams whose rows drift apart (phase-2 parts of different
     lengths, blank and phase-1 frames) and with a refused frame (its phone's rows from there on are
-    no-message events)."""
+    no-message events) -- also with the frames split into chunks parsed by separate waves
+    (PEKF_WIRE_CHUNKS; automatic where the grid is small)."""
+    if chunks:
+        monkeypatch.setenv("PEKF_WIRE_CHUNKS", chunks)
     rng = np.random.default_rng(31)
     K = 150
     texts = []
@@ -266,17 +270,35 @@ def test_wire_events_frame_rows(eng):
             assert got.shape[0] == a[n][k] and _same(got, comp[:a[n][k], k])
     # a refused frame: its phone's rows from there on are no-message events
     bad_texts = [texts[0], _frame(["1.0", "2.0", "3.0"], 5, phase=3) + _frame(["1.5abc", "2.0", "3.0"], 6) +
-                 _frame(["1.0", "2.0", "3.0"], 7, phase=3)]
+                 _frame(["1.0", "2.0", "3.0"], 7, phase=3) * 5]
     fb = wire.frames(bad_texts)
     with pytest.raises(ValueError, match="phone 1, frame 1"):
         eng.wire_events(fb, frame_rows=True)
+    # the refused phone's counts and rows, read past the error
+    from poseestimationkf_amd._lib import check, lib
+    Fb, Kb = fb.shape[:2]
+    bufs = [eng.DeviceBuffer(n) for n in (fb.nbytes, 32 * Fb * Kb, 32 * Fb * Kb, 8 * Kb, 4 * Kb, 4 * Kb, 4 * Kb, 4)]
+    bufs[0].upload(fb)
+    bufs[7].upload(np.zeros(1, np.int32))
+    check(lib.pekf_wire_events_ext_dev(Kb, Fb, bufs[0].ptr, Fb, Fb, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr,
+                                       bufs[4].ptr, bufs[5].ptr, bufs[6].ptr, bufs[7].ptr, 1, None))
+    check(lib.pekf_device_sync())
+    assert bufs[6].download((Kb,), np.int32).tolist() == [-1, 1]
+    assert bufs[5].download((Kb,), np.int32)[1] == 1                  # the message before the refused frame
+    e3 = bufs[2].download((Fb, Kb, 4), np.float64)[:, 1]
+    w = np.ascontiguousarray(e3[:, 3]).view(np.uint64)
+    assert w[0] != np.uint64(synth.EV64_NONE_W) and np.all(w[1:] == np.uint64(synth.EV64_NONE_W))
 
 
 @pytest.mark.gpu
-def test_wire_session_frame_rows(eng):
+@pytest.mark.parametrize("chunks", [None, "5"])
+def test_wire_session_frame_rows(eng, chunks, monkeypatch):
     """run_wire_session with frame-row planes (phase 2 and phase 3 skipping the no-message rows) equals
     the compacted session bit for bit -- ready, counts, refs, X, P -- on phones whose phase-2 parts differ
-    in length, so that their phase-3 rows drift apart."""
+    in length, so that their phase-3 rows drift apart; also with the frames in chunks parsed by separate
+    waves."""
+    if chunks:
+        monkeypatch.setenv("PEKF_WIRE_CHUNKS", chunks)
     K = 96
     ph2 = synth.generate_events(np.arange(K), 700, seed=63)
     ph3 = synth.generate_events(np.arange(K), 500, seed=64)
@@ -288,7 +310,7 @@ def test_wire_session_frame_rows(eng):
                      wire.events_text(ph3["types"][:n3, k], ph3["values"][:n3, k], ph3["times"][:n3, k], phase=3))
     fr = wire.frames(texts)
     fa, fb = eng.BatchedEKF(K), eng.BatchedEKF(K)
-    oa = eng.run_wire_session(fr, fa)
+    oa = eng.run_wire_session(fr, fa, frame_rows=False)
     ob = eng.run_wire_session(fr, fb, frame_rows=True)
     assert oa["ready"].sum() > K // 2 and oa["counts"][oa["ready"]].min() > 0
     for key in ("ready", "counts", "refs"):
