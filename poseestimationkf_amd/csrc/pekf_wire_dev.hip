@@ -12,7 +12,10 @@
 // into LDS by buffer loads to LDS, the next index's in flight while this one is parsed), and
 // appends each phase-2 / phase-3 message to that phase's plane as the FP64 event {x, y, z, bits(t) |
 // type} (type 3 for a Type no sensor takes); the rows after a phone's last message get the no-message
-// event.
+// event.  With PEKF_WIRE_FRAME_ROWS a message goes to row f, its frame's index, instead (the no-message
+// event to row f of the other plane): every lane of a wave stores one row however far the phones' message
+// counts drift apart, and since no row depends on the frames before it, a small batch's frames are split
+// into chunks over several waves, their counts combined by k_wire_rows_finalize.
 //
 // Frames in the client's own form are parsed without a character loop (wire_frame_fast: digit masks of
 // 16-byte windows, 8 digits per SWAR conversion); any other frame by wire_frame, the general parser.
