@@ -366,11 +366,14 @@ int pekf_wire_events_dev(int64_t batch, int64_t n_frames, const void *frames, in
  * messages.  A phone's rows from its refused frame on are no-message events.  Where the grid leaves the
  * GPU's SIMDs short of 4 waves, the frames are split into chunks parsed by separate waves (a stream-ordered
  * allocation of 24 B per phone and chunk holds their counts until a second kernel combines them;
- * PEKF_WIRE_CHUNKS=n in the environment forces n chunks). */
+ * PEKF_WIRE_CHUNKS=n in the environment forces n chunks).  row_bounds (device, 2 int32, may be NULL; with
+ * PEKF_WIRE_FRAME_ROWS only): [0] = 1 + the last row holding a phase-2 message of any phone, [1] = n_frames
+ * - the first row holding a phase-3 message of any phone (0: none) -- the rows outside them are no-message
+ * rows in every column, which a consumer may leave out (ev2's first [0] rows, ev3 from row n_frames - [1]). */
 #define PEKF_WIRE_FRAME_ROWS 0x1u
 int pekf_wire_events_ext_dev(int64_t batch, int64_t n_frames, const void *frames, int64_t e2_max, int64_t e3_max,
                              void *ev2, void *ev3, int64_t *first_t2, int32_t *n2, int32_t *n3, int32_t *bad_frame,
-                             int *dev_error, uint32_t flags, void *stream);
+                             int *dev_error, int32_t *row_bounds, uint32_t flags, void *stream);
 
 /* ---------------- the phone -> server wire: host code ----------------
  * The Android client sends each sample as text, Float.toString of each value

@@ -120,7 +120,7 @@ SIGNATURES = {
     "pekf_f32_wire_values": [_i64, _vp, _vp],
     "pekf_wire_parse": [ctypes.c_char_p, _i64, _i64, _vp, _vp, _vp, _vp, ctypes.POINTER(_i64)],
     "pekf_wire_events_dev": [_i64, _i64, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
-    "pekf_wire_events_ext_dev": [_i64, _i64, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp],
+    "pekf_wire_events_ext_dev": [_i64, _i64, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp],
     "pekf_live_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _vp, _vp, _dbl, _dbl, _vp, _vp, _vp, _vp],
     "pekf_live_ext_dev": [_i64, _i64, _vp, _vp, _vp, _dbl, _vp, _vp, _dbl, _dbl, _vp, _vp, _u32, _vp, _vp],
     "pekf_log_scan": [ctypes.c_char_p, ctypes.POINTER(_i64)],

@@ -412,7 +412,7 @@ __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4)))
     int64_t batch, int64_t n_frames, const uint32_t *__restrict__ frames, int64_t e2_max, int64_t e3_max,
     double4 *__restrict__ ev2, double4 *__restrict__ ev3, int64_t *__restrict__ first_t2, int32_t *__restrict__ n2,
     int32_t *__restrict__ n3, int32_t *__restrict__ bad_frame, int *__restrict__ err, int64_t f_per_chunk,
-    int4 *__restrict__ part, int64_t *__restrict__ part_t2) {
+    int4 *__restrict__ part, int64_t *__restrict__ part_t2, int32_t *__restrict__ bounds) {
     // (ROWS, f_per_chunk > 0: block row blockIdx.y parses frames [fb, fe) and leaves its counts, first
     // phase-2 time and refused frame in part / part_t2 [chunk][batch] for k_wire_rows_finalize)
     const int64_t fb = f_per_chunk > 0 ? (int64_t)blockIdx.y * f_per_chunk : 0;
@@ -467,6 +467,7 @@ __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4)))
     };
     const uint8_t *fr = reinterpret_cast<const uint8_t *>(lds) + lane * kWireFrame;
     int32_t c2 = 0, c3 = 0, bad = -1, resume = -1;
+    int32_t end2 = 0, from3 = 0;  // (ROWS, bounds) 1 + the last phase-2 row, n_frames - the first phase-3 row
     int64_t t2 = 0;
     const double4 none = ev64_null();
     // One parsed frame: a message to its phase's next row (ROWS: to row f, and the no-message event to
@@ -485,14 +486,18 @@ __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4)))
                                                __longlong_as_double(__double_as_longlong(td) | (long long)ty));
                 if (m.phase == '2') {
                     if (c2 == 0) t2 = m.t;
-                    if constexpr (ROWS)
+                    if constexpr (ROWS) {
                         e2r = e;
+                        end2 = (int32_t)f + 1;
+                    }
                     else if (c2 < e2_max)
                         ev2[(int64_t)c2 * batch + b] = e;
                     ++c2;
                 } else {
-                    if constexpr (ROWS)
+                    if constexpr (ROWS) {
                         e3r = e;
+                        if (from3 == 0) from3 = (int32_t)(n_frames - f);
+                    }
                     else if (c3 < e3_max)
                         ev3[(int64_t)c3 * batch + b] = e;
                     ++c3;
@@ -542,6 +547,16 @@ __global__ __launch_bounds__(kWireBlock) __attribute__((amdgpu_waves_per_eu(4)))
         WireMsg m;
         const int st = wire_frame(fr, m);
         take(st, m, f);
+    }
+    if (ROWS && bounds) {  // the rows the planes' consumers need: max over the wave, one atomic per wave
+        for (int d = 1; d < kWireBlock; d <<= 1) {
+            end2 = max(end2, __shfl_xor(end2, d));
+            from3 = max(from3, __shfl_xor(from3, d));
+        }
+        if (lane == 0) {
+            atomicMax(bounds, end2);
+            atomicMax(bounds + 1, from3);
+        }
     }
     if (b >= batch) return;
     if (part) {
@@ -605,8 +620,8 @@ using namespace pekf;
 
 extern "C" int pekf_wire_events_ext_dev(int64_t batch, int64_t n_frames, const void *frames, int64_t e2_max,
                                         int64_t e3_max, void *ev2, void *ev3, int64_t *first_t2, int32_t *n2,
-                                        int32_t *n3, int32_t *bad_frame, int *dev_error, uint32_t flags,
-                                        void *stream) {
+                                        int32_t *n3, int32_t *bad_frame, int *dev_error, int32_t *row_bounds,
+                                        uint32_t flags, void *stream) {
     PEKF_CHECK_ARG(batch >= 0 && n_frames >= 0 && e2_max >= 0 && e3_max >= 0, "negative size");
     PEKF_CHECK_ARG((flags & ~(uint32_t)PEKF_WIRE_FRAME_ROWS) == 0, "unknown flags");
     const bool rows = flags & PEKF_WIRE_FRAME_ROWS;
@@ -645,6 +660,10 @@ extern "C" int pekf_wire_events_ext_dev(int64_t batch, int64_t n_frames, const v
     int4 *part = nullptr;
     int64_t *part_t2 = nullptr;
     hipStream_t st = as_stream(stream);
+    if (rows && row_bounds) {
+        hipError_t z = hipMemsetAsync(row_bounds, 0, 2 * sizeof(int32_t), st);
+        if (z != hipSuccess) return hip_fail(z, "k_wire_events row bounds");
+    }
     if (per) {
         hipError_t a = hipMallocAsync(reinterpret_cast<void **>(&part), (size_t)(chunks * batch) * 24, st);
         if (a != hipSuccess) return hip_fail(a, "k_wire_events chunk counts");
@@ -653,7 +672,8 @@ extern "C" int pekf_wire_events_ext_dev(int64_t batch, int64_t n_frames, const v
     auto launch = [&](auto kernel) {
         hipLaunchKernelGGL(kernel, dim3(waves, per ? chunks : 1), dim3(kWireBlock), 0, st, batch, n_frames,
                            static_cast<const uint32_t *>(frames), e2_max, e3_max, static_cast<double4 *>(ev2),
-                           static_cast<double4 *>(ev3), first_t2, n2, n3, bad_frame, dev_error, per, part, part_t2);
+                           static_cast<double4 *>(ev3), first_t2, n2, n3, bad_frame, dev_error, per, part, part_t2,
+                           rows ? row_bounds : nullptr);
     };
     if (rows)
         launch(k_wire_events<true>);
@@ -677,5 +697,5 @@ extern "C" int pekf_wire_events_dev(int64_t batch, int64_t n_frames, const void 
                                     int64_t e3_max, void *ev2, void *ev3, int64_t *first_t2, int32_t *n2,
                                     int32_t *n3, int32_t *bad_frame, int *dev_error, void *stream) {
     return pekf_wire_events_ext_dev(batch, n_frames, frames, e2_max, e3_max, ev2, ev3, first_t2, n2, n3, bad_frame,
-                                    dev_error, 0u, stream);
+                                    dev_error, nullptr, 0u, stream);
 }

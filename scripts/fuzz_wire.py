@@ -122,7 +122,7 @@ def main(argv=None):
                                engine.DeviceBuffer(4 * K))
         errb = engine.DeviceBuffer(4).upload(np.zeros(1, np.int32))
         check(lib.pekf_wire_events_ext_dev(K, F, fb.ptr, F, F, ev2.ptr, ev3.ptr, t2b.ptr, n2b.ptr, n3b.ptr,
-                                           badb.ptr, errb.ptr, 1 if a.rows else 0, None))
+                                           badb.ptr, errb.ptr, None, 1 if a.rows else 0, None))
         check(lib.pekf_device_sync())
         d2, d3 = ev2.download((F, K, 4), np.float64), ev3.download((F, K, 4), np.float64)
         n2, n3 = n2b.download((K,), np.int32), n3b.download((K,), np.int32)

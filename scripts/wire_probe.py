@@ -12,6 +12,7 @@ import json
 import os
 import sys
 import time
+import types
 
 import numpy as np
 
@@ -56,7 +57,7 @@ def main():
     for _ in range(reps):
         e0.record(st.handle)
         check(lib.pekf_wire_events_ext_dev(K, F, fb.ptr, F if rows else 0, F if rows else E, ev2.ptr, ev3.ptr,
-                                           t2b.ptr, n2b.ptr, n3b.ptr, badb.ptr, errb.ptr, 1 if rows else 0,
+                                           t2b.ptr, n2b.ptr, n3b.ptr, badb.ptr, errb.ptr, None, 1 if rows else 0,
                                            st.handle))
         e1.record(st.handle)
         e1.sync()
@@ -109,22 +110,28 @@ def session(reps):
     ib, tib, rb = engine.DeviceBuffer(48 * K), engine.DeviceBuffer(8 * K), engine.DeviceBuffer(4 * K)
     cnt, refs = engine.DeviceBuffer(4 * K), engine.DeviceBuffer(48 * K)
     f = engine.BatchedEKF(K)
+    bounds = engine.DeviceBuffer(8)
     st = engine.Stream()
-    ev = [engine.Event() for _ in range(4)]
+    ev = [engine.Event() for _ in range(5)]
     rows = []
     for _ in range(reps):
         f.reset()
         ev[0].record(st.handle)
         check(lib.pekf_wire_events_ext_dev(K, F, fb.ptr, F, F, ev2.ptr, ev3.ptr, t2b.ptr, n2b.ptr, n3b.ptr, None,
-                                           errb.ptr, 1 if rows_mode else 0, st.handle))
+                                           errb.ptr, bounds.ptr if rows_mode else None, 1 if rows_mode else 0,
+                                           st.handle))
         ev[1].record(st.handle)
-        check(lib.pekf_frontend_init_ext_dev(K, F if rows_mode else E2, ev2.ptr, t2b.ptr, 100, ib.ptr, tib.ptr, None,
+        if rows_mode:  # (engine.run_wire_session reads the bounds the same way: one small copy, not timed)
+            r2, r3 = (int(v) for v in bounds.download((2,), np.int32, st.handle))
+        ev[4].record(st.handle)
+        check(lib.pekf_frontend_init_ext_dev(K, r2 if rows_mode else E2, ev2.ptr, t2b.ptr, 100, ib.ptr, tib.ptr, None,
                                              rb.ptr, EV_F64_EVENTS, st.handle))
         ev[2].record(st.handle)
-        f.run_events_async(ev3, F if rows_mode else E3, ib, tib, cnt, refs, 0.1, st.handle, flags=EV_F64_EVENTS)
+        ev3v = types.SimpleNamespace(ptr=ev3.ptr + 32 * K * (F - r3)) if rows_mode else ev3
+        f.run_events_async(ev3v, r3 if rows_mode else E3, ib, tib, cnt, refs, 0.1, st.handle, flags=EV_F64_EVENTS)
         ev[3].record(st.handle)
         ev[3].sync()
-        rows.append([ev[i].elapsed_ms(ev[i + 1]) for i in range(3)])
+        rows.append([ev[0].elapsed_ms(ev[1]), ev[4].elapsed_ms(ev[2]), ev[2].elapsed_ms(ev[3])])
     assert int(errb.download((1,), np.int32)[0]) == 0
     assert np.array_equal(n2b.download((K,), np.int32), np.tile(n2k, tile)) and np.all(n3b.download((K,), np.int32) == E3)
     assert rb.download((K,), np.int32).all()

@@ -260,7 +260,11 @@ def test_wire_events_frame_rows(eng, chunks, monkeypatch):
     F = fr.shape[0]
     a = eng.wire_events(fr)
     r = eng.wire_events(fr, frame_rows=True)
-    assert r["E2"] == r["E3"] == F
+    assert 0 < r["E2"] <= F and 0 < r["E3"] <= F and r["ev3_from"] == F - r["E3"]
+    rows2 = r["ev2"].download((F, K, 4), np.float64)[r["E2"]:]
+    rows3 = r["ev3"].download((F, K, 4), np.float64)[:r["ev3_from"]]
+    for rest in (rows2, rows3):  # the rows outside the bounds hold no message of any phone
+        assert np.all(np.ascontiguousarray(rest[..., 3]).view(np.uint64) == np.uint64(synth.EV64_NONE_W))
     assert np.array_equal(a["n2"], r["n2"]) and np.array_equal(a["n3"], r["n3"])
     assert _same(a["first_t2"].download((K,), np.int64), r["first_t2"].download((K,), np.int64))
     for plane, n in (("ev2", "n2"), ("ev3", "n3")):
@@ -281,7 +285,7 @@ def test_wire_events_frame_rows(eng, chunks, monkeypatch):
     bufs[0].upload(fb)
     bufs[7].upload(np.zeros(1, np.int32))
     check(lib.pekf_wire_events_ext_dev(Kb, Fb, bufs[0].ptr, Fb, Fb, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr,
-                                       bufs[4].ptr, bufs[5].ptr, bufs[6].ptr, bufs[7].ptr, 1, None))
+                                       bufs[4].ptr, bufs[5].ptr, bufs[6].ptr, bufs[7].ptr, None, 1, None))
     check(lib.pekf_device_sync())
     assert bufs[6].download((Kb,), np.int32).tolist() == [-1, 1]
     assert bufs[5].download((Kb,), np.int32)[1] == 1                  # the message before the refused frame
